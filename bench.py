@@ -1,0 +1,263 @@
+#!/usr/bin/env python3
+"""bench.py -- Mrays/s (closest-hit + shadow queries) of the MI355X render path.
+
+A "step" renders one whole frame of the workload: every rank renders its
+8x8 tiles (tile t -> rank t % N) through the C ABI of lib/librtgpu.so on
+torch's current stream, rank tile buffers are gathered to rank 0 with one
+RCCL gather (torch.distributed "nccl" backend = RCCL over xGMI), and rank 0
+assembles the PPM-order float image.  Scene image and octree are built and
+uploaded before timing (inputs resident in HBM).
+
+Default workload = config C5 (BASELINE.json): the deterministic synthetic
+10M-triangle sphere field at 3840x2160, octree traversal.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c5|c4|c3|c2|c1]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Prints ONE JSON line on rank 0 (plus progress on stderr).
+"""
+import argparse
+import gzip
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "raytracing-gpu_amd"))
+import rtgpu  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+NODE_BYTES = 32        # octree node record (host/rt_internal.h)
+TRI_BYTES = 48         # triangle record
+RAY_BYTES = 24         # origin + direction
+NORMAL_BYTES = 36      # 3 vertex normals of a closest-hit winner
+
+WORKLOADS = {
+    "c5": dict(kind="synthetic", accel="octree", W=3840, H=2160,
+               desc="C5 synthetic 10M-triangle sphere field (32x32 UV spheres x 9776 tris + ground, "
+                    "seed 0x5EED), 3840x2160, octree"),
+    "c4": dict(kind="svati", scene="car-on-road", accel="octree", W=3840, H=2160,
+               desc="C4 car-on-road.svati at 3840x2160, octree"),
+    "c3": dict(kind="svati", scene="island_smooth", accel="octree", W=1920, H=1080,
+               desc="C3 island_smooth.svati at 1920x1080, octree"),
+    "c2": dict(kind="svati", scene="spheres", accel="flat", W=1920, H=1080,
+               desc="C2 spheres.svati at 1920x1080, flat triangle list"),
+    "c1": dict(kind="svati", scene="cube", accel="flat", W=256, H=256,
+               desc="C1 cube.svati at 256x256, flat triangle list"),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def load_scene(wl, tmpdir):
+    if wl["kind"] == "synthetic":
+        return rtgpu.Scene.synthetic(32, 32, 9766, seed=0x5EED, width=wl["W"], height=wl["H"])
+    src = os.path.join(REPO, "tests", "golden", "scenes", wl["scene"] + ".svati.gz")
+    path = os.path.join(tmpdir, wl["scene"] + ".svati")
+    with gzip.open(src, "rb") as i, open(path, "wb") as o:
+        o.write(i.read())
+    s = rtgpu.Scene.load_svati(path)
+    s.set_size(wl["W"], wl["H"])
+    return s
+
+
+def cpu_baseline(scene, W, H, seconds, threads, gpu_img):
+    """The oracle (plain-C restatement of cpu/rt, brute force like the
+    reference) on a bounded deterministic pixel sample of the same frame."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as orc
+    orc.lib()
+    rng = np.random.default_rng(1234)
+    order = rng.permutation(W * H)
+    done = 0
+    closest = shadow = 0
+    mism = 0
+    batch = threads
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds and done < len(order):
+        idx = order[done:done + batch]
+        pix = np.stack([idx // W, idx % W], axis=1).astype(np.int32)
+        vals, cnt = orc.render(scene.ptr, W, H, pixels=pix, threads=threads)
+        closest += cnt["closest"]
+        shadow += cnt["shadow"]
+        if gpu_img is not None:
+            g = gpu_img[pix[:, 0], pix[:, 1]]
+            mism += int((g.view(np.uint32) != vals.view(np.uint32)).any(axis=1).sum())
+        done += len(idx)
+        el = time.perf_counter() - t0
+        if el < seconds / 4:
+            batch *= 2
+    el = time.perf_counter() - t0
+    return {
+        "value": (closest + shadow) / el / 1e6,
+        "unit": "Mrays/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{done} pixels ({closest} closest + {shadow} shadow queries) of the same "
+                  f"{W}x{H} frame, deterministic random order, {el:.1f} s, oracle/rt_oracle.c "
+                  f"(brute force like cpu/rt, -O2, {threads} threads)",
+        "sample_pixels_bitexact_vs_gpu": (mism == 0) if gpu_img is not None else None,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", default="c5", choices=sorted(WORKLOADS))
+    ap.add_argument("--accel", default=None, choices=["flat", "octree"])
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC summary (tools/pmc_traffic.py) to report as roofline.traffic")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    wl = dict(WORKLOADS[args.workload])
+    if args.accel:
+        wl["accel"] = args.accel
+    W, H = wl["W"], wl["H"]
+
+    with tempfile.TemporaryDirectory() as td:
+        t = time.perf_counter()
+        scene = load_scene(wl, td)
+    ntri = scene.triangle_count
+    ctx = rtgpu.Context(scene, wl["accel"], device=local)
+    info = ctx.info()
+    log(f"[rank {rank}] scene {ntri} triangles, accel {wl['accel']}: {info['tri_refs']} records, "
+        f"{info['nodes']} nodes, build {info['build_seconds']:.1f}s, setup {time.perf_counter()-t:.1f}s")
+    frame = scene.frame()
+    per = rtgpu.tile_buffer_floats(W, H, world)
+    tiles = torch.empty(per, dtype=torch.float32, device=dev)
+    gathered = torch.empty(per * world, dtype=torch.float32, device=dev) if rank == 0 else None
+    rgb = torch.empty(W * H * 3, dtype=torch.float32, device=dev) if rank == 0 else None
+    stream = torch.cuda.current_stream()
+    sh = stream.cuda_stream
+
+    # instrumented pass (untimed): algorithmic work per frame for the roofline
+    ctx.set_count_work(True)
+    ctx.render(frame, rank, world, tiles.data_ptr(), sh)
+    work = ctx.stats()
+    ctx.set_count_work(False)
+
+    k_start = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    k_end = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+
+    def step(i=None):
+        if i is not None:
+            k_start[i].record(stream)
+        ctx.render(frame, rank, world, tiles.data_ptr(), sh)
+        if i is not None:
+            k_end[i].record(stream)
+        if world > 1:
+            dist.gather(tiles, list(gathered.view(world, per)) if rank == 0 else None, dst=0)
+            if rank == 0:
+                ctx.assemble(frame, gathered.data_ptr(), world, rgb.data_ptr(), sh)
+        else:
+            ctx.assemble(frame, tiles.data_ptr(), 1, rgb.data_ptr(), sh)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    st = ctx.stats()
+    assert st["depth_overflow"] == 0
+    counts = torch.tensor([st["closest"], st["shadow"], st["hits"], st["pixels"],
+                           work["node_visits"], work["tri_tests"], work["hits"],
+                           work["closest"] + work["shadow"]], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(counts)
+    closest, shadow, hits, pixels, nodes, tris, whits, wq = [float(x) for x in counts.tolist()]
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in zip(k_start, k_end)) / args.steps
+    tt = torch.tensor([el, kern_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    el, kern_ms = tt.tolist()
+
+    queries = closest + shadow
+    value = queries * args.steps / el / 1e6
+    # algorithmic bytes of one render launch (per rank, averaged over ranks)
+    alg_bytes = (wq * RAY_BYTES + nodes * NODE_BYTES + tris * TRI_BYTES + whits * NORMAL_BYTES)
+    per_launch = alg_bytes / world
+    achieved = per_launch / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    if args.traffic_json and os.path.exists(args.traffic_json):
+        with open(args.traffic_json) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu:
+            img = rgb.view(H, W, 3).cpu().numpy()
+            log(f"[rank 0] cpu baseline: {args.cpu_seconds:.0f}s sample on {args.cpu_threads} threads")
+            cpu = cpu_baseline(scene, W, H, args.cpu_seconds, args.cpu_threads, img)
+        out = {
+            "metric": "Mrays/sec (primary+shadow) at 3840x2160",
+            "value": round(value, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic" if wl["kind"] == "synthetic" else f"reference scene {wl['scene']}.svati",
+            "config": {
+                "workload": wl["desc"],
+                "width": W, "height": H, "triangles": ntri, "accel": wl["accel"],
+                "parallelism": f"image tiles over {world} GPU(s) + RCCL gather" if world > 1
+                               else "1 GPU",
+                "queries_per_frame": {"closest": int(closest), "shadow": int(shadow),
+                                      "closest_hits": int(hits), "pixels": int(pixels)},
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5),
+                "traffic": traffic,
+                "kernel": "render_kernel<OCTREE>" if wl["accel"] == "octree" else "render_kernel<FLAT>",
+                "kernel_ms": round(kern_ms, 3),
+                "algorithmic_bytes_per_launch": int(per_launch),
+                "per_query_bytes": round(alg_bytes / wq, 1) if wq else None,
+                "node_visits_per_query": round(nodes / wq, 2) if wq else None,
+                "tri_tests_per_query": round(tris / wq, 2) if wq else None,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,138 @@
+/*
+ * rt_hip.h -- C ABI of the MI355X (gfx950) render path.
+ *
+ * Plain pointers and sizes only.  This is the drop-in boundary for the
+ * reference's hot path:
+ *
+ *   rt_raytrace()        replaces  void raytrace(const char *input, const char *output)
+ *                                  (/root/reference/cpu/headers/raytracer.h:4,
+ *                                   cpu/raytracer.c:79-136)
+ *   rt_hip_create()      replaces  struct scene *to_cuda(const struct scene *)
+ *                                  (/root/reference/gpu/headers/scene.h:52, gpu/scene.cu:224-352)
+ *                                  + create_octree() (gpu/partitioning/octree.h:39, octree.cu:362-411)
+ *   rt_hip_render()      replaces  render(...) (gpu/headers/raytracer.h:6, gpu/raytracer.cu:177-253)
+ *                                  with cpu/rt semantics: 2x2 SSAA in cpu order, float
+ *                                  channels, unbounded-by-design reflection recursion
+ *                                  (cpu/raytracer.c:19-77), collide/collide_dist/apply_light
+ *                                  (cpu/hit.c:72-109, cpu/light.c:33-100) on the device
+ *   rt_hip_assemble()    (new)     tile buffers of all ranks -> PPM-order float image
+ *   rt_raytrace_multi()  (new)     in-process 1..8 GPU render + RCCL gather over xGMI
+ *
+ * Threading: calls on distinct contexts may run concurrently on distinct host
+ * threads; one context is not re-entrant.  rt_hip_render is asynchronous on
+ * the given stream (NULL = the context's own stream); rt_hip_stats and
+ * rt_hip_render_image synchronise.
+ */
+#ifndef RT_HIP_H
+#define RT_HIP_H
+
+#include "rt_scene.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Camera frame, cpu/raytracer.c:82-86: u = norm(cam.u), v = norm(cam.v),
+ * C = pos + (u x v) * L with L = (float)(W / (2 tan(fov*pi/360))). */
+typedef struct rt_frame {
+  rt_vec3 u, v, C, position;
+  int width, height;
+} rt_frame;
+
+int rt_frame_from_camera(const rt_camera *cam, rt_frame *out);
+
+/* Acceleration structure selection. */
+enum { RT_ACCEL_FLAT = 0, RT_ACCEL_OCTREE = 1 };
+
+/* Per-render counters.  closest = closest-hit queries
+ * (collide() calls: camera + reflection rays), shadow = shadow queries
+ * (collide_dist() calls), camera = 4*pixels rendered.  node_visits and
+ * tri_tests are only filled by the instrumented kernel (rt_hip_set_count_work)
+ * and give the algorithmic bytes of the roofline. */
+typedef struct rt_stats {
+  unsigned long long closest, shadow, camera;
+  unsigned long long node_visits, tri_tests;
+  unsigned long long depth_overflow;   /* paths deeper than the term buffer (must be 0) */
+  unsigned long long zero_normal;      /* winners with an exactly-zero interpolated normal */
+  unsigned long long pixels;
+  unsigned long long hits;             /* closest-hit queries that hit geometry */
+} rt_stats;
+
+/* Sizes of the device-side scene image, for the roofline accounting. */
+typedef struct rt_accel_info {
+  unsigned long long triangles;        /* scene triangles                        */
+  unsigned long long tri_refs;         /* triangle records in traversal order    */
+  unsigned long long nodes;            /* octree nodes (0 for FLAT)              */
+  unsigned long long leaves;
+  unsigned long long max_depth;
+  unsigned long long tri_record_bytes; /* bytes per triangle record             */
+  unsigned long long node_record_bytes;
+  unsigned long long device_bytes;     /* total device memory of the scene image */
+  double build_seconds;                /* host build time (flatten + octree)     */
+} rt_accel_info;
+
+/* Host-only: build the acceleration structure rt_hip_create would build and
+ * report its sizes (no device needed). */
+int rt_accel_build_info(const rt_scene *scene, int accel, rt_accel_info *out);
+/* Host-only: build it and check its invariants (every triangle referenced by
+ * a leaf, every leaf box contains its triangles, every node box contains its
+ * children).  0 = valid, RT_EINVAL = violated (rt_last_error says where). */
+int rt_accel_validate(const rt_scene *scene, int accel);
+
+typedef struct rt_hip_ctx rt_hip_ctx;
+
+int rt_hip_device_count(int *n);
+
+/* Deep-copies the scene into device memory of `device` (flattened SoA
+ * triangle records, pre-normalised vertex normals, materials, lights) and
+ * builds the acceleration structure.  The caller keeps ownership of scene. */
+int rt_hip_create(int device, const rt_scene *scene, int accel, rt_hip_ctx **out);
+int rt_hip_accel_info(const rt_hip_ctx *ctx, rt_accel_info *out);
+void rt_hip_destroy(rt_hip_ctx *ctx);
+
+/* Image tiling: 8x8-pixel tiles in PPM order, tile t belongs to rank t % nranks.
+ * A rank's tile buffer holds rt_hip_tiles_per_rank() tiles, each 64 pixels
+ * x 3 floats (pixel p of a tile = row p/8, col p%8 inside the tile). */
+int rt_hip_tiles_per_rank(int width, int height, int nranks);
+size_t rt_hip_tile_buffer_floats(int width, int height, int nranks);
+
+/* Renders every tile of `rank` into d_tiles (device memory of the context's
+ * device, rt_hip_tile_buffer_floats() floats).  Asynchronous on `stream`
+ * (a hipStream_t; NULL = the context's stream). */
+int rt_hip_render(rt_hip_ctx *ctx, const rt_frame *frame, int rank, int nranks, float *d_tiles,
+                  void *stream);
+/* Waits for the last render and returns its counters. */
+int rt_hip_stats(rt_hip_ctx *ctx, rt_stats *out);
+/* Instrumented build: also count node visits and triangle tests (slower). */
+int rt_hip_set_count_work(rt_hip_ctx *ctx, int enable);
+
+/* d_gathered = nranks consecutive tile buffers (rank-major, as an RCCL gather
+ * delivers them); writes the PPM-order image (W*H*3 floats) to d_rgb. */
+int rt_hip_assemble(rt_hip_ctx *ctx, const rt_frame *frame, const float *d_gathered, int nranks,
+                    float *d_rgb, void *stream);
+
+/* Convenience: single-GPU render of the whole frame into host memory
+ * h_rgb (W*H*3 floats, PPM order); synchronous. */
+int rt_hip_render_image(rt_hip_ctx *ctx, const rt_frame *frame, float *h_rgb, rt_stats *stats);
+
+/* Device memory helpers so C callers need no HIP headers. */
+int rt_hip_malloc(int device, size_t bytes, void **d_ptr);
+int rt_hip_free(void *d_ptr);
+int rt_hip_memcpy_d2h(void *h_dst, const void *d_src, size_t bytes);
+int rt_hip_memcpy_h2d(void *d_dst, const void *h_src, size_t bytes);
+
+/* Drop-in for raytrace() (cpu/raytracer.c:79-136): parse, render on GPU 0,
+ * write the P3 PPM.  Returns an RT_E* code instead of exiting. */
+int rt_raytrace(const char *input, const char *output);
+
+/* Same with the frame tiled over `ngpus` devices of this node and gathered
+ * to device 0 with one RCCL gather over xGMI.  accel = RT_ACCEL_*.
+ * stats (optional) receives the summed counters; render_ms the wall time of
+ * render + gather. */
+int rt_raytrace_multi(const char *input, const char *output, int ngpus, int accel,
+                      rt_stats *stats, double *render_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,105 @@
+"""oracle.py -- TEST INFRASTRUCTURE ONLY.
+
+ctypes access to oracle/_build/liboracle.so, the plain-C restatement of the
+reference cpu/rt (oracle/rt_oracle.c).  Only tests/, __graft_entry__.smoke()
+and bench.py's cpu_baseline leg may import this; the product never does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "_build", "liboracle.so")
+
+
+class Counts(C.Structure):
+    _fields_ = [("closest", C.c_ulonglong), ("shadow", C.c_ulonglong),
+                ("max_depth", C.c_ulonglong)]
+
+
+class ColorS(C.Structure):
+    _fields_ = [("r", C.c_float), ("g", C.c_float), ("b", C.c_float)]
+
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE, "oracle"], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = C.CDLL(LIB)
+        L.oracle_load_svati.argtypes = [C.c_char_p, C.POINTER(C.c_void_p)]
+        L.oracle_load_svati.restype = C.c_int
+        L.oracle_free_scene.argtypes = [C.c_void_p]
+        L.oracle_free_scene.restype = None
+        L.oracle_render.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p,
+                                    C.POINTER(Counts)]
+        L.oracle_render.restype = C.c_int
+        L.oracle_init_color.argtypes = [C.c_float, C.c_float, C.c_float]
+        L.oracle_init_color.restype = ColorS
+        L.oracle_color_add.argtypes = [ColorS, ColorS]
+        L.oracle_color_add.restype = ColorS
+        L.oracle_color_mul.argtypes = [ColorS, C.c_float]
+        L.oracle_color_mul.restype = ColorS
+        L.oracle_color_mul2.argtypes = [ColorS, ColorS]
+        L.oracle_color_mul2.restype = ColorS
+        _lib = L
+    return _lib
+
+
+class OracleScene:
+    """A scene loaded by the oracle's own restated parser."""
+
+    def __init__(self, path):
+        p = C.c_void_p()
+        rc = lib().oracle_load_svati(os.fsencode(path), C.byref(p))
+        if rc != 0:
+            raise RuntimeError(f"oracle_load_svati({path}) = {rc}")
+        self.ptr = p
+
+    def set_size(self, width, height):
+        # struct or_scene: objects*, size_t, lights*, size_t, camera{int w, int h, ...}
+        cam = C.cast(self.ptr.value + 32, C.POINTER(C.c_int))
+        cam[0] = width
+        cam[1] = height
+
+    def __del__(self):
+        if getattr(self, "ptr", None) and _lib is not None:
+            _lib.oracle_free_scene(self.ptr)
+            self.ptr = None
+
+
+def render(scene_ptr, width, height, pixels=None, threads=0):
+    """Render with the oracle.  scene_ptr: an oracle scene or a product rt_scene*
+    (same C layout).  pixels: None (whole frame, PPM order) or an (N, 2) int
+    array of (row, col).  Returns (float32 array (N,3) or (H,W,3), counts dict)."""
+    if pixels is None:
+        n = width * height
+        pix_ptr = None
+    else:
+        pixels = np.ascontiguousarray(pixels, dtype=np.int32)
+        n = len(pixels)
+        pix_ptr = pixels.ctypes.data_as(C.c_void_p)
+    out = np.zeros((n, 3), np.float32)
+    cnt = Counts()
+    ptr = scene_ptr.ptr if isinstance(scene_ptr, OracleScene) else scene_ptr
+    if not isinstance(ptr, C.c_void_p):
+        ptr = C.cast(ptr, C.c_void_p)
+    rc = lib().oracle_render(ptr, pix_ptr, n, threads, out.ctypes.data_as(C.c_void_p),
+                             C.byref(cnt))
+    if rc != 0:
+        raise RuntimeError(f"oracle_render = {rc}")
+    counts = {"closest": cnt.closest, "shadow": cnt.shadow, "max_depth": cnt.max_depth}
+    if pixels is None:
+        out = out.reshape(height, width, 3)
+    return out, counts

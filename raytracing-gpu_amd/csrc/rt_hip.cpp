@@ -1,0 +1,410 @@
+// rt_hip.cpp -- host side of the C ABI declared in include/rt_hip.h.
+//
+// Owns device memory, streams and launches; the scene preparation (flatten,
+// octree) is host C (host/accel.c).  No CPU fallback: every entry point fails
+// with RT_ENODEV / RT_EHIP when the gfx950 device or the kernels are missing.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "rt_kernels.h"
+
+extern "C" {
+#include "../host/rt_internal.h"
+}
+
+#define HIP_TRY(expr)                                                                    \
+  do {                                                                                   \
+    hipError_t e_ = (expr);                                                              \
+    if (e_ != hipSuccess)                                                                \
+      return rt_set_error(RT_EHIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
+                          __LINE__);                                                     \
+  } while (0)
+
+struct rt_hip_ctx {
+  int device = 0;
+  int accel = RT_ACCEL_FLAT;
+  int count_work = 0;
+  int grid = 0;
+  hipStream_t stream = nullptr;
+  hipStream_t last_stream = nullptr;
+  float4* d_tri = nullptr;
+  float* d_nrm = nullptr;
+  float* d_mat = nullptr;
+  float* d_light = nullptr;
+  float4* d_node = nullptr;
+  uint32_t* d_counter = nullptr;
+  unsigned long long* d_stats = nullptr;
+  uint32_t nrec = 0, nlight = 0;
+  rt_accel_info info{};
+  float scene_c[3]{}, scene_r = 0;
+};
+
+static int tiles_x_of(int W) { return (W + 7) / 8; }
+static int tiles_y_of(int H) { return (H + 7) / 8; }
+
+extern "C" int rt_hip_tiles_per_rank(int width, int height, int nranks) {
+  if (width <= 0 || height <= 0 || nranks <= 0) return 0;
+  long nt = (long)tiles_x_of(width) * tiles_y_of(height);
+  return (int)((nt + nranks - 1) / nranks);
+}
+
+extern "C" size_t rt_hip_tile_buffer_floats(int width, int height, int nranks) {
+  return (size_t)rt_hip_tiles_per_rank(width, height, nranks) * 64 * 3;
+}
+
+extern "C" int rt_hip_device_count(int* n) {
+  if (!n) return rt_set_error(RT_EINVAL, "null argument");
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e != hipSuccess || c <= 0) {
+    *n = 0;
+    return rt_set_error(RT_ENODEV, "no HIP device (%s)", hipGetErrorString(e));
+  }
+  *n = c;
+  return RT_OK;
+}
+
+template <class T>
+static int upload(T** dst, const void* src, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  HIP_TRY(hipMalloc((void**)dst, bytes));
+  if (src) HIP_TRY(hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice));
+  return RT_OK;
+}
+
+extern "C" void rt_hip_destroy(rt_hip_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)hipFree(c->d_tri);
+  (void)hipFree(c->d_nrm);
+  (void)hipFree(c->d_mat);
+  (void)hipFree(c->d_light);
+  (void)hipFree(c->d_node);
+  (void)hipFree(c->d_counter);
+  (void)hipFree(c->d_stats);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+extern "C" int rt_hip_create(int device, const rt_scene* scene, int accel, rt_hip_ctx** out) {
+  if (!scene || !out) return rt_set_error(RT_EINVAL, "null argument");
+  if (accel != RT_ACCEL_FLAT && accel != RT_ACCEL_OCTREE)
+    return rt_set_error(RT_EINVAL, "unknown accel %d", accel);
+  int ndev = 0;
+  int rc = rt_hip_device_count(&ndev);
+  if (rc) return rc;
+  if (device < 0 || device >= ndev) return rt_set_error(RT_ENODEV, "device %d of %d", device, ndev);
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return rt_set_error(RT_ENODEV, "device %d is %s, kernels are built for gfx950", device,
+                        prop.gcnArchName);
+  HIP_TRY(hipSetDevice(device));
+
+  auto t0 = std::chrono::steady_clock::now();
+  rt_flat_scene fs;
+  rc = rt_flatten(scene, accel, &fs);
+  if (rc) return rc;
+  auto t1 = std::chrono::steady_clock::now();
+
+  rt_hip_ctx* c = new rt_hip_ctx();
+  c->device = device;
+  c->accel = accel;
+  c->nrec = (uint32_t)fs.nrec;
+  c->nlight = (uint32_t)fs.nlight;
+  size_t bytes_tri = fs.nrec * RT_TRI_FLOATS * sizeof(float);
+  size_t bytes_nrm = fs.ntri * 9 * sizeof(float);
+  size_t bytes_mat = fs.nobj * RT_MAT_FLOATS * sizeof(float);
+  size_t bytes_light = fs.nlight * RT_LIGHT_FLOATS * sizeof(float);
+  size_t bytes_node = fs.nnode * RT_NODE_FLOATS * sizeof(float);
+  rc = upload(&c->d_tri, fs.tri, bytes_tri);
+  if (!rc) rc = upload(&c->d_nrm, fs.nrm, bytes_nrm);
+  if (!rc) rc = upload(&c->d_mat, fs.mat, bytes_mat);
+  if (!rc) rc = upload(&c->d_light, fs.light, bytes_light);
+  if (!rc && fs.nnode) rc = upload(&c->d_node, fs.node, bytes_node);
+  if (!rc) rc = upload(&c->d_counter, nullptr, 64);
+  if (!rc) rc = upload(&c->d_stats, nullptr, RT_NSTATS * sizeof(unsigned long long));
+  if (!rc && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+    rc = rt_set_error(RT_EHIP, "hipStreamCreate");
+  for (int a = 0; a < 3; a++) {
+    float lo = fs.ntri ? fs.scene_lo[a] : 0.0f, hi = fs.ntri ? fs.scene_hi[a] : 0.0f;
+    c->scene_c[a] = 0.5f * (lo + hi);
+    c->scene_r = std::fmax(c->scene_r, 0.5f * (hi - lo));
+  }
+  c->info.triangles = fs.ntri;
+  c->info.tri_refs = fs.nrec;
+  c->info.nodes = fs.nnode;
+  c->info.leaves = fs.leaves;
+  c->info.max_depth = fs.max_depth;
+  c->info.tri_record_bytes = RT_TRI_FLOATS * sizeof(float);
+  c->info.node_record_bytes = RT_NODE_FLOATS * sizeof(float);
+  c->info.device_bytes = bytes_tri + bytes_nrm + bytes_mat + bytes_light + bytes_node;
+  c->info.build_seconds = std::chrono::duration<double>(t1 - t0).count();
+  rt_flat_free(&fs);
+  if (rc) {
+    rt_hip_destroy(c);
+    return rc;
+  }
+  // persistent grid: enough one-wave workgroups to fill every SIMD
+  c->grid = prop.multiProcessorCount * 16;
+  *out = c;
+  return RT_OK;
+}
+
+extern "C" int rt_hip_accel_info(const rt_hip_ctx* c, rt_accel_info* out) {
+  if (!c || !out) return rt_set_error(RT_EINVAL, "null argument");
+  *out = c->info;
+  return RT_OK;
+}
+
+extern "C" int rt_hip_set_count_work(rt_hip_ctx* c, int enable) {
+  if (!c) return rt_set_error(RT_EINVAL, "null context");
+  c->count_work = enable ? 1 : 0;
+  return RT_OK;
+}
+
+extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nranks,
+                             float* d_tiles, void* stream) {
+  if (!c || !f || !d_tiles) return rt_set_error(RT_EINVAL, "null argument");
+  if (nranks <= 0 || rank < 0 || rank >= nranks)
+    return rt_set_error(RT_EINVAL, "rank %d of %d", rank, nranks);
+  if (f->width <= 0 || f->height <= 0) return rt_set_error(RT_EINVAL, "empty frame");
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  KParams p;
+  std::memset(&p, 0, sizeof p);
+  p.tri = c->d_tri;
+  p.nrm = c->d_nrm;
+  p.mat = c->d_mat;
+  p.light = c->d_light;
+  p.node = c->d_node;
+  p.nrec = c->nrec;
+  p.nlight = c->nlight;
+  p.u = rt::f3{f->u.x, f->u.y, f->u.z};
+  p.v = rt::f3{f->v.x, f->v.y, f->v.z};
+  p.C = rt::f3{f->C.x, f->C.y, f->C.z};
+  p.pos = rt::f3{f->position.x, f->position.y, f->position.z};
+  p.W = f->width;
+  p.H = f->height;
+  p.tiles_x = tiles_x_of(f->width);
+  p.ntiles_total = tiles_x_of(f->width) * tiles_y_of(f->height);
+  p.rank = rank;
+  p.nranks = nranks;
+  p.ntiles_local = (p.ntiles_total - rank + nranks - 1) / nranks;
+  p.out = d_tiles;
+  p.tile_counter = c->d_counter;
+  p.stats = c->d_stats;
+  p.scene_c = rt::f3{c->scene_c[0], c->scene_c[1], c->scene_c[2]};
+  p.scene_r = c->scene_r;
+  // culling slack: 256 ulps of the origin-to-geometry distance
+  p.eps_rel = 256.0f * 5.9604645e-8f;
+  p.eps_abs = 1e-6f;
+  if (c->accel == RT_ACCEL_OCTREE && !c->d_node) {
+    // empty scene: nothing to traverse, the FLAT kernel with 0 records is exact
+    HIP_TRY(hipMemsetAsync(c->d_counter, 0, 64, s));
+    HIP_TRY(hipMemsetAsync(c->d_stats, 0, RT_NSTATS * sizeof(unsigned long long), s));
+    HIP_TRY(rt_launch_render(&p, RT_ACCEL_FLAT_D, c->count_work, c->grid, s));
+  } else {
+    HIP_TRY(hipMemsetAsync(c->d_counter, 0, 64, s));
+    HIP_TRY(hipMemsetAsync(c->d_stats, 0, RT_NSTATS * sizeof(unsigned long long), s));
+    HIP_TRY(rt_launch_render(&p, c->accel, c->count_work, c->grid, s));
+  }
+  c->last_stream = s;
+  return RT_OK;
+}
+
+extern "C" int rt_hip_stats(rt_hip_ctx* c, rt_stats* out) {
+  if (!c || !out) return rt_set_error(RT_EINVAL, "null argument");
+  HIP_TRY(hipSetDevice(c->device));
+  unsigned long long h[RT_NSTATS];
+  hipStream_t s = c->last_stream ? c->last_stream : c->stream;
+  HIP_TRY(hipMemcpyAsync(h, c->d_stats, sizeof h, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  std::memset(out, 0, sizeof *out);
+  out->closest = h[0];
+  out->shadow = h[1];
+  out->pixels = h[2];
+  out->camera = 4 * h[2];
+  out->node_visits = h[3];
+  out->tri_tests = h[4];
+  out->depth_overflow = h[5];
+  out->zero_normal = h[6];
+  out->hits = h[7];
+  if (out->depth_overflow)
+    return rt_set_error(RT_EDEPTH, "%llu paths overflowed the depth/stack buffers",
+                        out->depth_overflow);
+  return RT_OK;
+}
+
+extern "C" int rt_hip_assemble(rt_hip_ctx* c, const rt_frame* f, const float* d_gathered,
+                               int nranks, float* d_rgb, void* stream) {
+  if (!c || !f || !d_gathered || !d_rgb || nranks <= 0)
+    return rt_set_error(RT_EINVAL, "bad argument");
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  int tx = tiles_x_of(f->width);
+  int nt = tx * tiles_y_of(f->height);
+  HIP_TRY(rt_launch_assemble(d_gathered, d_rgb, f->width, f->height, tx, nt, nranks,
+                             rt_hip_tiles_per_rank(f->width, f->height, nranks), s));
+  return RT_OK;
+}
+
+extern "C" int rt_hip_render_image(rt_hip_ctx* c, const rt_frame* f, float* h_rgb, rt_stats* st) {
+  if (!c || !f || !h_rgb) return rt_set_error(RT_EINVAL, "null argument");
+  HIP_TRY(hipSetDevice(c->device));
+  size_t nt = rt_hip_tile_buffer_floats(f->width, f->height, 1);
+  size_t npx = (size_t)f->width * f->height;
+  float *d_tiles = nullptr, *d_rgb = nullptr;
+  HIP_TRY(hipMalloc((void**)&d_tiles, nt * sizeof(float)));
+  if (hipMalloc((void**)&d_rgb, npx * 3 * sizeof(float)) != hipSuccess) {
+    (void)hipFree(d_tiles);
+    return rt_set_error(RT_EHIP, "hipMalloc image");
+  }
+  int rc = rt_hip_render(c, f, 0, 1, d_tiles, nullptr);
+  if (!rc) rc = rt_hip_assemble(c, f, d_tiles, 1, d_rgb, nullptr);
+  if (!rc && hipMemcpyAsync(h_rgb, d_rgb, npx * 3 * sizeof(float), hipMemcpyDeviceToHost,
+                            c->stream) != hipSuccess)
+    rc = rt_set_error(RT_EHIP, "D2H image");
+  rt_stats tmp;
+  if (!rc) rc = rt_hip_stats(c, st ? st : &tmp);
+  (void)hipFree(d_tiles);
+  (void)hipFree(d_rgb);
+  return rc;
+}
+
+extern "C" int rt_hip_malloc(int device, size_t bytes, void** d_ptr) {
+  if (!d_ptr) return rt_set_error(RT_EINVAL, "null argument");
+  HIP_TRY(hipSetDevice(device));
+  HIP_TRY(hipMalloc(d_ptr, bytes ? bytes : 16));
+  return RT_OK;
+}
+extern "C" int rt_hip_free(void* d_ptr) {
+  HIP_TRY(hipFree(d_ptr));
+  return RT_OK;
+}
+extern "C" int rt_hip_memcpy_d2h(void* dst, const void* src, size_t bytes) {
+  HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+  return RT_OK;
+}
+extern "C" int rt_hip_memcpy_h2d(void* dst, const void* src, size_t bytes) {
+  HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+  return RT_OK;
+}
+
+// ------------------------------------------------------------ drop-in entry
+
+static int choose_accel(const rt_scene* s) {
+  // brute force is exact and cheapest for tiny scenes; the octree otherwise
+  return rt_scene_triangle_count(s) <= 64 ? RT_ACCEL_FLAT : RT_ACCEL_OCTREE;
+}
+
+extern "C" int rt_raytrace(const char* input, const char* output) {
+  return rt_raytrace_multi(input, output, 1, -1, nullptr, nullptr);
+}
+
+#define NCCL_TRY(expr)                                                                 \
+  do {                                                                                 \
+    ncclResult_t r_ = (expr);                                                          \
+    if (r_ != ncclSuccess) {                                                           \
+      rc = rt_set_error(RT_ERCCL, "%s: %s", #expr, ncclGetErrorString(r_));            \
+      goto out;                                                                        \
+    }                                                                                  \
+  } while (0)
+
+extern "C" int rt_raytrace_multi(const char* input, const char* output, int ngpus, int accel,
+                                 rt_stats* stats, double* render_ms) {
+  if (!input || !output || ngpus < 1 || ngpus > 64) return rt_set_error(RT_EINVAL, "bad argument");
+  rt_scene* scene = nullptr;
+  int rc = rt_scene_load_svati(input, &scene);
+  if (rc) return rc;
+  rt_frame f;
+  rc = rt_frame_from_camera(&scene->camera, &f);
+  if (rc) {
+    rt_scene_free(scene);
+    return rc;
+  }
+  if (accel < 0) accel = choose_accel(scene);
+  int ndev = 0;
+  rc = rt_hip_device_count(&ndev);
+  if (!rc && ngpus > ndev) rc = rt_set_error(RT_ENODEV, "%d GPUs requested, %d present", ngpus, ndev);
+  std::vector<rt_hip_ctx*> ctx(ngpus, nullptr);
+  std::vector<float*> d_tiles(ngpus, nullptr);
+  std::vector<ncclComm_t> comms(ngpus, nullptr);
+  float* d_gather = nullptr;
+  float* d_rgb = nullptr;
+  std::vector<float> h_rgb;
+  size_t tile_floats = rt_hip_tile_buffer_floats(f.width, f.height, ngpus);
+  size_t npx = (size_t)f.width * f.height;
+  std::chrono::steady_clock::time_point t0, t1;
+  rt_stats sum{};
+  for (int g = 0; !rc && g < ngpus; g++) {
+    rc = rt_hip_create(g, scene, accel, &ctx[g]);
+    if (!rc) rc = rt_hip_malloc(g, tile_floats * sizeof(float), (void**)&d_tiles[g]);
+  }
+  if (!rc) rc = rt_hip_malloc(0, tile_floats * ngpus * sizeof(float), (void**)&d_gather);
+  if (!rc) rc = rt_hip_malloc(0, npx * 3 * sizeof(float), (void**)&d_rgb);
+  if (rc) goto out;
+  if (ngpus > 1) {
+    std::vector<int> devs(ngpus);
+    for (int g = 0; g < ngpus; g++) devs[g] = g;
+    NCCL_TRY(ncclCommInitAll(comms.data(), ngpus, devs.data()));
+  }
+  for (int g = 0; g < ngpus; g++) {
+    (void)hipSetDevice(g);
+    (void)hipDeviceSynchronize();
+  }
+  t0 = std::chrono::steady_clock::now();
+  for (int g = 0; !rc && g < ngpus; g++) rc = rt_hip_render(ctx[g], &f, g, ngpus, d_tiles[g], nullptr);
+  if (rc) goto out;
+  if (ngpus > 1) {
+    // one gather of every rank's tile buffer to device 0 over xGMI
+    NCCL_TRY(ncclGroupStart());
+    for (int g = 0; g < ngpus; g++) {
+      (void)hipSetDevice(g);
+      NCCL_TRY(ncclGather(d_tiles[g], g == 0 ? d_gather : nullptr, tile_floats, ncclFloat, 0,
+                          comms[g], ctx[g]->stream));
+    }
+    NCCL_TRY(ncclGroupEnd());
+    rc = rt_hip_assemble(ctx[0], &f, d_gather, ngpus, d_rgb, nullptr);
+  } else {
+    rc = rt_hip_assemble(ctx[0], &f, d_tiles[0], 1, d_rgb, nullptr);
+  }
+  if (rc) goto out;
+  for (int g = 0; !rc && g < ngpus; g++) {
+    rt_stats st;
+    rc = rt_hip_stats(ctx[g], &st);
+    sum.closest += st.closest;
+    sum.shadow += st.shadow;
+    sum.camera += st.camera;
+    sum.pixels += st.pixels;
+    sum.node_visits += st.node_visits;
+    sum.tri_tests += st.tri_tests;
+    sum.depth_overflow += st.depth_overflow;
+    sum.zero_normal += st.zero_normal;
+    sum.hits += st.hits;
+  }
+  t1 = std::chrono::steady_clock::now();
+  if (rc) goto out;
+  h_rgb.resize(npx * 3);
+  rc = rt_hip_memcpy_d2h(h_rgb.data(), d_rgb, npx * 3 * sizeof(float));
+  if (!rc) rc = rt_ppm_write(output, f.width, f.height, h_rgb.data());
+  if (stats) *stats = sum;
+  if (render_ms) *render_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+out:
+  for (int g = 0; g < ngpus; g++) {
+    if (comms[g]) ncclCommDestroy(comms[g]);
+    if (d_tiles[g]) rt_hip_free(d_tiles[g]);
+    rt_hip_destroy(ctx[g]);
+  }
+  if (d_gather) rt_hip_free(d_gather);
+  if (d_rgb) rt_hip_free(d_rgb);
+  rt_scene_free(scene);
+  return rc;
+}

@@ -1,0 +1,454 @@
+// rt_render.hip -- the MI355X (gfx950) render kernels.
+//
+// One lane renders one pixel: the 4 supersamples of cpu/raytracer.c:55-69 in
+// the reference order, each a path of closest-hit queries (cpu/raytracer.c:19-34)
+// with Phong + shadow-ray shading at every hit (cpu/light.c:33-100).  A wave
+// owns an 8x8 pixel tile; waves are persistent and pull tiles from an atomic
+// counter, so the irregular per-tile cost balances across the 256 CUs.
+//
+// Bit-parity with cpu/rt:
+//   * -ffp-contract=off, IEEE div/sqrt, f64 sqrt/pow where the reference uses them;
+//   * closest hit = lexicographic min of (new_dist, prim) over hits with
+//     new_dist > 0.01 (prim = object-major, LIFO-triangle index);
+//   * shadow = any hit with new_dist > 0.01 (early exit is exact);
+//   * reflection terms are buffered and summed deepest-first.
+//
+// Acceleration: FLAT tests every triangle record (the reference's brute
+// force, cpu/hit.c:72-109) with wave-uniform scalar loads of each record;
+// OCTREE walks the octree built by host/accel.c with a per-lane stack,
+// front-to-back child order and conservative distance culling.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rt_device.h"
+#include "rt_kernels.h"
+
+namespace rt {
+
+static constexpr float kEps = 0.0000001f;  // cpu/hit.c:7 (float)1e-7
+static constexpr int kMaxDepth = RT_MAX_DEPTH;
+static constexpr int kStack = 128;
+
+__device__ __forceinline__ f3 ld3(const float* p) { return f3{p[0], p[1], p[2]}; }
+
+// Moller-Trumbore, cpu/hit.c:15-33 with e1/e2 precomputed (same bits).
+__device__ __forceinline__ bool mt_test(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float& t, float& u,
+                                        float& v) {
+  f3 h = cross(d, e2);
+  float a = dot(e1, h);
+  if (a > -kEps && a < kEps) return false;
+  float f = 1.0f / a;
+  f3 s = sub(o, v0);
+  u = f * dot(s, h);
+  if (u < 0.0f || u > 1.0f) return false;
+  f3 q = cross(s, e1);
+  v = f * dot(d, q);
+  if (v < 0.0f || u + v > 1.0f) return false;
+  t = f * dot(e2, q);
+  return t > kEps;
+}
+
+struct Ray {
+  f3 o, d;     // origin, direction (as the reference holds them)
+  f3 nd;       // normalize(d)
+  float dlen;  // length(d)
+  float eps;   // culling slack (world units) for this origin
+};
+
+__device__ __forceinline__ Ray make_ray(const KParams& p, f3 o, f3 d) {
+  Ray r;
+  r.o = o;
+  r.d = d;
+  r.dlen = length(d);
+  r.nd = f3{d.x / r.dlen, d.y / r.dlen, d.z / r.dlen};
+  float m = fmaxf(fabsf(o.x - p.scene_c.x), fmaxf(fabsf(o.y - p.scene_c.y), fabsf(o.z - p.scene_c.z)));
+  r.eps = p.eps_rel * (m + p.scene_r) + p.eps_abs;
+  return r;
+}
+
+// new_dist = |(o + nd * (t*|d|)) - o| (cpu/hit.c:35-37,58); returns the hit point too.
+__device__ __forceinline__ float hit_dist(const Ray& r, float t, f3& out) {
+  out = add(r.o, scale(r.nd, t * r.dlen));
+  return length(sub(out, r.o));
+}
+
+struct Best {
+  float dist;  // +inf = none
+  uint32_t prim, obj;
+  float u, v;
+  f3 pt;
+};
+
+__device__ __forceinline__ void consider(const Ray& r, const float4& q0, const float4& q1,
+                                         const float4& q2, Best& b) {
+  float t, u, v;
+  if (!mt_test(r.o, r.d, f3{q0.x, q0.y, q0.z}, f3{q0.w, q1.x, q1.y}, f3{q1.z, q1.w, q2.x}, t, u,
+               v))
+    return;
+  f3 out;
+  float nd = hit_dist(r, t, out);
+  if (!((double)nd > 0.01)) return;
+  uint32_t prim = __float_as_uint(q2.y);
+  if (nd < b.dist || (nd == b.dist && prim < b.prim)) {
+    b.dist = nd;
+    b.prim = prim;
+    b.obj = __float_as_uint(q2.z);
+    b.u = u;
+    b.v = v;
+    b.pt = out;
+  }
+}
+
+__device__ __forceinline__ bool any_hit_rec(const Ray& r, const float4& q0, const float4& q1,
+                                            const float4& q2) {
+  float t, u, v;
+  if (!mt_test(r.o, r.d, f3{q0.x, q0.y, q0.z}, f3{q0.w, q1.x, q1.y}, f3{q1.z, q1.w, q2.x}, t, u,
+               v))
+    return false;
+  f3 out;
+  return (double)hit_dist(r, t, out) > 0.01;
+}
+
+// ---------------------------------------------------------------- FLAT
+template <bool COUNT>
+__device__ void flat_closest(const KParams& p, const Ray& r, Best& b, WorkCount& wc) {
+  const float4* __restrict__ tri = p.tri;
+  const uint32_t n = p.nrec;
+  for (uint32_t i = 0; i < n; i++) {
+    float4 q0 = tri[3 * i], q1 = tri[3 * i + 1], q2 = tri[3 * i + 2];
+    consider(r, q0, q1, q2, b);
+  }
+  if (COUNT) wc.tris += n;
+}
+
+template <bool COUNT>
+__device__ bool flat_any(const KParams& p, const Ray& r, WorkCount& wc) {
+  const float4* __restrict__ tri = p.tri;
+  const uint32_t n = p.nrec;
+  for (uint32_t i = 0; i < n; i++) {
+    if (COUNT) wc.tris++;
+    if (any_hit_rec(r, tri[3 * i], tri[3 * i + 1], tri[3 * i + 2])) return true;
+  }
+  return false;
+}
+
+// -------------------------------------------------------------- OCTREE
+// Slab test against a box grown by r.eps; returns entry parameter (>= 0 side
+// not enforced) or +inf on miss.
+__device__ __forceinline__ float box_enter(const Ray& r, f3 inv, float4 lo, float4 hi) {
+  float tx0 = (lo.x - r.eps - r.o.x) * inv.x, tx1 = (hi.x + r.eps - r.o.x) * inv.x;
+  float ty0 = (lo.y - r.eps - r.o.y) * inv.y, ty1 = (hi.y + r.eps - r.o.y) * inv.y;
+  float tz0 = (lo.z - r.eps - r.o.z) * inv.z, tz1 = (hi.z + r.eps - r.o.z) * inv.z;
+  float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
+  float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+  // slack on the parametric interval too (inv may be huge)
+  float slack = 1e-5f * fmaxf(fabsf(tmin), fabsf(tmax));
+  if (tmax + slack < fmaxf(tmin, 0.0f) - slack) return __builtin_inff();
+  return tmin;
+}
+
+__device__ __forceinline__ f3 inv_dir(f3 d) { return f3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z}; }
+
+template <bool COUNT>
+__device__ void oct_closest(const KParams& p, const Ray& r, Best& b, WorkCount& wc) {
+  const float4* __restrict__ node = p.node;
+  const float4* __restrict__ tri = p.tri;
+  f3 inv = inv_dir(r.d);
+  uint32_t stk_n[kStack];
+  float stk_t[kStack];
+  int sp = 0;
+  {
+    float t0 = box_enter(r, inv, node[0], node[1]);
+    if (t0 != __builtin_inff()) {
+      stk_n[0] = 0;
+      stk_t[0] = t0;
+      sp = 1;
+    }
+  }
+  while (sp > 0) {
+    --sp;
+    uint32_t ni = stk_n[sp];
+    float tn = stk_t[sp];
+    // prune: the node starts beyond the current best (with slack)
+    if (b.dist != __builtin_inff() &&
+        tn * r.dlen > b.dist + b.dist * 1e-5f + 2.0f * r.eps)
+      continue;
+    float4 lo = node[2 * ni], hi = node[2 * ni + 1];
+    uint32_t first = __float_as_uint(lo.w), cnt = __float_as_uint(hi.w);
+    if (COUNT) wc.nodes++;
+    if (cnt & RT_LEAF_FLAG_D) {
+      cnt &= ~RT_LEAF_FLAG_D;
+      for (uint32_t k = 0; k < cnt; k++) {
+        const float4* q = tri + 3 * (size_t)(first + k);
+        consider(r, q[0], q[1], q[2], b);
+      }
+      if (COUNT) wc.tris += cnt;
+    } else {
+      // test the children, push hits far-to-near so the nearest pops first
+      uint32_t cidx[8];
+      float ct[8];
+      int nh = 0;
+      for (uint32_t c = 0; c < cnt; c++) {
+        uint32_t ci = first + c;
+        float t0 = box_enter(r, inv, node[2 * ci], node[2 * ci + 1]);
+        if (t0 == __builtin_inff()) continue;
+        if (b.dist != __builtin_inff() && t0 * r.dlen > b.dist + b.dist * 1e-5f + 2.0f * r.eps)
+          continue;
+        // insertion sort, descending t
+        int j = nh++;
+        while (j > 0 && ct[j - 1] < t0) {
+          ct[j] = ct[j - 1];
+          cidx[j] = cidx[j - 1];
+          --j;
+        }
+        ct[j] = t0;
+        cidx[j] = ci;
+      }
+      for (int j = 0; j < nh; j++) {
+        if (sp < kStack) {
+          stk_n[sp] = cidx[j];
+          stk_t[sp] = ct[j];
+          ++sp;
+        } else {
+          wc.overflow++;
+        }
+      }
+    }
+  }
+}
+
+template <bool COUNT>
+__device__ bool oct_any(const KParams& p, const Ray& r, WorkCount& wc) {
+  const float4* __restrict__ node = p.node;
+  const float4* __restrict__ tri = p.tri;
+  f3 inv = inv_dir(r.d);
+  uint32_t stk[kStack];
+  int sp = 0;
+  if (box_enter(r, inv, node[0], node[1]) != __builtin_inff()) stk[sp++] = 0;
+  while (sp > 0) {
+    uint32_t ni = stk[--sp];
+    float4 lo = node[2 * ni], hi = node[2 * ni + 1];
+    uint32_t first = __float_as_uint(lo.w), cnt = __float_as_uint(hi.w);
+    if (COUNT) wc.nodes++;
+    if (cnt & RT_LEAF_FLAG_D) {
+      cnt &= ~RT_LEAF_FLAG_D;
+      for (uint32_t k = 0; k < cnt; k++) {
+        const float4* q = tri + 3 * (size_t)(first + k);
+        if (COUNT) wc.tris++;
+        if (any_hit_rec(r, q[0], q[1], q[2])) return true;
+      }
+    } else {
+      for (uint32_t c = 0; c < cnt; c++) {
+        uint32_t ci = first + c;
+        if (box_enter(r, inv, node[2 * ci], node[2 * ci + 1]) == __builtin_inff()) continue;
+        if (sp < kStack)
+          stk[sp++] = ci;
+        else
+          wc.overflow++;
+      }
+    }
+  }
+  return false;
+}
+
+template <int ACCEL, bool COUNT>
+__device__ __forceinline__ void closest(const KParams& p, const Ray& r, Best& b, WorkCount& wc) {
+  if (ACCEL == RT_ACCEL_FLAT_D)
+    flat_closest<COUNT>(p, r, b, wc);
+  else
+    oct_closest<COUNT>(p, r, b, wc);
+}
+
+template <int ACCEL, bool COUNT>
+__device__ __forceinline__ bool shadowed(const KParams& p, f3 o, f3 d, WorkCount& wc) {
+  wc.shadow++;
+  Ray r = make_ray(p, o, d);
+  if (ACCEL == RT_ACCEL_FLAT_D) return flat_any<COUNT>(p, r, wc);
+  return oct_any<COUNT>(p, r, wc);
+}
+
+// cpu/light.c:7-22
+__device__ __forceinline__ col specular(col tmp, f3 inc_o, f3 inc_d, f3 P, f3 N, const float* m) {
+  col k = init_color(m[6], m[7], m[8]);
+  f3 V = sub(inc_o, P);
+  f3 R = sub(inc_d, scale(N, 2.0f * dot(N, inc_d)));
+  R = normalize(R);
+  V = normalize(V);
+  float ls = (float)pow(fmax((double)dot(R, V), 0.0), (double)m[9]);
+  k = color_mul(k, ls);
+  return color_add(tmp, k);
+}
+
+// cpu/light.c:33-100; P = hit point, N = interpolated (unnormalised) normal
+template <int ACCEL, bool COUNT>
+__device__ col apply_light(const KParams& p, const float* m, f3 P, f3 N, WorkCount& wc) {
+  col acc = init_color(0.0f, 0.0f, 0.0f);
+  for (uint32_t li = 0; li < p.nlight; li++) {
+    const float* L = p.light + RT_LIGHT_FLOATS_D * li;
+    uint32_t type = __float_as_uint(L[0]);
+    col lc = init_color(L[1], L[2], L[3]);
+    f3 lv = f3{L[4], L[5], L[6]};
+    if (type == 0) {  // AMBIENT
+      col tmp = color_mul2(lc, init_color(m[0], m[1], m[2]));
+      acc = color_add(acc, tmp);
+    } else if (type == 1) {  // DIRECTIONAL
+      f3 Ldir = scale(lv, -1.0f);
+      if (shadowed<ACCEL, COUNT>(p, P, Ldir, wc)) continue;
+      col tmp = color_mul2(lc, init_color(m[3], m[4], m[5]));
+      tmp = color_mul(tmp, dot(Ldir, N));
+      f3 inc_o = add(P, scale(lv, -10.0f));
+      tmp = specular(tmp, inc_o, lv, P, N, m);
+      acc = color_add(acc, tmp);
+    } else if (type == 2) {  // POINT: "L" is minus the light position
+      f3 Lp = scale(lv, -1.0f);
+      f3 Nf = N;
+      if (dot(Lp, Nf) < 0.0f) Nf = scale(Nf, -1.0f);
+      f3 to_l = sub(lv, P);
+      float dist = length(sub(lv, P));
+      if (shadowed<ACCEL, COUNT>(p, P, to_l, wc)) continue;
+      col tmp = color_mul2(lc, init_color(m[3], m[4], m[5]));
+      tmp = color_mul(tmp, dot(Lp, Nf) * 1.0f / dist);
+      f3 inc_o = add(P, scale(to_l, -10.0f));
+      tmp = specular(tmp, inc_o, to_l, P, N, m);
+      acc = color_add(acc, tmp);
+    }
+  }
+  return acc;
+}
+
+// One camera sample: cpu/raytracer.c:19-34 unrolled into a loop; local terms
+// buffered and folded deepest-first.
+template <int ACCEL, bool COUNT>
+__device__ col trace_path(const KParams& p, f3 o, f3 d, WorkCount& wc) {
+  col terms[kMaxDepth];
+  int depth = 0;
+  float coef = 1.0f;
+  for (;;) {
+    if ((double)coef < 0.01) break;
+    wc.closest++;
+    Ray r = make_ray(p, o, d);
+    Best b;
+    b.dist = __builtin_inff();
+    b.prim = 0xffffffffu;
+    closest<ACCEL, COUNT>(p, r, b, wc);
+    if (b.dist == __builtin_inff()) break;
+    wc.hits++;
+    const float* nm = p.nrm + 9 * (size_t)b.prim;
+    float w0 = 1.0f - b.u - b.v;
+    f3 N = add(add(scale(ld3(nm), w0), scale(ld3(nm + 3), b.u)), scale(ld3(nm + 6), b.v));
+    if (is_zero(N)) {  // cpu/hit.c:79 would skip this object; see DESIGN.md
+      wc.zero_normal++;
+      break;
+    }
+    const float* m = p.mat + RT_MAT_FLOATS_D * b.obj;
+    col local = apply_light<ACCEL, COUNT>(p, m, b.pt, N, wc);
+    if (depth == kMaxDepth) {
+      wc.overflow++;
+      break;
+    }
+    terms[depth++] = color_mul(local, coef);
+    d = bounce_dir(d, N);
+    o = b.pt;
+    coef = m[10] * coef;
+  }
+  col acc = init_color(0.0f, 0.0f, 0.0f);
+  for (int k = depth - 1; k >= 0; --k) acc = color_add(acc, terms[k]);
+  return acc;
+}
+
+template <int ACCEL, bool COUNT>
+__global__ __launch_bounds__(64) void render_kernel(KParams p) {
+  const int lane = threadIdx.x & 63;
+  WorkCount wc = {};
+  for (;;) {
+    uint32_t t = 0;
+    if (lane == 0) t = atomicAdd(p.tile_counter, 1u);
+    t = __shfl(t, 0);
+    if (t >= (uint32_t)p.ntiles_local) break;
+    uint32_t g = t * (uint32_t)p.nranks + (uint32_t)p.rank;  // global tile index
+    int ty = (int)(g / (uint32_t)p.tiles_x), tx = (int)(g % (uint32_t)p.tiles_x);
+    int pr = ty * 8 + (lane >> 3), pc = tx * 8 + (lane & 7);
+    col acc = col{0.0f, 0.0f, 0.0f};
+    // PPM (row, col) -> framebuffer slot (j, i) of cpu/raytracer.c:71,128-134
+    int ii = p.W - pc, jj = p.H - pr;
+    if (pr < p.H && pc < p.W && ii >= 1 && ii <= 2 * (p.W / 2) && jj >= 1 && jj <= 2 * (p.H / 2)) {
+      int i = ii - p.W / 2, j = jj - p.H / 2;
+      acc = init_color(0.0f, 0.0f, 0.0f);
+      wc.pixels++;
+      // for (float k = i; k < i + 1; k += 0.5) for (float l = j; ...)  (cpu/raytracer.c:55-58)
+      for (int sk = 0; sk < 2; sk++) {
+        float k = (float)i + 0.5f * (float)sk;
+        for (int sl = 0; sl < 2; sl++) {
+          float l = (float)j + 0.5f * (float)sl;
+          f3 point = add(add(p.C, scale(p.u, k)), scale(p.v, l));
+          f3 dir = normalize(sub(p.pos, point));
+          col s = trace_path<ACCEL, COUNT>(p, point, dir, wc);
+          acc = color_add(acc, color_mul(s, 0.25f));
+        }
+      }
+    }
+    float* out = p.out + ((size_t)t * 64 + (size_t)lane) * 3;
+    out[0] = acc.r;
+    out[1] = acc.g;
+    out[2] = acc.b;
+  }
+  // wave-reduce the counters, one atomic per wave
+  unsigned long long v[8] = {wc.closest, wc.shadow,   wc.pixels,      wc.nodes,
+                             wc.tris,    wc.overflow, wc.zero_normal, wc.hits};
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    unsigned long long x = v[k];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+    if (lane == 0 && x) atomicAdd(p.stats + k, x);
+  }
+}
+
+// tiles of all ranks (rank-major, as gathered) -> PPM-order image
+__global__ __launch_bounds__(256) void assemble_kernel(const float* __restrict__ tiles,
+                                                       float* __restrict__ rgb, int W, int H,
+                                                       int tiles_x, int ntiles, int nranks,
+                                                       int tiles_per_rank) {
+  size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  size_t npx = (size_t)W * (size_t)H;
+  if (idx >= npx) return;
+  int row = (int)(idx / (size_t)W), col = (int)(idx % (size_t)W);
+  int g = (row >> 3) * tiles_x + (col >> 3);
+  int rank = g % nranks, local = g / nranks;
+  int lane = ((row & 7) << 3) | (col & 7);
+  const float* src = tiles + (((size_t)rank * tiles_per_rank + local) * 64 + lane) * 3;
+  rgb[3 * idx + 0] = src[0];
+  rgb[3 * idx + 1] = src[1];
+  rgb[3 * idx + 2] = src[2];
+  (void)ntiles;
+}
+
+}  // namespace rt
+
+// ---------------------------------------------------------------- launchers
+extern "C" hipError_t rt_launch_render(const KParams* p, int accel, int count_work, int grid,
+                                       hipStream_t stream) {
+  dim3 g(grid), b(64);
+  if (accel == RT_ACCEL_FLAT_D) {
+    if (count_work)
+      hipLaunchKernelGGL((rt::render_kernel<RT_ACCEL_FLAT_D, true>), g, b, 0, stream, *p);
+    else
+      hipLaunchKernelGGL((rt::render_kernel<RT_ACCEL_FLAT_D, false>), g, b, 0, stream, *p);
+  } else {
+    if (count_work)
+      hipLaunchKernelGGL((rt::render_kernel<RT_ACCEL_OCTREE_D, true>), g, b, 0, stream, *p);
+    else
+      hipLaunchKernelGGL((rt::render_kernel<RT_ACCEL_OCTREE_D, false>), g, b, 0, stream, *p);
+  }
+  return hipGetLastError();
+}
+
+extern "C" hipError_t rt_launch_assemble(const float* tiles, float* rgb, int W, int H, int tiles_x,
+                                         int ntiles, int nranks, int tiles_per_rank,
+                                         hipStream_t stream) {
+  size_t npx = (size_t)W * (size_t)H;
+  dim3 g((unsigned)((npx + 255) / 256)), b(256);
+  hipLaunchKernelGGL(rt::assemble_kernel, g, b, 0, stream, tiles, rgb, W, H, tiles_x, ntiles,
+                     nranks, tiles_per_rank);
+  return hipGetLastError();
+}

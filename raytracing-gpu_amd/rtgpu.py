@@ -1,0 +1,372 @@
+"""rtgpu -- Python view of the C ABI in include/rt_scene.h and include/rt_hip.h.
+
+A thin ctypes binding used by bench.py and the tests; the product is the
+shared library lib/librtgpu.so (host C + gfx950 HIP kernels).  There is no
+Python or CPU fallback: if the library or a gfx950 device is missing every
+render call raises RtError.
+
+Mirrors the reference interface for the path: `raytrace(input, output)`
+(cpu/headers/raytracer.h:4) is `raytrace()`, the scene model of
+cpu/headers/scene.h:7-55 is `Scene` (same C layout), the per-render query
+counters are those of SURVEY.md §8d.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(HERE, "lib")
+LIB_PATH = os.path.join(LIB_DIR, "librtgpu.so")
+
+RT_ACCEL_FLAT = 0
+RT_ACCEL_OCTREE = 1
+ACCEL = {"flat": RT_ACCEL_FLAT, "octree": RT_ACCEL_OCTREE}
+
+
+class RtError(RuntimeError):
+    def __init__(self, code, what):
+        super().__init__(f"{what}: rt error {code}")
+        self.code = code
+
+
+# ---- C layouts (include/rt_scene.h, identical to cpu/headers/scene.h) ----
+class Vec3(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("z", C.c_float)]
+
+
+class Triangle(C.Structure):
+    _fields_ = [("vertex", Vec3 * 3), ("normal", Vec3 * 3)]
+
+
+class Object(C.Structure):
+    _fields_ = [("triangles", C.POINTER(Triangle)), ("triangle_count", C.c_uint),
+                ("ka", Vec3), ("kd", Vec3), ("ks", Vec3),
+                ("ns", C.c_float), ("ni", C.c_float), ("nr", C.c_float), ("d", C.c_float)]
+
+
+class Light(C.Structure):
+    _fields_ = [("type", C.c_int), ("r", C.c_float), ("g", C.c_float), ("b", C.c_float),
+                ("v", Vec3)]
+
+
+class Camera(C.Structure):
+    _fields_ = [("width", C.c_int), ("height", C.c_int), ("position", Vec3), ("u", Vec3),
+                ("v", Vec3), ("fov", C.c_float)]
+
+
+class SceneStruct(C.Structure):
+    _fields_ = [("objects", C.POINTER(Object)), ("object_count", C.c_size_t),
+                ("lights", C.POINTER(Light)), ("light_count", C.c_size_t),
+                ("camera", Camera)]
+
+
+class Frame(C.Structure):
+    _fields_ = [("u", Vec3), ("v", Vec3), ("C", Vec3), ("position", Vec3),
+                ("width", C.c_int), ("height", C.c_int)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("closest", C.c_ulonglong), ("shadow", C.c_ulonglong), ("camera", C.c_ulonglong),
+                ("node_visits", C.c_ulonglong), ("tri_tests", C.c_ulonglong),
+                ("depth_overflow", C.c_ulonglong), ("zero_normal", C.c_ulonglong),
+                ("pixels", C.c_ulonglong), ("hits", C.c_ulonglong)]
+
+    def as_dict(self):
+        return {k: int(getattr(self, k)) for k, _ in self._fields_}
+
+
+class AccelInfo(C.Structure):
+    _fields_ = [("triangles", C.c_ulonglong), ("tri_refs", C.c_ulonglong),
+                ("nodes", C.c_ulonglong), ("leaves", C.c_ulonglong), ("max_depth", C.c_ulonglong),
+                ("tri_record_bytes", C.c_ulonglong), ("node_record_bytes", C.c_ulonglong),
+                ("device_bytes", C.c_ulonglong), ("build_seconds", C.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+# (name, restype, argtypes) for every entry point of include/*.h
+_PROTOS = [
+    ("rt_strerror", C.c_char_p, [C.c_int]),
+    ("rt_last_error", C.c_char_p, []),
+    ("rt_scene_load_svati", C.c_int, [C.c_char_p, C.POINTER(C.POINTER(SceneStruct))]),
+    ("rt_scene_load_obj", C.c_int, [C.c_char_p, C.POINTER(C.POINTER(SceneStruct))]),
+    ("rt_scene_append_obj", C.c_int, [C.POINTER(SceneStruct), C.c_char_p]),
+    ("rt_scene_write_svati", C.c_int, [C.POINTER(SceneStruct), C.c_char_p]),
+    ("rt_scene_write_obj", C.c_int, [C.POINTER(SceneStruct), C.c_char_p]),
+    ("rt_scene_synthetic", C.c_int, [C.c_uint, C.c_uint, C.c_uint, C.c_ulonglong, C.c_int,
+                                     C.c_int, C.POINTER(C.POINTER(SceneStruct))]),
+    ("rt_scene_triangle_count", C.c_size_t, [C.POINTER(SceneStruct)]),
+    ("rt_scene_free", None, [C.POINTER(SceneStruct)]),
+    ("rt_ppm_write", C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_void_p]),
+    ("rt_frame_from_camera", C.c_int, [C.POINTER(Camera), C.POINTER(Frame)]),
+    ("rt_accel_build_info", C.c_int, [C.POINTER(SceneStruct), C.c_int, C.POINTER(AccelInfo)]),
+    ("rt_accel_validate", C.c_int, [C.POINTER(SceneStruct), C.c_int]),
+    ("rt_hip_device_count", C.c_int, [C.POINTER(C.c_int)]),
+    ("rt_hip_create", C.c_int, [C.c_int, C.POINTER(SceneStruct), C.c_int, C.POINTER(C.c_void_p)]),
+    ("rt_hip_accel_info", C.c_int, [C.c_void_p, C.POINTER(AccelInfo)]),
+    ("rt_hip_destroy", None, [C.c_void_p]),
+    ("rt_hip_tiles_per_rank", C.c_int, [C.c_int, C.c_int, C.c_int]),
+    ("rt_hip_tile_buffer_floats", C.c_size_t, [C.c_int, C.c_int, C.c_int]),
+    ("rt_hip_render", C.c_int, [C.c_void_p, C.POINTER(Frame), C.c_int, C.c_int, C.c_void_p,
+                                C.c_void_p]),
+    ("rt_hip_stats", C.c_int, [C.c_void_p, C.POINTER(Stats)]),
+    ("rt_hip_set_count_work", C.c_int, [C.c_void_p, C.c_int]),
+    ("rt_hip_assemble", C.c_int, [C.c_void_p, C.POINTER(Frame), C.c_void_p, C.c_int, C.c_void_p,
+                                  C.c_void_p]),
+    ("rt_hip_render_image", C.c_int, [C.c_void_p, C.POINTER(Frame), C.c_void_p,
+                                      C.POINTER(Stats)]),
+    ("rt_hip_malloc", C.c_int, [C.c_int, C.c_size_t, C.POINTER(C.c_void_p)]),
+    ("rt_hip_free", C.c_int, [C.c_void_p]),
+    ("rt_hip_memcpy_d2h", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
+    ("rt_hip_memcpy_h2d", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
+    ("rt_raytrace", C.c_int, [C.c_char_p, C.c_char_p]),
+    ("rt_raytrace_multi", C.c_int, [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.POINTER(Stats),
+                                    C.POINTER(C.c_double)]),
+]
+
+_lib = None
+
+
+def build():
+    """Compile lib/librtgpu.so and lib/rt for gfx950 (make -C raytracing-gpu_amd)."""
+    subprocess.run(["make", "-s", "-j8", "-C", HERE], check=True)
+
+
+def lib():
+    """The loaded product library; raises if it was never built (no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RtError(-6, f"{LIB_PATH} missing: run raytracing-gpu_amd/rtgpu.build() "
+                              "(make -C raytracing-gpu_amd)")
+        L = C.CDLL(LIB_PATH)
+        for name, res, args in _PROTOS:
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(rc, what):
+    if rc != 0:
+        L = lib()
+        raise RtError(rc, f"{what}: {L.rt_strerror(rc).decode()} ({L.rt_last_error().decode()})")
+
+
+class Scene:
+    """Owns an rt_scene* (layout of cpu/headers/scene.h)."""
+
+    def __init__(self, ptr):
+        self.ptr = ptr
+
+    @classmethod
+    def load_svati(cls, path):
+        p = C.POINTER(SceneStruct)()
+        _check(lib().rt_scene_load_svati(os.fsencode(path), C.byref(p)), f"load {path}")
+        return cls(p)
+
+    @classmethod
+    def load_obj(cls, path):
+        p = C.POINTER(SceneStruct)()
+        _check(lib().rt_scene_load_obj(os.fsencode(path), C.byref(p)), f"load {path}")
+        return cls(p)
+
+    @classmethod
+    def synthetic(cls, gx=32, gy=32, tris_per_sphere=9766, seed=0x5EED, width=3840, height=2160):
+        p = C.POINTER(SceneStruct)()
+        _check(lib().rt_scene_synthetic(gx, gy, tris_per_sphere, seed, width, height, C.byref(p)),
+               "synthetic scene")
+        return cls(p)
+
+    @property
+    def s(self):
+        return self.ptr.contents
+
+    @property
+    def camera(self):
+        return self.s.camera
+
+    def set_size(self, width, height):
+        """Same effect as rewriting the camera line's width/height."""
+        self.s.camera.width = width
+        self.s.camera.height = height
+
+    @property
+    def triangle_count(self):
+        return int(lib().rt_scene_triangle_count(self.ptr))
+
+    def write_svati(self, path):
+        _check(lib().rt_scene_write_svati(self.ptr, os.fsencode(path)), f"write {path}")
+
+    def write_obj(self, path):
+        _check(lib().rt_scene_write_obj(self.ptr, os.fsencode(path)), f"write {path}")
+
+    def triangles_array(self):
+        """All triangles as a (T, 6, 3) float32 array (vertices then normals)."""
+        return scene_triangles(self.ptr)
+
+    def materials_array(self):
+        return scene_materials(self.ptr)
+
+    def frame(self):
+        f = Frame()
+        cam = Camera()
+        C.pointer(cam)[0] = self.s.camera
+        _check(lib().rt_frame_from_camera(C.byref(cam), C.byref(f)), "frame")
+        return f
+
+    def close(self):
+        if self.ptr:
+            lib().rt_scene_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _as_scene_ptr(ptr):
+    if isinstance(ptr, C.c_void_p):
+        return C.cast(ptr, C.POINTER(SceneStruct))
+    return ptr
+
+
+def scene_triangles(ptr):
+    """Triangles of any scene with the cpu/headers/scene.h layout (product or
+    oracle), as a (T, 6, 3) float32 array: 3 vertices then 3 normals."""
+    s = _as_scene_ptr(ptr).contents
+    out = []
+    for i in range(s.object_count):
+        o = s.objects[i]
+        n = o.triangle_count
+        if n:
+            buf = (C.c_float * (18 * n)).from_address(C.addressof(o.triangles.contents))
+            out.append(np.frombuffer(buf, dtype=np.float32).reshape(n, 6, 3).copy())
+    return np.concatenate(out) if out else np.zeros((0, 6, 3), np.float32)
+
+
+def scene_materials(ptr):
+    """(objects, 13) float32: ka kd ks ns ni nr d per object."""
+    s = _as_scene_ptr(ptr).contents
+    rows = []
+    for i in range(s.object_count):
+        o = s.objects[i]
+        rows.append([o.ka.x, o.ka.y, o.ka.z, o.kd.x, o.kd.y, o.kd.z, o.ks.x, o.ks.y, o.ks.z,
+                     o.ns, o.ni, o.nr, o.d])
+    return np.array(rows, np.float32).reshape(-1, 13)
+
+
+def accel_build_info(scene, accel="octree"):
+    i = AccelInfo()
+    a = ACCEL[accel] if isinstance(accel, str) else accel
+    _check(lib().rt_accel_build_info(scene.ptr, a, C.byref(i)), "accel_build_info")
+    return i.as_dict()
+
+
+def accel_validate(scene, accel="octree"):
+    a = ACCEL[accel] if isinstance(accel, str) else accel
+    _check(lib().rt_accel_validate(scene.ptr, a), "accel_validate")
+
+
+def device_count():
+    n = C.c_int(0)
+    rc = lib().rt_hip_device_count(C.byref(n))
+    return n.value if rc == 0 else 0
+
+
+def tiles_per_rank(width, height, nranks):
+    return int(lib().rt_hip_tiles_per_rank(width, height, nranks))
+
+
+def tile_buffer_floats(width, height, nranks):
+    return int(lib().rt_hip_tile_buffer_floats(width, height, nranks))
+
+
+class Context:
+    """One device image of a scene (rt_hip_create); renders through the C ABI."""
+
+    def __init__(self, scene: Scene, accel="octree", device=0):
+        self.device = device
+        self.accel = ACCEL[accel] if isinstance(accel, str) else accel
+        h = C.c_void_p()
+        _check(lib().rt_hip_create(device, scene.ptr, self.accel, C.byref(h)), "rt_hip_create")
+        self.h = h
+
+    def info(self):
+        i = AccelInfo()
+        _check(lib().rt_hip_accel_info(self.h, C.byref(i)), "accel_info")
+        return i.as_dict()
+
+    def set_count_work(self, on=True):
+        _check(lib().rt_hip_set_count_work(self.h, 1 if on else 0), "count_work")
+
+    def render(self, frame, rank, nranks, d_tiles, stream=None):
+        _check(lib().rt_hip_render(self.h, C.byref(frame), rank, nranks, C.c_void_p(d_tiles),
+                                   C.c_void_p(stream) if stream else None), "rt_hip_render")
+
+    def stats(self):
+        st = Stats()
+        _check(lib().rt_hip_stats(self.h, C.byref(st)), "rt_hip_stats")
+        return st.as_dict()
+
+    def assemble(self, frame, d_gathered, nranks, d_rgb, stream=None):
+        _check(lib().rt_hip_assemble(self.h, C.byref(frame), C.c_void_p(d_gathered), nranks,
+                                     C.c_void_p(d_rgb), C.c_void_p(stream) if stream else None),
+               "rt_hip_assemble")
+
+    def render_image(self, frame):
+        """Whole frame on this device -> (H, W, 3) float32 in PPM order, stats."""
+        img = np.empty((frame.height, frame.width, 3), np.float32)
+        st = Stats()
+        _check(lib().rt_hip_render_image(self.h, C.byref(frame),
+                                         img.ctypes.data_as(C.c_void_p), C.byref(st)),
+               "rt_hip_render_image")
+        return img, st.as_dict()
+
+    def close(self):
+        if self.h:
+            lib().rt_hip_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def write_ppm(path, rgb):
+    rgb = np.ascontiguousarray(rgb, dtype=np.float32)
+    h, w, _ = rgb.shape
+    _check(lib().rt_ppm_write(os.fsencode(path), w, h, rgb.ctypes.data_as(C.c_void_p)), "ppm")
+
+
+def raytrace(input_path, output_path, gpus=1, accel=None):
+    """Drop-in for raytrace() (cpu/raytracer.c:79-136); returns (stats, render_ms)."""
+    st = Stats()
+    ms = C.c_double(0)
+    a = -1 if accel is None else (ACCEL[accel] if isinstance(accel, str) else accel)
+    _check(lib().rt_raytrace_multi(os.fsencode(input_path), os.fsencode(output_path), gpus, a,
+                                   C.byref(st), C.byref(ms)), "rt_raytrace")
+    return st.as_dict(), ms.value
+
+
+def assemble_tiles_numpy(gathered, width, height, nranks):
+    """Host mirror of the assemble kernel's index map (for CPU tests of the
+    tiling / gather layout): gathered = nranks x tiles_per_rank x 64 x 3."""
+    tpr = tiles_per_rank(width, height, nranks) if _lib is not None else \
+        -(-(((width + 7) // 8) * ((height + 7) // 8)) // nranks)
+    g = np.asarray(gathered, np.float32).reshape(nranks, tpr, 64, 3)
+    tx = (width + 7) // 8
+    rows, cols = np.mgrid[0:height, 0:width]
+    t = (rows // 8) * tx + (cols // 8)
+    lane = (rows % 8) * 8 + (cols % 8)
+    return g[t % nranks, t // nranks, lane]

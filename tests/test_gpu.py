@@ -1,0 +1,143 @@
+"""GPU parity tests (MI355X).  Every render goes through the C ABI of
+lib/librtgpu.so; the checker is the reference's own output (tests/golden/,
+bit-exact) or the oracle restatement (oracle/, pinned to those goldens).
+
+Tolerance: north_star allows +-1 ULP per float channel; these tests demand
+bit-exact equality (0 ULP) and report the ULP histogram when it fails.
+"""
+import hashlib
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import REPO, case_id, golden_image, load_manifest_static
+
+pytestmark = pytest.mark.gpu
+CASES = load_manifest_static()
+
+
+def ulp_diff(a, b):
+    ai = a.view(np.int32).astype(np.int64)
+    bi = b.view(np.int32).astype(np.int64)
+    ai = np.where(ai < 0, -(ai & 0x7FFFFFFF), ai)
+    bi = np.where(bi < 0, -(bi & 0x7FFFFFFF), bi)
+    return np.abs(ai - bi)
+
+
+def assert_bitexact(img, ref, what):
+    d = ulp_diff(np.ascontiguousarray(img), np.ascontiguousarray(ref))
+    if d.max() != 0:
+        bad = np.argwhere(d.reshape(-1, 3).max(axis=1) > 0)[:5].ravel()
+        pytest.fail(f"{what}: {int((d > 0).sum())} channels differ, max {int(d.max())} ulp, "
+                    f"first bad flat pixels {bad.tolist()}")
+
+
+@pytest.fixture(scope="module")
+def gpu(built):
+    import rtgpu
+    if rtgpu.device_count() == 0:
+        pytest.fail("gpu tests need a gfx950 device")
+    return rtgpu
+
+
+@pytest.mark.parametrize("accel", ["flat", "octree"])
+@pytest.mark.parametrize("case", CASES, ids=[case_id(c) for c in CASES])
+def test_golden_bitexact(case, accel, gpu, scene_dir):
+    s = gpu.Scene.load_svati(os.path.join(scene_dir, case["scene"] + ".svati"))
+    s.set_size(case["width"], case["height"])
+    ctx = gpu.Context(s, accel)
+    img, st = ctx.render_image(s.frame())
+    assert_bitexact(img, golden_image(case), f"{case_id(case)}/{accel}")
+    assert st["closest"] == case["closest"]
+    assert st["shadow"] == case["shadow"]
+    assert st["depth_overflow"] == 0 and st["zero_normal"] == 0
+
+
+def test_cli_ppm_md5(gpu, scene_dir, tmp_path, manifest):
+    """`rt file.svati out.ppm` writes the reference's exact bytes (config C1)."""
+    case = next(c for c in manifest if c["scene"] == "cube" and c["width"] == 256)
+    src = os.path.join(scene_dir, "cube.svati")
+    sv = tmp_path / "cube256.svati"
+    txt = open(src).read().replace("camera 512 512", "camera 256 256")
+    sv.write_text(txt)
+    out = tmp_path / "o.ppm"
+    exe = os.path.join(REPO, "raytracing-gpu_amd", "lib", "rt")
+    subprocess.run([exe, str(sv), str(out)], check=True)
+    assert hashlib.md5(out.read_bytes()).hexdigest() == case["ppm_md5"]
+    p = subprocess.run([exe, str(sv)], capture_output=True, text=True)
+    assert p.returncode == 1 and "usage:" in p.stderr
+
+
+@pytest.mark.parametrize("nranks", [2, 3, 8])
+def test_tile_partition_gather_assemble(gpu, scene_dir, nranks, manifest):
+    """Rank-sharded renders + rank-major gather + assemble == the single image."""
+    import ctypes as C
+    case = next(c for c in manifest if c["scene"] == "island_smooth" and c["width"] == 192)
+    s = gpu.Scene.load_svati(os.path.join(scene_dir, "island_smooth.svati"))
+    s.set_size(case["width"], case["height"])
+    f = s.frame()
+    ctx = gpu.Context(s, "octree")
+    per = gpu.tile_buffer_floats(f.width, f.height, nranks)
+    L = gpu.lib()
+    dg = C.c_void_p()
+    drgb = C.c_void_p()
+    assert L.rt_hip_malloc(0, per * nranks * 4, C.byref(dg)) == 0
+    assert L.rt_hip_malloc(0, f.width * f.height * 12, C.byref(drgb)) == 0
+    tot = {"closest": 0, "shadow": 0}
+    for r in range(nranks):
+        ctx.render(f, r, nranks, dg.value + r * per * 4)
+        st = ctx.stats()
+        tot["closest"] += st["closest"]
+        tot["shadow"] += st["shadow"]
+    ctx.assemble(f, dg.value, nranks, drgb.value)
+    img = np.empty((f.height, f.width, 3), np.float32)
+    ctx.stats()  # sync
+    assert L.rt_hip_memcpy_d2h(img.ctypes.data_as(C.c_void_p), drgb, img.nbytes) == 0
+    L.rt_hip_free(dg)
+    L.rt_hip_free(drgb)
+    assert_bitexact(img, golden_image(case), f"{nranks} ranks")
+    assert tot["closest"] == case["closest"] and tot["shadow"] == case["shadow"]
+
+
+def _oracle_sample(scene, W, H, n, seed):
+    import oracle as orc
+    rng = np.random.default_rng(seed)
+    pix = np.stack([rng.integers(0, H, n), rng.integers(0, W, n)], axis=1).astype(np.int32)
+    vals, cnt = orc.render(scene.ptr, W, H, pixels=pix, threads=0)
+    return pix, vals
+
+
+@pytest.mark.parametrize("scene,W,H", [("island_smooth", 1920, 1080), ("spheres", 1920, 1080),
+                                       ("car-on-road", 960, 540), ("susans_smooth", 960, 540)])
+def test_large_flat_equals_octree_and_oracle_sample(gpu, scene_dir, scene, W, H):
+    """Full-size configs: octree == brute force over the whole frame (a
+    size-independent property), plus oracle parity on sampled pixels."""
+    s = gpu.Scene.load_svati(os.path.join(scene_dir, scene + ".svati"))
+    s.set_size(W, H)
+    f = s.frame()
+    img_o, st_o = gpu.Context(s, "octree").render_image(f)
+    img_f, st_f = gpu.Context(s, "flat").render_image(f)
+    assert_bitexact(img_o, img_f, f"{scene} octree vs flat")
+    assert st_o["closest"] == st_f["closest"] and st_o["shadow"] == st_f["shadow"]
+    pix, vals = _oracle_sample(s, W, H, 64, 11)
+    assert_bitexact(img_o[pix[:, 0], pix[:, 1]], vals, f"{scene} vs oracle sample")
+
+
+def test_synthetic_octree_vs_oracle(gpu):
+    s = gpu.Scene.synthetic(4, 4, 400, seed=0x5EED, width=96, height=54)
+    import oracle as orc
+    img, st = gpu.Context(s, "octree").render_image(s.frame())
+    ref, cnt = orc.render(s.ptr, 96, 54, threads=0)
+    assert_bitexact(img, ref, "synthetic small")
+    assert st["closest"] == cnt["closest"] and st["shadow"] == cnt["shadow"]
+
+
+def test_synthetic_c5_sample(gpu):
+    """C5 itself (10M triangles, 4K): oracle parity on a pixel sample."""
+    s = gpu.Scene.synthetic(32, 32, 9766, seed=0x5EED, width=3840, height=2160)
+    img, st = gpu.Context(s, "octree").render_image(s.frame())
+    assert st["pixels"] == 3840 * 2160 and st["depth_overflow"] == 0
+    pix, vals = _oracle_sample(s, 3840, 2160, 12, 5)
+    assert_bitexact(img[pix[:, 0], pix[:, 1]], vals, "C5 sample")

@@ -1,0 +1,181 @@
+"""Host C side of the product, no GPU: loaders, printer, writers, octree build,
+and the C-ABI library's exported surface."""
+import ctypes as C
+import hashlib
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import REPO, case_id, golden_image, load_manifest_static
+
+SCENES = sorted(f[:-9] for f in os.listdir(os.path.join(REPO, "tests", "golden", "scenes"))
+                if f.endswith(".svati.gz"))
+CASES = load_manifest_static()
+
+
+def _header_functions():
+    names = set()
+    for h in ("rt_scene.h", "rt_hip.h"):
+        src = open(os.path.join(REPO, "include", h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        for m in re.finditer(r"^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b(rt_\w+)\s*\(", src, re.M):
+            names.add(m.group(1))
+    return sorted(names)
+
+
+def test_library_exports_every_header_symbol(built):
+    import rtgpu
+    L = C.CDLL(rtgpu.LIB_PATH)
+    names = _header_functions()
+    assert len(names) >= 30
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+    bound = {p[0] for p in rtgpu._PROTOS}
+    assert set(names) <= bound, set(names) - bound
+
+
+@pytest.mark.parametrize("scene", SCENES)
+def test_svati_loader_matches_reference_parser(scene, built, scene_dir):
+    """Product loader == oracle's restatement of cpu/parser.c + parse_obj.c + stack.c."""
+    import oracle as orc
+    import rtgpu
+    path = os.path.join(scene_dir, scene + ".svati")
+    prod = rtgpu.Scene.load_svati(path)
+    ref = orc.OracleScene(path)
+    a = prod.triangles_array()
+    b = rtgpu.scene_triangles(ref.ptr)
+    assert a.shape == b.shape
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert np.array_equal(prod.materials_array().view(np.uint32),
+                          rtgpu.scene_materials(ref.ptr).view(np.uint32))
+    rs = C.cast(ref.ptr, C.POINTER(rtgpu.SceneStruct)).contents
+    ps = prod.s
+    assert rs.light_count == ps.light_count
+    for i in range(ps.light_count):
+        la, lb = ps.lights[i], rs.lights[i]
+        assert (la.type, la.r, la.g, la.b, la.v.x, la.v.y, la.v.z) == \
+               (lb.type, lb.r, lb.g, lb.b, lb.v.x, lb.v.y, lb.v.z)
+    assert bytes(ps.camera) == bytes(rs.camera)
+
+
+def test_lifo_triangle_order(built, tmp_path):
+    """cpu/parse_obj.c:29-40,83-88: triangle t, corner k = v line N-1-3t-k."""
+    import rtgpu
+    p = tmp_path / "order.svati"
+    lines = ["camera 8 8 0 0 -4 1 0 0 0 -1 0 70", "object 6"]
+    lines += [f"v {i} {10 + i} {20 + i}" for i in range(6)]
+    lines += [f"vn {i} 1 0" for i in range(6)]
+    p.write_text("\n".join(lines) + "\n")
+    tris = rtgpu.Scene.load_svati(str(p)).triangles_array()
+    for t in range(2):
+        for k in range(3):
+            assert tris[t, k, 0] == 6 - 1 - 3 * t - k
+            assert tris[t, 3 + k, 0] == 6 - 1 - 3 * t - k
+
+
+def test_comment_swallows_next_line_like_reference(built, tmp_path):
+    """'#' reads ' %[^\\n]' (cpu/parser.c:108-109): a bare '#' eats the next line."""
+    import rtgpu
+    p = tmp_path / "c.svati"
+    p.write_text("camera 8 8 0 0 -4 1 0 0 0 -1 0 70\n#\na_light 1 1 1\n# note\nd_light 1 1 1 0 -1 0\n")
+    s = rtgpu.Scene.load_svati(str(p))
+    assert s.s.light_count == 1 and s.s.lights[0].type == 1
+
+
+def test_parse_errors(built, tmp_path):
+    import rtgpu
+    p = tmp_path / "bad.svati"
+    p.write_text("camera 8 8 0 0 -4 1 0 0 0 -1 0 70\nbogus 1 2 3\n")
+    with pytest.raises(rtgpu.RtError) as e:
+        rtgpu.Scene.load_svati(str(p))
+    assert e.value.code == -3
+    with pytest.raises(rtgpu.RtError) as e:
+        rtgpu.Scene.load_svati(str(tmp_path / "missing.svati"))
+    assert e.value.code == -2
+
+
+@pytest.mark.parametrize("case", CASES, ids=[case_id(c) for c in CASES])
+def test_ppm_writer_byte_identical(case, built, tmp_path):
+    """cpu/printer.c:3-18 + cpu/raytracer.c:128-134 from the golden framebuffer."""
+    import rtgpu
+    out = tmp_path / "o.ppm"
+    rtgpu.write_ppm(str(out), golden_image(case))
+    assert hashlib.md5(out.read_bytes()).hexdigest() == case["ppm_md5"]
+
+
+def test_svati_and_obj_writers_round_trip(built, tmp_path):
+    import oracle as orc
+    import rtgpu
+    s = rtgpu.Scene.synthetic(3, 2, 96, seed=0x5EED, width=64, height=36)
+    tris = s.triangles_array()
+    assert tris.shape[0] == s.triangle_count == 6 * s.triangles_array().shape[0] // 6
+    sv = tmp_path / "syn.svati"
+    s.write_svati(str(sv))
+    back = rtgpu.Scene.load_svati(str(sv))
+    assert np.array_equal(back.triangles_array().view(np.uint32), tris.view(np.uint32))
+    ref = orc.OracleScene(str(sv))  # the reference grammar reads it back identically
+    assert np.array_equal(rtgpu.scene_triangles(ref.ptr).view(np.uint32), tris.view(np.uint32))
+    ob = tmp_path / "syn.obj"
+    s.write_obj(str(ob))
+    o = rtgpu.Scene.load_obj(str(ob))
+    assert np.array_equal(o.triangles_array().view(np.uint32), tris.view(np.uint32))
+    assert np.array_equal(o.materials_array().view(np.uint32),
+                          s.materials_array().view(np.uint32))
+    # objfile directive: camera + lights from .svati, geometry from .obj
+    sv2 = tmp_path / "withobj.svati"
+    sv2.write_text("camera 64 36 0 4 -20 1 0 0 0 -1 0 70\na_light 0.2 0.2 0.2\nobjfile syn.obj\n")
+    w = rtgpu.Scene.load_svati(str(sv2))
+    assert np.array_equal(w.triangles_array().view(np.uint32), tris.view(np.uint32))
+
+
+def test_obj_loader_faces(built, tmp_path):
+    import rtgpu
+    p = tmp_path / "q.obj"
+    p.write_text("v 0 0 0\nv 1 0 0\nv 1 1 0\nv 0 1 0\nvn 0 0 1\n"
+                 "o quad\nf 1//1 2//1 3//1 4//1\no tri\nf -4 -3 -2\n")
+    s = rtgpu.Scene.load_obj(str(p))
+    assert s.s.object_count == 2
+    t = s.triangles_array()
+    assert t.shape[0] == 3
+    assert t[1, 1].tolist() == [1, 1, 0] and t[1, 2].tolist() == [0, 1, 0]
+    assert t[2, 3].tolist() == [0, 0, 1]  # geometric normal for faces without vn
+
+
+def test_synthetic_is_deterministic(built):
+    import rtgpu
+    a = rtgpu.Scene.synthetic(4, 4, 200, seed=1, width=32, height=32).triangles_array()
+    b = rtgpu.Scene.synthetic(4, 4, 200, seed=1, width=32, height=32).triangles_array()
+    c = rtgpu.Scene.synthetic(4, 4, 200, seed=2, width=32, height=32).triangles_array()
+    assert np.array_equal(a, b) and not np.array_equal(a, c)
+
+
+@pytest.mark.parametrize("scene", ["cube", "spheres", "island_smooth", "car-on-road", "dark-night"])
+def test_octree_invariants(scene, built, scene_dir):
+    import rtgpu
+    s = rtgpu.Scene.load_svati(os.path.join(scene_dir, scene + ".svati"))
+    rtgpu.accel_validate(s, "octree")
+    rtgpu.accel_validate(s, "flat")
+    info = rtgpu.accel_build_info(s, "octree")
+    assert info["triangles"] == s.triangle_count
+    assert info["tri_refs"] >= info["triangles"]
+
+
+def test_octree_invariants_synthetic(built):
+    import rtgpu
+    s = rtgpu.Scene.synthetic(8, 8, 2000, seed=0x5EED, width=64, height=36)
+    rtgpu.accel_validate(s, "octree")
+    info = rtgpu.accel_build_info(s, "octree")
+    assert info["leaves"] > 100
+
+
+def test_render_fails_loudly_without_gpu(built, scene_dir):
+    """No CPU fallback in the product path."""
+    import rtgpu
+    if rtgpu.device_count() > 0:
+        pytest.skip("a GPU is present")
+    s = rtgpu.Scene.load_svati(os.path.join(scene_dir, "cube.svati"))
+    with pytest.raises(rtgpu.RtError) as e:
+        rtgpu.Context(s, "flat")
+    assert e.value.code == -6
