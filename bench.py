@@ -147,8 +147,12 @@ def main():
     tiles = torch.empty(per, dtype=torch.float32, device=dev)
     gathered = torch.empty(per * world, dtype=torch.float32, device=dev) if rank == 0 else None
     rgb = torch.empty(W * H * 3, dtype=torch.float32, device=dev) if rank == 0 else None
-    stream = torch.cuda.current_stream()
+    # a real (non-null) stream: the render, the events around it, the gather
+    # and the assemble are all ordered on it
+    stream = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(stream)
     sh = stream.cuda_stream
+    assert sh, "expected a non-null HIP stream handle"
 
     # instrumented pass (untimed): algorithmic work per frame for the roofline
     ctx.set_count_work(True)

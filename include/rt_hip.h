@@ -79,6 +79,15 @@ int rt_accel_build_info(const rt_scene *scene, int accel, rt_accel_info *out);
  * children).  0 = valid, RT_EINVAL = violated (rt_last_error says where). */
 int rt_accel_validate(const rt_scene *scene, int accel);
 
+/* Host-only traversal model of the device octree walk (tuning / checking):
+ * camera-ray closest-hit queries of every sample_stride-th pixel; with check,
+ * each winner is compared with brute force over all triangles. */
+typedef struct rt_accel_probe_result {
+  unsigned long long queries, hits, node_visits, tri_tests, max_stack, mismatches;
+} rt_accel_probe_result;
+int rt_accel_probe(const rt_scene *scene, int accel, int sample_stride, int check,
+                   rt_accel_probe_result *out);
+
 typedef struct rt_hip_ctx rt_hip_ctx;
 
 int rt_hip_device_count(int *n);
@@ -103,6 +112,12 @@ int rt_hip_render(rt_hip_ctx *ctx, const rt_frame *frame, int rank, int nranks, 
                   void *stream);
 /* Waits for the last render and returns its counters. */
 int rt_hip_stats(rt_hip_ctx *ctx, rt_stats *out);
+/* Octree culling slack, in units of 2^-24 x (ray-origin-to-scene distance):
+ * boxes are grown by that much so a triangle the reference's float
+ * Moller-Trumbore test accepts is never culled (DESIGN.md "Conservative
+ * culling").  Default RT_EPS_ULPS_DEFAULT (256).  Tuning knob: smaller is
+ * faster and risks parity on grazing rays. */
+int rt_hip_set_cull_slack(rt_hip_ctx *ctx, float ulps);
 /* Instrumented build: also count node visits and triangle tests (slower). */
 int rt_hip_set_count_work(rt_hip_ctx *ctx, int enable);
 

@@ -19,6 +19,10 @@ extern "C" {
 #include "../host/rt_internal.h"
 }
 
+#ifndef RT_EPS_ULPS_DEFAULT
+#define RT_EPS_ULPS_DEFAULT 256
+#endif
+
 #define HIP_TRY(expr)                                                                    \
   do {                                                                                   \
     hipError_t e_ = (expr);                                                              \
@@ -44,6 +48,7 @@ struct rt_hip_ctx {
   uint32_t nrec = 0, nlight = 0;
   rt_accel_info info{};
   float scene_c[3]{}, scene_r = 0;
+  float eps_ulps = RT_EPS_ULPS_DEFAULT;
 };
 
 static int tiles_x_of(int W) { return (W + 7) / 8; }
@@ -164,6 +169,12 @@ extern "C" int rt_hip_accel_info(const rt_hip_ctx* c, rt_accel_info* out) {
   return RT_OK;
 }
 
+extern "C" int rt_hip_set_cull_slack(rt_hip_ctx* c, float ulps) {
+  if (!c || !(ulps >= 0.0f)) return rt_set_error(RT_EINVAL, "bad slack");
+  c->eps_ulps = ulps;
+  return RT_OK;
+}
+
 extern "C" int rt_hip_set_count_work(rt_hip_ctx* c, int enable) {
   if (!c) return rt_set_error(RT_EINVAL, "null context");
   c->count_work = enable ? 1 : 0;
@@ -203,8 +214,9 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
   p.stats = c->d_stats;
   p.scene_c = rt::f3{c->scene_c[0], c->scene_c[1], c->scene_c[2]};
   p.scene_r = c->scene_r;
-  // culling slack: 256 ulps of the origin-to-geometry distance
-  p.eps_rel = 256.0f * 5.9604645e-8f;
+  // culling slack: eps_ulps ulps of the origin-to-geometry distance
+  // (DESIGN.md "Conservative culling")
+  p.eps_rel = c->eps_ulps * 5.9604645e-8f;
   p.eps_abs = 1e-6f;
   if (c->accel == RT_ACCEL_OCTREE && !c->d_node) {
     // empty scene: nothing to traverse, the FLAT kernel with 0 records is exact

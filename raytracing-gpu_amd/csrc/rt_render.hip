@@ -72,8 +72,37 @@ __device__ __forceinline__ float hit_dist(const Ray& r, float t, f3& out) {
   return length(sub(out, r.o));
 }
 
+// Conservative pre-filter of the Moller-Trumbore test.  h, a, s.h, d.q, e2.q
+// are the reference's own float values (same operations); only the IEEE
+// division f = 1/a is replaced by v_rcp_f32 (1 ulp).  A triangle is dropped
+// only when the reference's u, v, t (which differ from these by a few ulps)
+// are certain to fail cpu/hit.c:20-33, or when its distance certainly exceeds
+// t_cut (closest hit: it cannot beat the current winner, ties included);
+// survivors are re-tested exactly.  DESIGN.md "Exact MT with a cheap reject".
+__device__ __forceinline__ bool mt_candidate(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float t_cut) {
+#ifdef RT_EXACT_ONLY
+  return true;
+#else
+  f3 h = cross(d, e2);
+  float a = dot(e1, h);
+  if (a > -kEps && a < kEps) return false;  // identical test, identical a
+  float r = __builtin_amdgcn_rcpf(a);
+  f3 s = sub(o, v0);
+  float su = dot(s, h);
+  f3 q = cross(s, e1);
+  float sv = dot(d, q);
+  float st = dot(e2, q);
+  float u = su * r, v = sv * r, t = st * r;
+  const float m = 1e-5f;  // >> the few-ulp gap between (u,v,t) and the reference's
+  bool rej = (u < -1e-30f) | (u > 1.0f + m) | (v < -1e-30f) | (u + v > 1.0f + m) |
+             (t < kEps * (1.0f - m)) | (t > t_cut);
+  return !rej;
+#endif
+}
+
 struct Best {
   float dist;  // +inf = none
+  float t_cut; // parametric bound beyond which no triangle can win (+inf = none)
   uint32_t prim, obj;
   float u, v;
   f3 pt;
@@ -81,16 +110,20 @@ struct Best {
 
 __device__ __forceinline__ void consider(const Ray& r, const float4& q0, const float4& q1,
                                          const float4& q2, Best& b) {
+  f3 v0{q0.x, q0.y, q0.z}, e1{q0.w, q1.x, q1.y}, e2{q1.z, q1.w, q2.x};
+  if (!mt_candidate(r.o, r.d, v0, e1, e2, b.t_cut)) return;
   float t, u, v;
-  if (!mt_test(r.o, r.d, f3{q0.x, q0.y, q0.z}, f3{q0.w, q1.x, q1.y}, f3{q1.z, q1.w, q2.x}, t, u,
-               v))
-    return;
+  if (!mt_test(r.o, r.d, v0, e1, e2, t, u, v)) return;
   f3 out;
   float nd = hit_dist(r, t, out);
   if (!((double)nd > 0.01)) return;
   uint32_t prim = __float_as_uint(q2.y);
   if (nd < b.dist || (nd == b.dist && prim < b.prim)) {
     b.dist = nd;
+    // a rival's new_dist is |(o + nd*(t*|d|)) - o|: t*|d| up to a few ulps of
+    // |t*|d||, plus the rounding of the hit point (ulps of |o|+dist)
+    float ao = fmaxf(fabsf(r.o.x), fmaxf(fabsf(r.o.y), fabsf(r.o.z)));
+    b.t_cut = (nd * (1.0f + 1e-5f) + (ao + nd) * 2e-6f) / r.dlen;
     b.prim = prim;
     b.obj = __float_as_uint(q2.z);
     b.u = u;
@@ -101,10 +134,10 @@ __device__ __forceinline__ void consider(const Ray& r, const float4& q0, const f
 
 __device__ __forceinline__ bool any_hit_rec(const Ray& r, const float4& q0, const float4& q1,
                                             const float4& q2) {
+  f3 v0{q0.x, q0.y, q0.z}, e1{q0.w, q1.x, q1.y}, e2{q1.z, q1.w, q2.x};
+  if (!mt_candidate(r.o, r.d, v0, e1, e2, __builtin_inff())) return false;
   float t, u, v;
-  if (!mt_test(r.o, r.d, f3{q0.x, q0.y, q0.z}, f3{q0.w, q1.x, q1.y}, f3{q1.z, q1.w, q2.x}, t, u,
-               v))
-    return false;
+  if (!mt_test(r.o, r.d, v0, e1, e2, t, u, v)) return false;
   f3 out;
   return (double)hit_dist(r, t, out) > 0.01;
 }
@@ -142,7 +175,7 @@ __device__ __forceinline__ float box_enter(const Ray& r, f3 inv, float4 lo, floa
   float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
   float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
   // slack on the parametric interval too (inv may be huge)
-  float slack = 1e-5f * fmaxf(fabsf(tmin), fabsf(tmax));
+  float slack = 1e-5f * fminf(fmaxf(fabsf(tmin), fabsf(tmax)), 1e30f);  // finite even for +-inf slabs
   if (tmax + slack < fmaxf(tmin, 0.0f) - slack) return __builtin_inff();
   return tmin;
 }
@@ -329,6 +362,7 @@ __device__ col trace_path(const KParams& p, f3 o, f3 d, WorkCount& wc) {
     Ray r = make_ray(p, o, d);
     Best b;
     b.dist = __builtin_inff();
+    b.t_cut = __builtin_inff();
     b.prim = 0xffffffffu;
     closest<ACCEL, COUNT>(p, r, b, wc);
     if (b.dist == __builtin_inff()) break;

@@ -57,6 +57,8 @@ typedef struct {
   const float *rec;        /* prim-order records (12 floats each) */
   const float *pbox;       /* prim bounding boxes, 6 floats each  */
   double pad;              /* conservative slack of the overlap tests */
+  double size_stop;        /* leaf once mean triangle extent > size_stop * cell */
+  int leaf_max;            /* leaf at <= leaf_max references */
 } oct_input;
 
 /* One (sub)tree under construction.  Node slot 0 is its root. */
@@ -217,9 +219,20 @@ static void build_node(const oct_input *in, oct_tree *b, size_t slot, const dbox
   double mean_ext;
   float lo[3], hi[3];
   refs_box(in, ids, n, lo, hi, cell_ext, &mean_ext);
+  /* clip to the cell (rounded outwards): boxes of disjoint cells stay
+   * disjoint, so front-to-back culling stops early */
+  for (int a = 0; a < 3; a++)
+  {
+    float cl = (float)cell->lo[a], ch = (float)cell->hi[a];
+    if ((double)cl > cell->lo[a]) cl = nextafterf(cl, -INFINITY);
+    if ((double)ch < cell->hi[a]) ch = nextafterf(ch, INFINITY);
+    if (lo[a] < cl) lo[a] = cl;
+    if (hi[a] > ch) hi[a] = ch;
+  }
   if (depth > b->max_depth)
     b->max_depth = depth;
-  int make_leaf = n <= RT_OCT_LEAF || depth >= RT_OCT_DEPTH || mean_ext > RT_OCT_SIZE_STOP * cell_ext;
+  int make_leaf = n <= (size_t)in->leaf_max || depth >= RT_OCT_DEPTH ||
+                  mean_ext > in->size_stop * cell_ext;
   uint32_t *child_ids[8] = { 0 };
   size_t child_n[8] = { 0 };
   dbox cb[8];
@@ -543,7 +556,11 @@ int rt_flatten(const rt_scene *s, int accel, rt_flat_scene *out)
     root.lo[a] = c - 0.5 * ext;
     root.hi[a] = c + 0.5 * ext;
   }
-  oct_input in = { rec, pbox, ext * 1e-6 };
+  oct_input in = { rec, pbox, ext * 1e-6, RT_OCT_SIZE_STOP, RT_OCT_LEAF };
+  const char *ev = getenv("RT_OCT_SIZE_STOP"); /* tuning knobs (tools/, not the API) */
+  if (ev) in.size_stop = atof(ev);
+  ev = getenv("RT_OCT_LEAF");
+  if (ev) in.leaf_max = atoi(ev);
   oct_tree b;
   if (build_octree(&in, ntri, &root, &b))
   {
@@ -679,11 +696,13 @@ int rt_accel_validate(const rt_scene *s, int accel)
           lo[a] = fminf(v0, fminf(c1, c2));
           hi[a] = fmaxf(v0, fmaxf(c1, c2));
           float slack = 1e-5f * (fabsf(lo[a]) + fabsf(hi[a])) + 1e-6f;
-          lo[a] += slack;
-          hi[a] -= slack;
+          lo[a] -= slack;
+          hi[a] += slack;
         }
-        if (!box_contains(nd, lo, hi))
-          rc = rt_set_error(RT_EINVAL, "leaf %zu box misses prim %u", n, prim);
+        /* boxes are clipped to their cell: the triangle must overlap it */
+        for (int a = 0; a < 3 && !rc; a++)
+          if (hi[a] < nd[a] || lo[a] > nd[4 + a])
+            rc = rt_set_error(RT_EINVAL, "leaf %zu box misses prim %u", n, prim);
       }
     }
     else

@@ -64,6 +64,15 @@ class SceneStruct(C.Structure):
                 ("camera", Camera)]
 
 
+class ProbeResult(C.Structure):
+    _fields_ = [("queries", C.c_ulonglong), ("hits", C.c_ulonglong),
+                ("node_visits", C.c_ulonglong), ("tri_tests", C.c_ulonglong),
+                ("max_stack", C.c_ulonglong), ("mismatches", C.c_ulonglong)]
+
+    def as_dict(self):
+        return {k: int(getattr(self, k)) for k, _ in self._fields_}
+
+
 class Frame(C.Structure):
     _fields_ = [("u", Vec3), ("v", Vec3), ("C", Vec3), ("position", Vec3),
                 ("width", C.c_int), ("height", C.c_int)]
@@ -106,6 +115,8 @@ _PROTOS = [
     ("rt_frame_from_camera", C.c_int, [C.POINTER(Camera), C.POINTER(Frame)]),
     ("rt_accel_build_info", C.c_int, [C.POINTER(SceneStruct), C.c_int, C.POINTER(AccelInfo)]),
     ("rt_accel_validate", C.c_int, [C.POINTER(SceneStruct), C.c_int]),
+    ("rt_accel_probe", C.c_int, [C.POINTER(SceneStruct), C.c_int, C.c_int, C.c_int,
+                                 C.POINTER(ProbeResult)]),
     ("rt_hip_device_count", C.c_int, [C.POINTER(C.c_int)]),
     ("rt_hip_create", C.c_int, [C.c_int, C.POINTER(SceneStruct), C.c_int, C.POINTER(C.c_void_p)]),
     ("rt_hip_accel_info", C.c_int, [C.c_void_p, C.POINTER(AccelInfo)]),
@@ -116,6 +127,7 @@ _PROTOS = [
                                 C.c_void_p]),
     ("rt_hip_stats", C.c_int, [C.c_void_p, C.POINTER(Stats)]),
     ("rt_hip_set_count_work", C.c_int, [C.c_void_p, C.c_int]),
+    ("rt_hip_set_cull_slack", C.c_int, [C.c_void_p, C.c_float]),
     ("rt_hip_assemble", C.c_int, [C.c_void_p, C.POINTER(Frame), C.c_void_p, C.c_int, C.c_void_p,
                                   C.c_void_p]),
     ("rt_hip_render_image", C.c_int, [C.c_void_p, C.POINTER(Frame), C.c_void_p,
@@ -276,6 +288,13 @@ def accel_validate(scene, accel="octree"):
     _check(lib().rt_accel_validate(scene.ptr, a), "accel_validate")
 
 
+def accel_probe(scene, accel="octree", stride=97, check=True):
+    r = ProbeResult()
+    a = ACCEL[accel] if isinstance(accel, str) else accel
+    _check(lib().rt_accel_probe(scene.ptr, a, stride, 1 if check else 0, C.byref(r)), "probe")
+    return r.as_dict()
+
+
 def device_count():
     n = C.c_int(0)
     rc = lib().rt_hip_device_count(C.byref(n))
@@ -307,6 +326,9 @@ class Context:
 
     def set_count_work(self, on=True):
         _check(lib().rt_hip_set_count_work(self.h, 1 if on else 0), "count_work")
+
+    def set_cull_slack(self, ulps):
+        _check(lib().rt_hip_set_cull_slack(self.h, float(ulps)), "cull_slack")
 
     def render(self, frame, rank, nranks, d_tiles, stream=None):
         _check(lib().rt_hip_render(self.h, C.byref(frame), rank, nranks, C.c_void_p(d_tiles),
@@ -370,3 +392,24 @@ def assemble_tiles_numpy(gathered, width, height, nranks):
     t = (rows // 8) * tx + (cols // 8)
     lane = (rows % 8) * 8 + (cols % 8)
     return g[t % nranks, t // nranks, lane]
+
+
+def tiles_from_image_numpy(img, rank, nranks):
+    """Host mirror of what rank `rank` renders: its tile buffer
+    (tiles_per_rank x 64 x 3, zero-padded) cut from a full (H, W, 3) image."""
+    img = np.asarray(img, np.float32)
+    height, width, _ = img.shape
+    tx, ty = (width + 7) // 8, (height + 7) // 8
+    nt = tx * ty
+    tpr = -(-nt // nranks)
+    out = np.zeros((tpr, 64, 3), np.float32)
+    for local in range(tpr):
+        g = local * nranks + rank
+        if g >= nt:
+            break
+        r0, c0 = (g // tx) * 8, (g % tx) * 8
+        blk = np.zeros((8, 8, 3), np.float32)
+        sub = img[r0:r0 + 8, c0:c0 + 8]
+        blk[:sub.shape[0], :sub.shape[1]] = sub
+        out[local] = blk.reshape(64, 3)
+    return out
