@@ -658,6 +658,9 @@ int rt_accel_validate(const rt_scene *s, int accel)
     rt_flat_free(&f);
     return rc;
   }
+  float scene_ext = 0;
+  for (int a = 0; a < 3; a++)
+    scene_ext = fmaxf(scene_ext, f.scene_hi[a] - f.scene_lo[a]);
   unsigned char *seen = calloc(f.ntri ? f.ntri : 1, 1);
   if (!seen)
   {
@@ -695,14 +698,16 @@ int rt_accel_validate(const rt_scene *s, int accel)
           float c1 = v0 + e1, c2 = v0 + e2;
           lo[a] = fminf(v0, fminf(c1, c2));
           hi[a] = fmaxf(v0, fmaxf(c1, c2));
-          float slack = 1e-5f * (fabsf(lo[a]) + fabsf(hi[a])) + 1e-6f;
+          /* the builder inserts triangles that touch a cell within its pad
+           * (2e-6 of the scene extent here), while the box is clipped to the cell */
+          float slack = 1e-5f * (fabsf(lo[a]) + fabsf(hi[a])) + 2e-6f * scene_ext + 1e-6f;
           lo[a] -= slack;
           hi[a] += slack;
         }
         /* boxes are clipped to their cell: the triangle must overlap it */
         for (int a = 0; a < 3 && !rc; a++)
           if (hi[a] < nd[a] || lo[a] > nd[4 + a])
-            rc = rt_set_error(RT_EINVAL, "leaf %zu box misses prim %u", n, prim);
+            rc = rt_set_error(RT_EINVAL, "leaf %zu box misses prim %u (axis %d: tri [%g,%g] box [%g,%g])", n, prim, a, lo[a], hi[a], nd[a], nd[4 + a]);
       }
     }
     else

@@ -179,3 +179,24 @@ def test_render_fails_loudly_without_gpu(built, scene_dir):
     with pytest.raises(rtgpu.RtError) as e:
         rtgpu.Context(s, "flat")
     assert e.value.code == -6
+
+
+@pytest.mark.parametrize("scene,W,H,stride", [("island_smooth", 960, 540, 31),
+                                              ("car-on-road", 960, 540, 61),
+                                              ("spheres", 480, 270, 37),
+                                              ("susans_smooth", 960, 540, 61)])
+def test_octree_culling_matches_brute_force_camera_rays(built, scene_dir, scene, W, H, stride):
+    """Host model of the device walk (host/accel_probe.c): every sampled camera
+    ray's closest-hit winner through the octree equals brute force."""
+    import rtgpu
+    s = rtgpu.Scene.load_svati(os.path.join(scene_dir, scene + ".svati"))
+    s.set_size(W, H)
+    r = rtgpu.accel_probe(s, "octree", stride, True)
+    assert r["queries"] > 1000 and r["mismatches"] == 0, r
+
+
+def test_octree_probe_synthetic(built):
+    import rtgpu
+    s = rtgpu.Scene.synthetic(3, 3, 2000, seed=0x5EED, width=1280, height=720)
+    r = rtgpu.accel_probe(s, "octree", 53, True)
+    assert r["mismatches"] == 0 and r["hits"] > 100, r
