@@ -197,6 +197,6 @@ def test_octree_culling_matches_brute_force_camera_rays(built, scene_dir, scene,
 
 def test_octree_probe_synthetic(built):
     import rtgpu
-    s = rtgpu.Scene.synthetic(3, 3, 2000, seed=0x5EED, width=1280, height=720)
+    s = rtgpu.Scene.synthetic(2, 2, 1000, seed=0x5EED, width=640, height=360)
     r = rtgpu.accel_probe(s, "octree", 53, True)
     assert r["mismatches"] == 0 and r["hits"] > 100, r

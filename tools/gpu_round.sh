@@ -14,6 +14,13 @@ rc=$?
 tail -5 gpurun_out/pytest_gpu.log
 echo "pytest rc=$rc"
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+if [ -n "${EXTRA:-}" ]; then
+  timeout -k 10 ${EXTRA_TIMEOUT:-600} bash -c "$EXTRA" > gpurun_out/extra.log 2>&1
+  rc=$?
+  tail -40 gpurun_out/extra.log
+  echo "extra rc=$rc"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+fi
 if [ -n "${BENCH_ARGS:-}" ]; then
   timeout -k 10 ${BENCH_TIMEOUT:-600} python bench.py $BENCH_ARGS > gpurun_out/bench.json 2> gpurun_out/bench.err
   rc=$?
