@@ -118,6 +118,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cull-slack", type=float, default=None,
+                    help="octree culling slack override (tuning; default = library default)")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary (tools/pmc_traffic.py) to report as roofline.traffic")
     args = ap.parse_args()
@@ -139,6 +141,8 @@ def main():
         scene = load_scene(wl, td)
     ntri = scene.triangle_count
     ctx = rtgpu.Context(scene, wl["accel"], device=local)
+    if args.cull_slack is not None:
+        ctx.set_cull_slack(args.cull_slack)
     info = ctx.info()
     log(f"[rank {rank}] scene {ntri} triangles, accel {wl['accel']}: {info['tri_refs']} records, "
         f"{info['nodes']} nodes, build {info['build_seconds']:.1f}s, setup {time.perf_counter()-t:.1f}s")

@@ -69,6 +69,7 @@ typedef struct rt_accel_info {
   unsigned long long node_record_bytes;
   unsigned long long device_bytes;     /* total device memory of the scene image */
   double build_seconds;                /* host build time (flatten + octree)     */
+  unsigned long long max_leaf;         /* largest leaf (triangle records)        */
 } rt_accel_info;
 
 /* Host-only: build the acceleration structure rt_hip_create would build and
@@ -84,6 +85,8 @@ int rt_accel_validate(const rt_scene *scene, int accel);
  * each winner is compared with brute force over all triangles. */
 typedef struct rt_accel_probe_result {
   unsigned long long queries, hits, node_visits, tri_tests, max_stack, mismatches;
+  /* shadow rays of the camera hits (one per non-ambient light, any-hit) */
+  unsigned long long shadow_queries, shadow_hits, shadow_node_visits, shadow_tri_tests;
 } rt_accel_probe_result;
 int rt_accel_probe(const rt_scene *scene, int accel, int sample_stride, int check,
                    rt_accel_probe_result *out);
@@ -115,7 +118,7 @@ int rt_hip_stats(rt_hip_ctx *ctx, rt_stats *out);
 /* Octree culling slack, in units of 2^-24 x (ray-origin-to-scene distance):
  * boxes are grown by that much so a triangle the reference's float
  * Moller-Trumbore test accepts is never culled (DESIGN.md "Conservative
- * culling").  Default RT_EPS_ULPS_DEFAULT (256).  Tuning knob: smaller is
+ * culling").  Default RT_EPS_ULPS_DEFAULT (64).  Tuning knob: smaller is
  * faster and risks parity on grazing rays. */
 int rt_hip_set_cull_slack(rt_hip_ctx *ctx, float ulps);
 /* Instrumented build: also count node visits and triangle tests (slower). */

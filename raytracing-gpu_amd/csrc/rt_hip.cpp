@@ -20,7 +20,7 @@ extern "C" {
 }
 
 #ifndef RT_EPS_ULPS_DEFAULT
-#define RT_EPS_ULPS_DEFAULT 256
+#define RT_EPS_ULPS_DEFAULT 64
 #endif
 
 #define HIP_TRY(expr)                                                                    \
@@ -45,10 +45,12 @@ struct rt_hip_ctx {
   float4* d_node = nullptr;
   uint32_t* d_counter = nullptr;
   unsigned long long* d_stats = nullptr;
+  uint2* d_spill = nullptr;
   uint32_t nrec = 0, nlight = 0;
   rt_accel_info info{};
   float scene_c[3]{}, scene_r = 0;
   float eps_ulps = RT_EPS_ULPS_DEFAULT;
+  int min_waves = 0;  // launch-bounds variant (tuning: env RT_MIN_WAVES)
 };
 
 static int tiles_x_of(int W) { return (W + 7) / 8; }
@@ -94,6 +96,7 @@ extern "C" void rt_hip_destroy(rt_hip_ctx* c) {
   (void)hipFree(c->d_node);
   (void)hipFree(c->d_counter);
   (void)hipFree(c->d_stats);
+  (void)hipFree(c->d_spill);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -148,6 +151,7 @@ extern "C" int rt_hip_create(int device, const rt_scene* scene, int accel, rt_hi
   c->info.nodes = fs.nnode;
   c->info.leaves = fs.leaves;
   c->info.max_depth = fs.max_depth;
+  c->info.max_leaf = fs.max_leaf;
   c->info.tri_record_bytes = RT_TRI_FLOATS * sizeof(float);
   c->info.node_record_bytes = RT_NODE_FLOATS * sizeof(float);
   c->info.device_bytes = bytes_tri + bytes_nrm + bytes_mat + bytes_light + bytes_node;
@@ -159,6 +163,12 @@ extern "C" int rt_hip_create(int device, const rt_scene* scene, int accel, rt_hi
   }
   // persistent grid: enough one-wave workgroups to fill every SIMD
   c->grid = prop.multiProcessorCount * 16;
+  if (accel == RT_ACCEL_OCTREE &&
+      hipMalloc((void**)&c->d_spill, (size_t)c->grid * 64 * RT_SPILL_STACK * sizeof(uint2)) !=
+          hipSuccess) {
+    rt_hip_destroy(c);
+    return rt_set_error(RT_EHIP, "hipMalloc traversal spill stack");
+  }
   *out = c;
   return RT_OK;
 }
@@ -214,19 +224,24 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
   p.stats = c->d_stats;
   p.scene_c = rt::f3{c->scene_c[0], c->scene_c[1], c->scene_c[2]};
   p.scene_r = c->scene_r;
+  p.scene_cmag = std::fmax(std::fabs(c->scene_c[0]), std::fmax(std::fabs(c->scene_c[1]),
+                                                               std::fabs(c->scene_c[2])));
+  p.spill = c->d_spill;
   // culling slack: eps_ulps ulps of the origin-to-geometry distance
   // (DESIGN.md "Conservative culling")
   p.eps_rel = c->eps_ulps * 5.9604645e-8f;
-  p.eps_abs = 1e-6f;
+  // launch-bounds variant: a tuning knob read per render (tools/sweep.py)
+  const char* mw = std::getenv("RT_MIN_WAVES");
+  c->min_waves = mw ? std::atoi(mw) : 0;
   if (c->accel == RT_ACCEL_OCTREE && !c->d_node) {
     // empty scene: nothing to traverse, the FLAT kernel with 0 records is exact
     HIP_TRY(hipMemsetAsync(c->d_counter, 0, 64, s));
     HIP_TRY(hipMemsetAsync(c->d_stats, 0, RT_NSTATS * sizeof(unsigned long long), s));
-    HIP_TRY(rt_launch_render(&p, RT_ACCEL_FLAT_D, c->count_work, c->grid, s));
+    HIP_TRY(rt_launch_render(&p, RT_ACCEL_FLAT_D, c->count_work, c->min_waves, c->grid, s));
   } else {
     HIP_TRY(hipMemsetAsync(c->d_counter, 0, 64, s));
     HIP_TRY(hipMemsetAsync(c->d_stats, 0, RT_NSTATS * sizeof(unsigned long long), s));
-    HIP_TRY(rt_launch_render(&p, c->accel, c->count_work, c->grid, s));
+    HIP_TRY(rt_launch_render(&p, c->accel, c->count_work, c->min_waves, c->grid, s));
   }
   c->last_stream = s;
   return RT_OK;

@@ -9,14 +9,16 @@
 
 #define RT_ACCEL_FLAT_D 0
 #define RT_ACCEL_OCTREE_D 1
-#define RT_LEAF_FLAG_D 0x80000000u
 #define RT_MAT_FLOATS_D 12
 #define RT_LIGHT_FLOATS_D 8
 #define RT_MAX_DEPTH 32
 #define RT_NSTATS 8
+// per-lane global overflow area of the traversal stack (entries beyond LDS)
+#define RT_SPILL_STACK 112
 
+// per-lane counters (32-bit per lane; widened to 64-bit in the wave reduction)
 struct WorkCount {
-  unsigned long long closest, shadow, pixels, nodes, tris, overflow, zero_normal, hits;
+  uint32_t closest, shadow, pixels, nodes, tris, overflow, zero_normal, hits;
 };
 
 struct KParams {
@@ -32,13 +34,17 @@ struct KParams {
   float* out;                   // rank's tile buffer
   uint32_t* tile_counter;       // zeroed before launch
   unsigned long long* stats;    // RT_NSTATS counters, zeroed before launch
+  uint2* spill;                 // grid*64 lanes x RT_SPILL_STACK stack entries
   rt::f3 scene_c;               // scene box centre
-  float scene_r;                // scene box half-diagonal (max-norm)
-  float eps_rel, eps_abs;       // culling slack: eps = eps_rel*(|o-c|+r)+eps_abs
+  float scene_cmag;             // max-norm of scene_c
+  float scene_r;                // scene box half-extent (max-norm)
+  float eps_rel;                // culling slack, rt_cull.h rt_cull_eps()
 };
 
-extern "C" hipError_t rt_launch_render(const KParams* p, int accel, int count_work, int grid,
-                                       hipStream_t stream);
+// min_waves = occupancy target per SIMD (launch bounds of the instantiation:
+// 2..5); 0 = default
+extern "C" hipError_t rt_launch_render(const KParams* p, int accel, int count_work, int min_waves,
+                                       int grid, hipStream_t stream);
 extern "C" hipError_t rt_launch_assemble(const float* tiles, float* rgb, int W, int H, int tiles_x,
                                          int ntiles, int nranks, int tiles_per_rank,
                                          hipStream_t stream);

@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "rt_cull.h"
 #include "rt_device.h"
 #include "rt_kernels.h"
 
@@ -27,7 +28,6 @@ namespace rt {
 
 static constexpr float kEps = 0.0000001f;  // cpu/hit.c:7 (float)1e-7
 static constexpr int kMaxDepth = RT_MAX_DEPTH;
-static constexpr int kStack = 128;
 
 __device__ __forceinline__ f3 ld3(const float* p) { return f3{p[0], p[1], p[2]}; }
 
@@ -61,8 +61,8 @@ __device__ __forceinline__ Ray make_ray(const KParams& p, f3 o, f3 d) {
   r.d = d;
   r.dlen = length(d);
   r.nd = f3{d.x / r.dlen, d.y / r.dlen, d.z / r.dlen};
-  float m = fmaxf(fabsf(o.x - p.scene_c.x), fmaxf(fabsf(o.y - p.scene_c.y), fabsf(o.z - p.scene_c.z)));
-  r.eps = p.eps_rel * (m + p.scene_r) + p.eps_abs;
+  r.eps = rt_cull_eps(p.eps_rel, o.x - p.scene_c.x, o.y - p.scene_c.y, o.z - p.scene_c.z,
+                      p.scene_cmag, p.scene_r);
   return r;
 }
 
@@ -166,138 +166,157 @@ __device__ bool flat_any(const KParams& p, const Ray& r, WorkCount& wc) {
 }
 
 // -------------------------------------------------------------- OCTREE
-// Slab test against a box grown by r.eps; returns entry parameter (>= 0 side
-// not enforced) or +inf on miss.
-__device__ __forceinline__ float box_enter(const Ray& r, f3 inv, float4 lo, float4 hi) {
-  float tx0 = (lo.x - r.eps - r.o.x) * inv.x, tx1 = (hi.x + r.eps - r.o.x) * inv.x;
-  float ty0 = (lo.y - r.eps - r.o.y) * inv.y, ty1 = (hi.y + r.eps - r.o.y) * inv.y;
-  float tz0 = (lo.z - r.eps - r.o.z) * inv.z, tz1 = (hi.z + r.eps - r.o.z) * inv.z;
-  float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
-  float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
-  // slack on the parametric interval too (inv may be huge)
-  float slack = 1e-5f * fminf(fmaxf(fabsf(tmin), fabsf(tmax)), 1e30f);  // finite even for +-inf slabs
-  if (tmax + slack < fmaxf(tmin, 0.0f) - slack) return __builtin_inff();
-  return tmin;
+// Per-lane traversal stack: the first kLdsStack entries live in LDS, laid
+// out [entry][lane] so every lane hits its own bank; deeper entries spill to
+// a per-lane area in global memory (rare: typical depth is < 16).
+static constexpr int kLdsStack = 16;
+static constexpr int kSpillStack = RT_SPILL_STACK;
+
+struct Stack {
+  uint32_t* idx;  // LDS, kLdsStack x 64
+  float* tt;      // LDS, kLdsStack x 64
+  uint2* spill;   // this lane's kSpillStack entries
+  int lane;
+  int sp;
+};
+
+__device__ __forceinline__ void push(Stack& s, uint32_t i, float t, WorkCount& wc) {
+  if (s.sp < kLdsStack) {
+    s.idx[s.sp * 64 + s.lane] = i;
+    s.tt[s.sp * 64 + s.lane] = t;
+  } else if (s.sp < kLdsStack + kSpillStack) {
+    s.spill[s.sp - kLdsStack] = make_uint2(i, __float_as_uint(t));
+  } else {
+    wc.overflow++;  // reported as RT_EDEPTH by rt_hip_stats: never silent
+    return;
+  }
+  s.sp++;
+}
+
+__device__ __forceinline__ void pop(Stack& s, uint32_t& i, float& t) {
+  --s.sp;
+  if (s.sp < kLdsStack) {
+    i = s.idx[s.sp * 64 + s.lane];
+    t = s.tt[s.sp * 64 + s.lane];
+  } else {
+    uint2 e = s.spill[s.sp - kLdsStack];
+    i = e.x;
+    t = __uint_as_float(e.y);
+  }
 }
 
 __device__ __forceinline__ f3 inv_dir(f3 d) { return f3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z}; }
 
+__device__ __forceinline__ float box_enter(const Ray& r, f3 inv, float4 lo, float4 hi) {
+  return rt_box_enter(r.o.x, r.o.y, r.o.z, inv.x, inv.y, inv.z, r.eps, lo.x, lo.y, lo.z, hi.x,
+                      hi.y, hi.z);
+}
+
+// octant nearest to the origin side (rt_cull.h: bit a = upper half of axis a)
+__device__ __forceinline__ uint32_t near_octant(f3 d) {
+  return (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
+}
+
+// Interior node: test the children's boxes and push the hits far-to-near in
+// octant order (a valid front-to-back order for the disjoint octant cells),
+// so the nearest child is popped first.  CLOSEST also prunes by best.
+template <bool CLOSEST>
+__device__ __forceinline__ void push_children(const float4* __restrict__ node, const Ray& r, f3 inv,
+                                              uint32_t dm, uint32_t first, uint32_t info,
+                                              float best, Stack& s, WorkCount& wc) {
+  uint32_t mask = RT_NODE_MASK(info);
+#pragma unroll 1
+  for (int j = 7; j >= 0; --j) {
+    uint32_t o = (uint32_t)j ^ dm;
+    if (mask & (1u << o)) {
+      uint32_t ci = first + (uint32_t)__popc(mask & ((1u << o) - 1u));
+      float t0 = box_enter(r, inv, node[2 * ci], node[2 * ci + 1]);
+      if (t0 == __builtin_inff()) continue;
+      if (CLOSEST && best != __builtin_inff() && rt_prune(t0, r.dlen, best, r.eps)) continue;
+      push(s, ci, t0, wc);
+    }
+  }
+}
+
 template <bool COUNT>
-__device__ void oct_closest(const KParams& p, const Ray& r, Best& b, WorkCount& wc) {
+__device__ void oct_closest(const KParams& p, const Ray& r, Best& b, Stack& s, WorkCount& wc) {
   const float4* __restrict__ node = p.node;
   const float4* __restrict__ tri = p.tri;
   f3 inv = inv_dir(r.d);
-  uint32_t stk_n[kStack];
-  float stk_t[kStack];
-  int sp = 0;
+  uint32_t dm = near_octant(r.d);
+  s.sp = 0;
   {
     float t0 = box_enter(r, inv, node[0], node[1]);
-    if (t0 != __builtin_inff()) {
-      stk_n[0] = 0;
-      stk_t[0] = t0;
-      sp = 1;
-    }
+    if (t0 != __builtin_inff()) push(s, 0, t0, wc);
   }
-  while (sp > 0) {
-    --sp;
-    uint32_t ni = stk_n[sp];
-    float tn = stk_t[sp];
-    // prune: the node starts beyond the current best (with slack)
-    if (b.dist != __builtin_inff() &&
-        tn * r.dlen > b.dist + b.dist * 1e-5f + 2.0f * r.eps)
-      continue;
+  while (s.sp > 0) {
+    uint32_t ni;
+    float tn;
+    pop(s, ni, tn);
+    if (b.dist != __builtin_inff() && rt_prune(tn, r.dlen, b.dist, r.eps)) continue;
     float4 lo = node[2 * ni], hi = node[2 * ni + 1];
-    uint32_t first = __float_as_uint(lo.w), cnt = __float_as_uint(hi.w);
+    uint32_t first = __float_as_uint(lo.w), info = __float_as_uint(hi.w);
     if (COUNT) wc.nodes++;
-    if (cnt & RT_LEAF_FLAG_D) {
-      cnt &= ~RT_LEAF_FLAG_D;
+    if (info & RT_NODE_LEAF) {
+      uint32_t cnt = RT_LEAF_COUNT(info);
       for (uint32_t k = 0; k < cnt; k++) {
         const float4* q = tri + 3 * (size_t)(first + k);
         consider(r, q[0], q[1], q[2], b);
       }
       if (COUNT) wc.tris += cnt;
     } else {
-      // test the children, push hits far-to-near so the nearest pops first
-      uint32_t cidx[8];
-      float ct[8];
-      int nh = 0;
-      for (uint32_t c = 0; c < cnt; c++) {
-        uint32_t ci = first + c;
-        float t0 = box_enter(r, inv, node[2 * ci], node[2 * ci + 1]);
-        if (t0 == __builtin_inff()) continue;
-        if (b.dist != __builtin_inff() && t0 * r.dlen > b.dist + b.dist * 1e-5f + 2.0f * r.eps)
-          continue;
-        // insertion sort, descending t
-        int j = nh++;
-        while (j > 0 && ct[j - 1] < t0) {
-          ct[j] = ct[j - 1];
-          cidx[j] = cidx[j - 1];
-          --j;
-        }
-        ct[j] = t0;
-        cidx[j] = ci;
-      }
-      for (int j = 0; j < nh; j++) {
-        if (sp < kStack) {
-          stk_n[sp] = cidx[j];
-          stk_t[sp] = ct[j];
-          ++sp;
-        } else {
-          wc.overflow++;
-        }
-      }
+      push_children<true>(node, r, inv, dm, first, info, b.dist, s, wc);
     }
   }
 }
 
 template <bool COUNT>
-__device__ bool oct_any(const KParams& p, const Ray& r, WorkCount& wc) {
+__device__ bool oct_any(const KParams& p, const Ray& r, Stack& s, WorkCount& wc) {
   const float4* __restrict__ node = p.node;
   const float4* __restrict__ tri = p.tri;
   f3 inv = inv_dir(r.d);
-  uint32_t stk[kStack];
-  int sp = 0;
-  if (box_enter(r, inv, node[0], node[1]) != __builtin_inff()) stk[sp++] = 0;
-  while (sp > 0) {
-    uint32_t ni = stk[--sp];
+  uint32_t dm = near_octant(r.d);
+  s.sp = 0;
+  if (box_enter(r, inv, node[0], node[1]) != __builtin_inff()) push(s, 0, 0.0f, wc);
+  while (s.sp > 0) {
+    uint32_t ni;
+    float tn;
+    pop(s, ni, tn);
     float4 lo = node[2 * ni], hi = node[2 * ni + 1];
-    uint32_t first = __float_as_uint(lo.w), cnt = __float_as_uint(hi.w);
+    uint32_t first = __float_as_uint(lo.w), info = __float_as_uint(hi.w);
     if (COUNT) wc.nodes++;
-    if (cnt & RT_LEAF_FLAG_D) {
-      cnt &= ~RT_LEAF_FLAG_D;
+    if (info & RT_NODE_LEAF) {
+      uint32_t cnt = RT_LEAF_COUNT(info);
       for (uint32_t k = 0; k < cnt; k++) {
         const float4* q = tri + 3 * (size_t)(first + k);
         if (COUNT) wc.tris++;
-        if (any_hit_rec(r, q[0], q[1], q[2])) return true;
+        if (any_hit_rec(r, q[0], q[1], q[2])) {
+          s.sp = 0;
+          return true;
+        }
       }
     } else {
-      for (uint32_t c = 0; c < cnt; c++) {
-        uint32_t ci = first + c;
-        if (box_enter(r, inv, node[2 * ci], node[2 * ci + 1]) == __builtin_inff()) continue;
-        if (sp < kStack)
-          stk[sp++] = ci;
-        else
-          wc.overflow++;
-      }
+      push_children<false>(node, r, inv, dm, first, info, __builtin_inff(), s, wc);
     }
   }
   return false;
 }
 
 template <int ACCEL, bool COUNT>
-__device__ __forceinline__ void closest(const KParams& p, const Ray& r, Best& b, WorkCount& wc) {
+__device__ __forceinline__ void closest(const KParams& p, const Ray& r, Best& b, Stack& s,
+                                        WorkCount& wc) {
   if (ACCEL == RT_ACCEL_FLAT_D)
     flat_closest<COUNT>(p, r, b, wc);
   else
-    oct_closest<COUNT>(p, r, b, wc);
+    oct_closest<COUNT>(p, r, b, s, wc);
 }
 
 template <int ACCEL, bool COUNT>
-__device__ __forceinline__ bool shadowed(const KParams& p, f3 o, f3 d, WorkCount& wc) {
+__device__ __forceinline__ bool shadowed(const KParams& p, f3 o, f3 d, Stack& s, WorkCount& wc) {
   wc.shadow++;
   Ray r = make_ray(p, o, d);
   if (ACCEL == RT_ACCEL_FLAT_D) return flat_any<COUNT>(p, r, wc);
-  return oct_any<COUNT>(p, r, wc);
+  return oct_any<COUNT>(p, r, s, wc);
 }
 
 // cpu/light.c:7-22
@@ -314,7 +333,7 @@ __device__ __forceinline__ col specular(col tmp, f3 inc_o, f3 inc_d, f3 P, f3 N,
 
 // cpu/light.c:33-100; P = hit point, N = interpolated (unnormalised) normal
 template <int ACCEL, bool COUNT>
-__device__ col apply_light(const KParams& p, const float* m, f3 P, f3 N, WorkCount& wc) {
+__device__ col apply_light(const KParams& p, const float* m, f3 P, f3 N, Stack& s, WorkCount& wc) {
   col acc = init_color(0.0f, 0.0f, 0.0f);
   for (uint32_t li = 0; li < p.nlight; li++) {
     const float* L = p.light + RT_LIGHT_FLOATS_D * li;
@@ -326,7 +345,7 @@ __device__ col apply_light(const KParams& p, const float* m, f3 P, f3 N, WorkCou
       acc = color_add(acc, tmp);
     } else if (type == 1) {  // DIRECTIONAL
       f3 Ldir = scale(lv, -1.0f);
-      if (shadowed<ACCEL, COUNT>(p, P, Ldir, wc)) continue;
+      if (shadowed<ACCEL, COUNT>(p, P, Ldir, s, wc)) continue;
       col tmp = color_mul2(lc, init_color(m[3], m[4], m[5]));
       tmp = color_mul(tmp, dot(Ldir, N));
       f3 inc_o = add(P, scale(lv, -10.0f));
@@ -338,7 +357,7 @@ __device__ col apply_light(const KParams& p, const float* m, f3 P, f3 N, WorkCou
       if (dot(Lp, Nf) < 0.0f) Nf = scale(Nf, -1.0f);
       f3 to_l = sub(lv, P);
       float dist = length(sub(lv, P));
-      if (shadowed<ACCEL, COUNT>(p, P, to_l, wc)) continue;
+      if (shadowed<ACCEL, COUNT>(p, P, to_l, s, wc)) continue;
       col tmp = color_mul2(lc, init_color(m[3], m[4], m[5]));
       tmp = color_mul(tmp, dot(Lp, Nf) * 1.0f / dist);
       f3 inc_o = add(P, scale(to_l, -10.0f));
@@ -352,7 +371,7 @@ __device__ col apply_light(const KParams& p, const float* m, f3 P, f3 N, WorkCou
 // One camera sample: cpu/raytracer.c:19-34 unrolled into a loop; local terms
 // buffered and folded deepest-first.
 template <int ACCEL, bool COUNT>
-__device__ col trace_path(const KParams& p, f3 o, f3 d, WorkCount& wc) {
+__device__ col trace_path(const KParams& p, f3 o, f3 d, Stack& s, WorkCount& wc) {
   col terms[kMaxDepth];
   int depth = 0;
   float coef = 1.0f;
@@ -364,7 +383,7 @@ __device__ col trace_path(const KParams& p, f3 o, f3 d, WorkCount& wc) {
     b.dist = __builtin_inff();
     b.t_cut = __builtin_inff();
     b.prim = 0xffffffffu;
-    closest<ACCEL, COUNT>(p, r, b, wc);
+    closest<ACCEL, COUNT>(p, r, b, s, wc);
     if (b.dist == __builtin_inff()) break;
     wc.hits++;
     const float* nm = p.nrm + 9 * (size_t)b.prim;
@@ -375,7 +394,7 @@ __device__ col trace_path(const KParams& p, f3 o, f3 d, WorkCount& wc) {
       break;
     }
     const float* m = p.mat + RT_MAT_FLOATS_D * b.obj;
-    col local = apply_light<ACCEL, COUNT>(p, m, b.pt, N, wc);
+    col local = apply_light<ACCEL, COUNT>(p, m, b.pt, N, s, wc);
     if (depth == kMaxDepth) {
       wc.overflow++;
       break;
@@ -390,10 +409,18 @@ __device__ col trace_path(const KParams& p, f3 o, f3 d, WorkCount& wc) {
   return acc;
 }
 
-template <int ACCEL, bool COUNT>
-__global__ __launch_bounds__(64) void render_kernel(KParams p) {
+template <int ACCEL, bool COUNT, int MINW>
+__global__ __launch_bounds__(64, MINW) void render_kernel(KParams p) {
   const int lane = threadIdx.x & 63;
   WorkCount wc = {};
+  __shared__ uint32_t s_idx[ACCEL == RT_ACCEL_FLAT_D ? 1 : kLdsStack * 64];
+  __shared__ float s_t[ACCEL == RT_ACCEL_FLAT_D ? 1 : kLdsStack * 64];
+  Stack stk;
+  stk.idx = s_idx;
+  stk.tt = s_t;
+  stk.spill = p.spill + ((size_t)blockIdx.x * 64 + (size_t)lane) * kSpillStack;
+  stk.lane = lane;
+  stk.sp = 0;
   for (;;) {
     uint32_t t = 0;
     if (lane == 0) t = atomicAdd(p.tile_counter, 1u);
@@ -416,7 +443,7 @@ __global__ __launch_bounds__(64) void render_kernel(KParams p) {
           float l = (float)j + 0.5f * (float)sl;
           f3 point = add(add(p.C, scale(p.u, k)), scale(p.v, l));
           f3 dir = normalize(sub(p.pos, point));
-          col s = trace_path<ACCEL, COUNT>(p, point, dir, wc);
+          col s = trace_path<ACCEL, COUNT>(p, point, dir, stk, wc);
           acc = color_add(acc, color_mul(s, 0.25f));
         }
       }
@@ -427,11 +454,11 @@ __global__ __launch_bounds__(64) void render_kernel(KParams p) {
     out[2] = acc.b;
   }
   // wave-reduce the counters, one atomic per wave
-  unsigned long long v[8] = {wc.closest, wc.shadow,   wc.pixels,      wc.nodes,
-                             wc.tris,    wc.overflow, wc.zero_normal, wc.hits};
+  uint32_t v[8] = {wc.closest, wc.shadow,   wc.pixels,      wc.nodes,
+                   wc.tris,    wc.overflow, wc.zero_normal, wc.hits};
 #pragma unroll
   for (int k = 0; k < 8; k++) {
-    unsigned long long x = v[k];
+    unsigned long long x = (unsigned long long)v[k];
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
     if (lane == 0 && x) atomicAdd(p.stats + k, x);
@@ -460,19 +487,34 @@ __global__ __launch_bounds__(256) void assemble_kernel(const float* __restrict__
 }  // namespace rt
 
 // ---------------------------------------------------------------- launchers
-extern "C" hipError_t rt_launch_render(const KParams* p, int accel, int count_work, int grid,
-                                       hipStream_t stream) {
+#ifndef RT_DEFAULT_MIN_WAVES
+#define RT_DEFAULT_MIN_WAVES 4
+#endif
+
+template <int ACCEL, bool COUNT>
+static void launch_render(const KParams* p, int min_waves, dim3 g, dim3 b, hipStream_t stream) {
+  switch (min_waves) {
+    case 2: hipLaunchKernelGGL((rt::render_kernel<ACCEL, COUNT, 2>), g, b, 0, stream, *p); break;
+    case 5: hipLaunchKernelGGL((rt::render_kernel<ACCEL, COUNT, 5>), g, b, 0, stream, *p); break;
+    case 3: hipLaunchKernelGGL((rt::render_kernel<ACCEL, COUNT, 3>), g, b, 0, stream, *p); break;
+    default: hipLaunchKernelGGL((rt::render_kernel<ACCEL, COUNT, 4>), g, b, 0, stream, *p); break;
+  }
+}
+
+extern "C" hipError_t rt_launch_render(const KParams* p, int accel, int count_work, int min_waves,
+                                       int grid, hipStream_t stream) {
   dim3 g(grid), b(64);
+  if (min_waves == 0) min_waves = RT_DEFAULT_MIN_WAVES;
   if (accel == RT_ACCEL_FLAT_D) {
     if (count_work)
-      hipLaunchKernelGGL((rt::render_kernel<RT_ACCEL_FLAT_D, true>), g, b, 0, stream, *p);
+      launch_render<RT_ACCEL_FLAT_D, true>(p, min_waves, g, b, stream);
     else
-      hipLaunchKernelGGL((rt::render_kernel<RT_ACCEL_FLAT_D, false>), g, b, 0, stream, *p);
+      launch_render<RT_ACCEL_FLAT_D, false>(p, min_waves, g, b, stream);
   } else {
     if (count_work)
-      hipLaunchKernelGGL((rt::render_kernel<RT_ACCEL_OCTREE_D, true>), g, b, 0, stream, *p);
+      launch_render<RT_ACCEL_OCTREE_D, true>(p, min_waves, g, b, stream);
     else
-      hipLaunchKernelGGL((rt::render_kernel<RT_ACCEL_OCTREE_D, false>), g, b, 0, stream, *p);
+      launch_render<RT_ACCEL_OCTREE_D, false>(p, min_waves, g, b, stream);
   }
   return hipGetLastError();
 }

@@ -34,13 +34,14 @@
 #include <time.h>
 #include <unistd.h>
 
+#include "rt_cull.h"
 #include "rt_internal.h"
 
-#define RT_OCT_LEAF 8
+#define RT_OCT_LEAF 4
 #define RT_OCT_DEPTH 20
-#ifndef RT_OCT_SIZE_STOP
-#define RT_OCT_SIZE_STOP 0.7
-#endif
+/* size_stop >= 1 disables the "triangles larger than the cell" stop (the
+ * SAH and RT_OCT_LEAF_CAP below decide instead) */
+#define RT_OCT_SIZE_STOP 4.0
 
 static float u2f(uint32_t u)
 {
@@ -59,13 +60,15 @@ typedef struct {
   double pad;              /* conservative slack of the overlap tests */
   double size_stop;        /* leaf once mean triangle extent > size_stop * cell */
   int leaf_max;            /* leaf at <= leaf_max references */
+  double c_box;            /* SAH cost of a child box test (triangle test = 1) */
+  int leaf_cap;            /* split past this many references while it separates them */
 } oct_input;
 
 /* One (sub)tree under construction.  Node slot 0 is its root. */
 typedef struct {
   float *node; size_t nnode, node_cap;
   uint32_t *refs; size_t nref, ref_cap;
-  size_t leaves, max_depth;
+  size_t leaves, max_depth, max_leaf;
   int oom;
 } oct_tree;
 
@@ -202,25 +205,26 @@ static void refs_box(const oct_input *in, const uint32_t *ids, size_t n, float l
 }
 
 /* Subdivision stops at RT_OCT_LEAF references, at RT_OCT_DEPTH, once the
- * cell is no larger than the triangles in it (splitting further would only
- * duplicate references), or when the surface-area estimate of the split
- * (each octant is hit by ~1/4 of the rays that hit the cell, plus the cost
- * of the child box tests) is no better than testing the references here. */
-#define RT_OCT_TRAVERSAL_COST 2.0
-#define RT_OCT_CHILD_PROB 0.25
+ * cell is much smaller than the triangles in it (size_stop), or when the
+ * surface-area heuristic says the split does not pay: a visit of this node
+ * tests its children's boxes (c_box each) and then the references of every
+ * child the ray enters, with probability area(child box) / area(node box),
+ * against testing all n references here (cost 1 each). */
+#define RT_OCT_C_BOX 4.0
+#define RT_OCT_LEAF_CAP 32
+#define RT_OCT_MAX_SHRINK 40
 
-static void build_node(const oct_input *in, oct_tree *b, size_t slot, const dbox *cell,
-                       uint32_t *ids, size_t n, size_t depth, oct_tasks *defer,
-                       size_t defer_depth)
+static double box_area(const float lo[3], const float hi[3])
 {
-  if (b->oom)
-    return;
-  double cell_ext = cell->hi[0] - cell->lo[0];
-  double mean_ext;
-  float lo[3], hi[3];
-  refs_box(in, ids, n, lo, hi, cell_ext, &mean_ext);
-  /* clip to the cell (rounded outwards): boxes of disjoint cells stay
-   * disjoint, so front-to-back culling stops early */
+  double dx = (double)hi[0] - lo[0], dy = (double)hi[1] - lo[1], dz = (double)hi[2] - lo[2];
+  if (dx < 0 || dy < 0 || dz < 0)
+    return 0;
+  return 2.0 * (dx * dy + dy * dz + dz * dx);
+}
+
+/* union of the references' boxes clipped to `cell` (rounded outwards) */
+static void clip_to_cell(float lo[3], float hi[3], const dbox *cell)
+{
   for (int a = 0; a < 3; a++)
   {
     float cl = (float)cell->lo[a], ch = (float)cell->hi[a];
@@ -229,6 +233,25 @@ static void build_node(const oct_input *in, oct_tree *b, size_t slot, const dbox
     if (lo[a] < cl) lo[a] = cl;
     if (hi[a] > ch) hi[a] = ch;
   }
+}
+
+static void build_node(const oct_input *in, oct_tree *b, size_t slot, const dbox *cell0,
+                       uint32_t *ids, size_t n, size_t depth, oct_tasks *defer,
+                       size_t defer_depth)
+{
+  if (b->oom)
+    return;
+  dbox cur = *cell0;
+  const dbox *cell = &cur;
+  int shrinks = 0;
+tighten:;
+  double cell_ext = cell->hi[0] - cell->lo[0];
+  double mean_ext;
+  float lo[3], hi[3];
+  refs_box(in, ids, n, lo, hi, cell_ext, &mean_ext);
+  /* clip to the cell: boxes of disjoint cells stay disjoint, so
+   * front-to-back culling stops early */
+  clip_to_cell(lo, hi, cell);
   if (depth > b->max_depth)
     b->max_depth = depth;
   int make_leaf = n <= (size_t)in->leaf_max || depth >= RT_OCT_DEPTH ||
@@ -241,7 +264,7 @@ static void build_node(const oct_input *in, oct_tree *b, size_t slot, const dbox
     double mid[3];
     for (int a = 0; a < 3; a++)
       mid[a] = 0.5 * (cell->lo[a] + cell->hi[a]);
-    size_t total = 0;
+    double split_cost = 0, parent_area = box_area(lo, hi);
     for (int o = 0; o < 8 && !b->oom; o++)
     {
       for (int a = 0; a < 3; a++)
@@ -267,9 +290,40 @@ static void build_node(const oct_input *in, oct_tree *b, size_t slot, const dbox
         if (tri_box_overlap(in->rec + RT_TRI_FLOATS * (size_t)ids[i], &cb[o], in->pad))
           child_ids[o][child_n[o]++] = ids[i];
       }
-      total += child_n[o];
+      if (child_n[o])
+      {
+        float clo[3], chi[3];
+        double unused;
+        refs_box(in, child_ids[o], child_n[o], clo, chi, cell_ext, &unused);
+        clip_to_cell(clo, chi, &cb[o]);
+        double pr = parent_area > 0 ? box_area(clo, chi) / parent_area : 1.0;
+        split_cost += in->c_box + (pr > 1 ? 1 : pr) * (double)child_n[o];
+      }
     }
-    if (!b->oom && RT_OCT_TRAVERSAL_COST + RT_OCT_CHILD_PROB * (double)total >= (double)n)
+    int nonempty = 0, only = -1;
+    for (int o = 0; o < 8; o++)
+      if (child_n[o])
+      {
+        nonempty++;
+        only = o;
+      }
+    if (!b->oom && nonempty == 1 && shrinks < RT_OCT_MAX_SHRINK)
+    {
+      /* everything lies in one octant: shrink this node's cell to it
+       * instead of emitting a one-child node, and decide again */
+      cur = cb[only];
+      shrinks++;
+      for (int o = 0; o < 8; o++)
+      {
+        free(child_ids[o]);
+        child_ids[o] = NULL;
+        child_n[o] = 0;
+      }
+      goto tighten;
+    }
+    /* SAH says "leaf" -- but a big leaf stalls a whole wave on one lane, so
+     * above leaf_cap references always split (down to RT_OCT_DEPTH) */
+    if (!b->oom && split_cost >= (double)n && n <= (size_t)in->leaf_cap)
       make_leaf = 1;
   }
   if (b->oom)
@@ -283,15 +337,22 @@ static void build_node(const oct_input *in, oct_tree *b, size_t slot, const dbox
     }
     memcpy(b->refs + b->nref, ids, n * sizeof(uint32_t));
     write_node(b->node + RT_NODE_FLOATS * slot, lo, hi, (uint32_t)b->nref,
-               RT_LEAF_FLAG | (uint32_t)n);
+               RT_NODE_LEAF | (uint32_t)n);
     b->nref += n;
     b->leaves++;
+    if (n > b->max_leaf)
+      b->max_leaf = n;
     goto done;
   }
   {
     int nc = 0;
+    uint32_t omask = 0;
     for (int o = 0; o < 8; o++)
-      nc += child_n[o] > 0;
+      if (child_n[o])
+      {
+        nc++;
+        omask |= 1u << o;
+      }
     size_t first = b->nnode;
     if (ensure((void **)&b->node, &b->node_cap, b->nnode + (size_t)nc,
                RT_NODE_FLOATS * sizeof(float)))
@@ -300,7 +361,8 @@ static void build_node(const oct_input *in, oct_tree *b, size_t slot, const dbox
       goto done;
     }
     b->nnode += (size_t)nc;
-    write_node(b->node + RT_NODE_FLOATS * slot, lo, hi, (uint32_t)first, (uint32_t)nc);
+    write_node(b->node + RT_NODE_FLOATS * slot, lo, hi, (uint32_t)first,
+               (uint32_t)nc | omask << 8);
     size_t k = 0;
     for (int o = 0; o < 8; o++)
     {
@@ -431,7 +493,7 @@ static int build_octree(const oct_input *in, size_t ntri, const dbox *root, oct_
       uint32_t first, cnt;
       memcpy(&first, &src[3], 4);
       memcpy(&cnt, &src[7], 4);
-      first = (cnt & RT_LEAF_FLAG) ? first + (uint32_t)rbase : first + (uint32_t)nbase - 1;
+      first = (cnt & RT_NODE_LEAF) ? first + (uint32_t)rbase : first + (uint32_t)nbase - 1;
       dst[3] = u2f(first);
     }
     out->nnode += sb->nnode - 1;
@@ -440,6 +502,8 @@ static int build_octree(const oct_input *in, size_t ntri, const dbox *root, oct_
     out->leaves += sb->leaves;
     if (sb->max_depth > out->max_depth)
       out->max_depth = sb->max_depth;
+    if (sb->max_leaf > out->max_leaf)
+      out->max_leaf = sb->max_leaf;
   }
   for (size_t i = 0; i < tasks.n; i++)
   {
@@ -556,11 +620,16 @@ int rt_flatten(const rt_scene *s, int accel, rt_flat_scene *out)
     root.lo[a] = c - 0.5 * ext;
     root.hi[a] = c + 0.5 * ext;
   }
-  oct_input in = { rec, pbox, ext * 1e-6, RT_OCT_SIZE_STOP, RT_OCT_LEAF };
+  oct_input in = { rec, pbox, ext * 1e-6, RT_OCT_SIZE_STOP, RT_OCT_LEAF, RT_OCT_C_BOX,
+                   RT_OCT_LEAF_CAP };
   const char *ev = getenv("RT_OCT_SIZE_STOP"); /* tuning knobs (tools/, not the API) */
   if (ev) in.size_stop = atof(ev);
   ev = getenv("RT_OCT_LEAF");
   if (ev) in.leaf_max = atoi(ev);
+  ev = getenv("RT_OCT_C_BOX");
+  if (ev) in.c_box = atof(ev);
+  ev = getenv("RT_OCT_LEAF_CAP");
+  if (ev) in.leaf_cap = atoi(ev);
   oct_tree b;
   if (build_octree(&in, ntri, &root, &b))
   {
@@ -591,6 +660,7 @@ int rt_flatten(const rt_scene *s, int accel, rt_flat_scene *out)
   out->root_count = 1;
   out->leaves = b.leaves;
   out->max_depth = b.max_depth;
+  out->max_leaf = b.max_leaf;
   free(b.refs);
   free(rec);
   free(pbox);
@@ -628,6 +698,7 @@ int rt_accel_build_info(const rt_scene *s, int accel, rt_accel_info *info)
   info->nodes = f.nnode;
   info->leaves = f.leaves;
   info->max_depth = f.max_depth;
+  info->max_leaf = f.max_leaf;
   info->tri_record_bytes = RT_TRI_FLOATS * sizeof(float);
   info->node_record_bytes = RT_NODE_FLOATS * sizeof(float);
   info->device_bytes = (f.nrec * RT_TRI_FLOATS + f.ntri * 9 + f.nobj * RT_MAT_FLOATS +
@@ -673,9 +744,9 @@ int rt_accel_validate(const rt_scene *s, int accel)
     uint32_t first, cnt;
     memcpy(&first, &nd[3], 4);
     memcpy(&cnt, &nd[7], 4);
-    if (cnt & RT_LEAF_FLAG)
+    if (cnt & RT_NODE_LEAF)
     {
-      cnt &= ~RT_LEAF_FLAG;
+      cnt = RT_LEAF_COUNT(cnt);
       if ((size_t)first + cnt > f.nrec)
         rc = rt_set_error(RT_EINVAL, "leaf %zu: records out of range", n);
       for (uint32_t k = 0; k < cnt && !rc; k++)
@@ -712,8 +783,12 @@ int rt_accel_validate(const rt_scene *s, int accel)
     }
     else
     {
-      if (cnt == 0 || cnt > 8 || (size_t)first + cnt > f.nnode || first <= n)
-        rc = rt_set_error(RT_EINVAL, "node %zu: bad children [%u,+%u)", n, first, cnt);
+      uint32_t mask = RT_NODE_MASK(cnt);
+      cnt = RT_NODE_COUNT(cnt);
+      if (cnt == 0 || cnt > 8 || (uint32_t)__builtin_popcount(mask) != cnt ||
+          (size_t)first + cnt > f.nnode || first <= n)
+        rc = rt_set_error(RT_EINVAL, "node %zu: bad children [%u,+%u) mask %#x", n, first, cnt,
+                          mask);
       for (uint32_t c = 0; c < cnt && !rc; c++)
       {
         const float *ch = f.node + RT_NODE_FLOATS * (size_t)(first + c);

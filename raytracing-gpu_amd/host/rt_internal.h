@@ -34,12 +34,8 @@ rt_vec3 rt_v_normalize(rt_vec3 a);
  * Normals (36 B per prim, indexed by prim): the three vertex normals
  * normalised exactly as cpu/hit.c:11-13 does per test.
  *
- * Octree node (32 B, 2 x float4):
- *   lo.xyz, bits(first)   hi.xyz, bits(count | flags)
- * Interior: first = index of first child node (children contiguous),
- *           count = number of children (1..8), flag bit 31 clear.
- * Leaf:     first = index of first triangle record, count = records,
- *           flag bit 31 set.
+ * Octree node (32 B, 2 x float4): encoding in rt_cull.h (shared with the
+ * device traversal).
  */
 typedef struct rt_flat_scene {
   size_t ntri;              /* scene triangles (prims)                       */
@@ -54,14 +50,14 @@ typedef struct rt_flat_scene {
   float *node;              /* nnode * 8                                     */
   uint32_t root_count;      /* 1 (root is node 0) or 0 for FLAT              */
   float scene_lo[3], scene_hi[3];
-  size_t leaves, max_depth;
+  size_t leaves, max_depth, max_leaf;
 } rt_flat_scene;
 
 #define RT_TRI_FLOATS 12
 #define RT_NODE_FLOATS 8
 #define RT_MAT_FLOATS 12
 #define RT_LIGHT_FLOATS 8
-#define RT_LEAF_FLAG 0x80000000u
+
 
 int rt_flatten(const rt_scene *scene, int accel, rt_flat_scene *out);
 void rt_flat_free(rt_flat_scene *f);

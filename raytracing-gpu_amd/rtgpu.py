@@ -67,7 +67,9 @@ class SceneStruct(C.Structure):
 class ProbeResult(C.Structure):
     _fields_ = [("queries", C.c_ulonglong), ("hits", C.c_ulonglong),
                 ("node_visits", C.c_ulonglong), ("tri_tests", C.c_ulonglong),
-                ("max_stack", C.c_ulonglong), ("mismatches", C.c_ulonglong)]
+                ("max_stack", C.c_ulonglong), ("mismatches", C.c_ulonglong),
+                ("shadow_queries", C.c_ulonglong), ("shadow_hits", C.c_ulonglong),
+                ("shadow_node_visits", C.c_ulonglong), ("shadow_tri_tests", C.c_ulonglong)]
 
     def as_dict(self):
         return {k: int(getattr(self, k)) for k, _ in self._fields_}
@@ -92,7 +94,8 @@ class AccelInfo(C.Structure):
     _fields_ = [("triangles", C.c_ulonglong), ("tri_refs", C.c_ulonglong),
                 ("nodes", C.c_ulonglong), ("leaves", C.c_ulonglong), ("max_depth", C.c_ulonglong),
                 ("tri_record_bytes", C.c_ulonglong), ("node_record_bytes", C.c_ulonglong),
-                ("device_bytes", C.c_ulonglong), ("build_seconds", C.c_double)]
+                ("device_bytes", C.c_ulonglong), ("build_seconds", C.c_double),
+                ("max_leaf", C.c_ulonglong)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

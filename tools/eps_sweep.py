@@ -45,6 +45,8 @@ def main():
     cases = [("island_smooth", 1920, 1080), ("spheres", 1920, 1080), ("car-on-road", 3840, 2160),
              ("dark-night", 3840, 2160), ("susans_smooth", 1920, 1080),
              ("synthetic:8", 3840, 2160)]
+    if os.environ.get("EPS_SWEEP_NO_SYNTH"):
+        cases = cases[:-1]
     eps_list = [float(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "4,16,32,64,128,256").split(",")]
     out = []
     os.makedirs("gpurun_out", exist_ok=True)
