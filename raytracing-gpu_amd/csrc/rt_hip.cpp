@@ -233,6 +233,11 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
   // launch-bounds variant: a tuning knob read per render (tools/sweep.py)
   const char* mw = std::getenv("RT_MIN_WAVES");
   c->min_waves = mw ? std::atoi(mw) : 0;
+  // traversal policy (tuning knobs, tools/sweep.py): 0 lane, 1 packet, 2 hybrid
+  const char* tv = std::getenv("RT_TRAV");
+  p.trav = tv ? std::atoi(tv) : 4;
+  const char* pm = std::getenv("RT_PACKET_MIN");
+  p.packet_min = pm ? std::atoi(pm) : 8;
   if (c->accel == RT_ACCEL_OCTREE && !c->d_node) {
     // empty scene: nothing to traverse, the FLAT kernel with 0 records is exact
     HIP_TRY(hipMemsetAsync(c->d_counter, 0, 64, s));

@@ -39,6 +39,8 @@ struct KParams {
   float scene_cmag;             // max-norm of scene_c
   float scene_r;                // scene box half-extent (max-norm)
   float eps_rel;                // culling slack, rt_cull.h rt_cull_eps()
+  int trav;                     // RT_TRAV_LANE / _PACKET / _HYBRID (rt_render.hip)
+  int packet_min;               // hybrid: packet walk while >= this many lanes query
 };
 
 // min_waves = occupancy target per SIMD (launch bounds of the instantiation:

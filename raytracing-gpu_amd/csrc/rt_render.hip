@@ -83,20 +83,21 @@ __device__ __forceinline__ bool mt_candidate(f3 o, f3 d, f3 v0, f3 e1, f3 e2, fl
 #ifdef RT_EXACT_ONLY
   return true;
 #else
+  // same staging as cpu/hit.c:15-33, so a wave whose lanes all fail u skips
+  // the v and t work (coherent packets mostly agree)
+  const float m = 1e-5f;  // >> the few-ulp gap between (u,v,t) and the reference's
   f3 h = cross(d, e2);
   float a = dot(e1, h);
   if (a > -kEps && a < kEps) return false;  // identical test, identical a
   float r = __builtin_amdgcn_rcpf(a);
   f3 s = sub(o, v0);
-  float su = dot(s, h);
+  float u = dot(s, h) * r;
+  if (u < -1e-30f || u > 1.0f + m) return false;
   f3 q = cross(s, e1);
-  float sv = dot(d, q);
-  float st = dot(e2, q);
-  float u = su * r, v = sv * r, t = st * r;
-  const float m = 1e-5f;  // >> the few-ulp gap between (u,v,t) and the reference's
-  bool rej = (u < -1e-30f) | (u > 1.0f + m) | (v < -1e-30f) | (u + v > 1.0f + m) |
-             (t < kEps * (1.0f - m)) | (t > t_cut);
-  return !rej;
+  float v = dot(d, q) * r;
+  if (v < -1e-30f || u + v > 1.0f + m) return false;
+  float t = dot(e2, q) * r;
+  return !(t < kEps * (1.0f - m) || t > t_cut);
 #endif
 }
 
@@ -142,34 +143,11 @@ __device__ __forceinline__ bool any_hit_rec(const Ray& r, const float4& q0, cons
   return (double)hit_dist(r, t, out) > 0.01;
 }
 
-// ---------------------------------------------------------------- FLAT
-template <bool COUNT>
-__device__ void flat_closest(const KParams& p, const Ray& r, Best& b, WorkCount& wc) {
-  const float4* __restrict__ tri = p.tri;
-  const uint32_t n = p.nrec;
-  for (uint32_t i = 0; i < n; i++) {
-    float4 q0 = tri[3 * i], q1 = tri[3 * i + 1], q2 = tri[3 * i + 2];
-    consider(r, q0, q1, q2, b);
-  }
-  if (COUNT) wc.tris += n;
-}
-
-template <bool COUNT>
-__device__ bool flat_any(const KParams& p, const Ray& r, WorkCount& wc) {
-  const float4* __restrict__ tri = p.tri;
-  const uint32_t n = p.nrec;
-  for (uint32_t i = 0; i < n; i++) {
-    if (COUNT) wc.tris++;
-    if (any_hit_rec(r, tri[3 * i], tri[3 * i + 1], tri[3 * i + 2])) return true;
-  }
-  return false;
-}
-
 // -------------------------------------------------------------- OCTREE
 // Per-lane traversal stack: the first kLdsStack entries live in LDS, laid
 // out [entry][lane] so every lane hits its own bank; deeper entries spill to
 // a per-lane area in global memory (rare: typical depth is < 16).
-static constexpr int kLdsStack = 16;
+static constexpr int kLdsStack = 4;
 static constexpr int kSpillStack = RT_SPILL_STACK;
 
 struct Stack {
@@ -302,21 +280,385 @@ __device__ bool oct_any(const KParams& p, const Ray& r, Stack& s, WorkCount& wc)
   return false;
 }
 
+// ------------------------------------------------------ PACKET (wave) walk
+// The 64 lanes of a wave walk the octree together: one wave-uniform stack of
+// node indices in LDS, node and triangle records fetched once per wave with
+// wave-uniform addresses (broadcast to every lane), each lane testing its own
+// ray, and __ballot deciding which children any lane still needs.  Camera
+// rays of an 8x8 tile and shadow rays toward one light are coherent, so the
+// union of the lanes' walks is barely larger than each one's.
+static constexpr int kWaveStack = 192;
+
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ float4 uni4(float4 v) {
+  return make_float4(__uint_as_float(uni(__float_as_uint(v.x))),
+                     __uint_as_float(uni(__float_as_uint(v.y))),
+                     __uint_as_float(uni(__float_as_uint(v.z))),
+                     __uint_as_float(uni(__float_as_uint(v.w))));
+}
+// Wave-uniform loads through the constant address space: with a uniform
+// address they become scalar (SMEM) loads straight into SGPRs.  The scene
+// image is read-only for the whole launch.
+__device__ __forceinline__ float4 ldu(const float4* p, size_t i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef const __attribute__((address_space(4))) float4 cfloat4;
+  return ((cfloat4*)p)[i];
+#else
+  return p[i];  // host pass only parses device code
+#endif
+}
+__device__ __forceinline__ void node_u(const float4* __restrict__ node, uint32_t ni, float4& lo,
+                                       float4& hi) {
+  lo = ldu(node, 2 * (size_t)ni);
+  hi = ldu(node, 2 * (size_t)ni + 1);
+}
+
+// majority ray-direction octant of the active lanes (child push order)
+__device__ __forceinline__ uint32_t wave_near_octant(bool act, f3 d, uint64_t am) {
+  int na = __popcll(am);
+  uint32_t dm = 0;
+  if (2 * __popcll(__ballot(act && d.x < 0.0f)) > na) dm |= 1u;
+  if (2 * __popcll(__ballot(act && d.y < 0.0f)) > na) dm |= 2u;
+  if (2 * __popcll(__ballot(act && d.z < 0.0f)) > na) dm |= 4u;
+  return dm;
+}
+
+// Must be called by all 64 lanes (converged); act = this lane has a query.
+template <bool COUNT>
+__device__ void packet_closest(const KParams& p, const Ray& r, bool act, Best& b, uint32_t* ws,
+                               int lane, WorkCount& wc) {
+  const float4* __restrict__ node = p.node;
+  const float4* __restrict__ tri = p.tri;
+  uint64_t am = __ballot(act);
+  if (am == 0) return;
+  f3 inv = inv_dir(r.d);
+  uint32_t dm = wave_near_octant(act, r.d, am);
+  int sp = 0;
+  ws[sp++] = 0;
+  while (sp > 0) {
+    uint32_t ni = uni(ws[--sp]);
+    float4 lo, hi;
+    node_u(node, ni, lo, hi);
+    float tn = box_enter(r, inv, lo, hi);
+    bool want = act && tn != __builtin_inff() &&
+                !(b.dist != __builtin_inff() && rt_prune(tn, r.dlen, b.dist, r.eps));
+    if (__ballot(want) == 0) continue;
+    uint32_t first = __float_as_uint(lo.w), info = __float_as_uint(hi.w);
+    if (COUNT && lane == 0) wc.nodes++;
+    if (info & RT_NODE_LEAF) {
+      uint32_t cnt = RT_LEAF_COUNT(info);
+      for (uint32_t k = 0; k < cnt; k++) {
+        const float4* q = tri + 3 * (size_t)(first + k);
+        float4 q0 = ldu(q, 0), q1 = ldu(q, 1), q2 = ldu(q, 2);
+        if (want) consider(r, q0, q1, q2, b);
+      }
+      if (COUNT && lane == 0) wc.tris += cnt;
+    } else {
+      uint32_t mask = RT_NODE_MASK(info);
+      for (int j = 7; j >= 0; --j) {
+        uint32_t o = (uint32_t)j ^ dm;
+        if (!(mask & (1u << o))) continue;
+        uint32_t ci = first + (uint32_t)__popc(mask & ((1u << o) - 1u));
+        float4 clo, chi;
+        node_u(node, ci, clo, chi);
+        float t0 = box_enter(r, inv, clo, chi);
+        bool w2 = want && t0 != __builtin_inff() &&
+                  !(b.dist != __builtin_inff() && rt_prune(t0, r.dlen, b.dist, r.eps));
+        if (__ballot(w2) != 0) {
+          if (sp < kWaveStack)
+            ws[sp++] = ci;
+          else if (lane == 0)
+            wc.overflow++;  // RT_EDEPTH, never silent
+        }
+      }
+    }
+  }
+}
+
+template <bool COUNT>
+__device__ bool packet_any(const KParams& p, const Ray& r, bool act, uint32_t* ws, int lane,
+                           WorkCount& wc) {
+  const float4* __restrict__ node = p.node;
+  const float4* __restrict__ tri = p.tri;
+  bool alive = act, hit = false;
+  uint64_t am = __ballot(alive);
+  if (am == 0) return false;
+  f3 inv = inv_dir(r.d);
+  uint32_t dm = wave_near_octant(act, r.d, am);
+  int sp = 0;
+  ws[sp++] = 0;
+  while (sp > 0) {
+    uint32_t ni = uni(ws[--sp]);
+    float4 lo, hi;
+    node_u(node, ni, lo, hi);
+    bool want = alive && box_enter(r, inv, lo, hi) != __builtin_inff();
+    if (__ballot(want) == 0) continue;
+    uint32_t first = __float_as_uint(lo.w), info = __float_as_uint(hi.w);
+    if (COUNT && lane == 0) wc.nodes++;
+    if (info & RT_NODE_LEAF) {
+      uint32_t cnt = RT_LEAF_COUNT(info);
+      for (uint32_t k = 0; k < cnt; k++) {
+        const float4* q = tri + 3 * (size_t)(first + k);
+        float4 q0 = ldu(q, 0), q1 = ldu(q, 1), q2 = ldu(q, 2);
+        if (COUNT && lane == 0) wc.tris++;
+        if (want && any_hit_rec(r, q0, q1, q2)) {
+          hit = true;
+          alive = false;
+          want = false;
+        }
+        if (__ballot(want) == 0) break;
+      }
+      if (__ballot(alive) == 0) break;
+    } else {
+      uint32_t mask = RT_NODE_MASK(info);
+      for (int j = 7; j >= 0; --j) {
+        uint32_t o = (uint32_t)j ^ dm;
+        if (!(mask & (1u << o))) continue;
+        uint32_t ci = first + (uint32_t)__popc(mask & ((1u << o) - 1u));
+        float4 clo, chi;
+        node_u(node, ci, clo, chi);
+        bool w2 = want && box_enter(r, inv, clo, chi) != __builtin_inff();
+        if (__ballot(w2) != 0) {
+          if (sp < kWaveStack)
+            ws[sp++] = ci;
+          else if (lane == 0)
+            wc.overflow++;
+        }
+      }
+    }
+  }
+  return hit;
+}
+
+// ------------------------------------------- PACKET walk, LDS-staged records
+// Same wave walk, but every fetch is one coalesced vector load by the lanes
+// (lane k loads float4 k of the records) staged in LDS, then read back as
+// broadcasts: a leaf's triangle records (3 float4 each, 21 per chunk) or an
+// interior node's child boxes (2 float4 each, <= 8 children, contiguous) cost
+// one memory round trip instead of one per record.  The wave stack holds the
+// pushed child's whole node record (box + first/info), so a pop needs no
+// memory access before the next fetch is issued.
+static constexpr int kStage = 192;    // float4 staging slots per wave (64 triangle records)
+static constexpr int kStack2 = 128;   // wave stack entries (2 float4 each)
+
+struct WaveCtx {
+  uint32_t* ws;    // kWaveStack node indices (packet walk)
+  float4* stk2;    // kStack2 x 2 float4 (staged packet walk)
+  float4* stage;   // kStage float4
+  int lane;
+};
+
+// the wave loads src[0, n) (lane k: float4 k, k+64, k+128) and stages it;
+// n <= kStage
+__device__ __forceinline__ void stage_load(const float4* __restrict__ src, int n, WaveCtx& w) {
+  float4 v0, v1, v2;
+  const int l = w.lane;
+  if (l < n) v0 = src[l];
+  if (l + 64 < n) v1 = src[l + 64];
+  if (l + 128 < n) v2 = src[l + 128];
+  __syncthreads();  // one-wave workgroup: orders the previous readers of stage
+  if (l < n) w.stage[l] = v0;
+  if (l + 64 < n) w.stage[l + 64] = v1;
+  if (l + 128 < n) w.stage[l + 128] = v2;
+  __syncthreads();
+}
+
+// Brute force over every triangle record (cpu/hit.c:72-109 order-free, the
+// (new_dist, prim) key makes the winner order-independent), streamed through
+// LDS 64 records at a time; converged calls.
+template <bool COUNT>
+__device__ void flat_closest_w(const KParams& p, const Ray& r, bool act, Best& b, WaveCtx& w,
+                               WorkCount& wc) {
+  if (__ballot(act) == 0) return;
+  const uint32_t n = p.nrec;
+  for (uint32_t base = 0; base < n; base += kStage / 3) {
+    uint32_t m = n - base < (uint32_t)(kStage / 3) ? n - base : (uint32_t)(kStage / 3);
+    stage_load(p.tri + 3 * (size_t)base, 3 * (int)m, w);
+    for (uint32_t k = 0; k < m; k++) {
+      float4 q0 = w.stage[3 * k], q1 = w.stage[3 * k + 1], q2 = w.stage[3 * k + 2];
+      if (act) consider(r, q0, q1, q2, b);
+    }
+  }
+  if (COUNT && w.lane == 0) wc.tris += n;
+}
+
+template <bool COUNT>
+__device__ bool flat_any_w(const KParams& p, const Ray& r, bool act, WaveCtx& w, WorkCount& wc) {
+  bool alive = act, hit = false;
+  const uint32_t n = p.nrec;
+  for (uint32_t base = 0; base < n && __ballot(alive) != 0; base += kStage / 3) {
+    uint32_t m = n - base < (uint32_t)(kStage / 3) ? n - base : (uint32_t)(kStage / 3);
+    stage_load(p.tri + 3 * (size_t)base, 3 * (int)m, w);
+    if (COUNT && w.lane == 0) wc.tris += m;
+    for (uint32_t k = 0; k < m; k++) {
+      float4 q0 = w.stage[3 * k], q1 = w.stage[3 * k + 1], q2 = w.stage[3 * k + 2];
+      if (alive && any_hit_rec(r, q0, q1, q2)) {
+        hit = true;
+        alive = false;
+      }
+      if (__ballot(alive) == 0) break;
+    }
+  }
+  return hit;
+}
+
+template <bool ANY>
+__device__ __forceinline__ void stage_push_children(const float4* __restrict__ node, const Ray& r,
+                                                    f3 inv, uint32_t dm, uint32_t first,
+                                                    uint32_t info, bool want, float best,
+                                                    int& sp, WaveCtx& w, WorkCount& wc) {
+  uint32_t mask = RT_NODE_MASK(info), cnt = RT_NODE_COUNT(info);
+  stage_load(node + 2 * (size_t)first, 2 * (int)cnt, w);
+  uint32_t hitmask = 0;
+#pragma unroll
+  for (int c = 0; c < 8; c++) {
+    if ((uint32_t)c < cnt) {
+      float4 clo = w.stage[2 * c], chi = w.stage[2 * c + 1];
+      float t0 = box_enter(r, inv, clo, chi);
+      bool w2 = want && t0 != __builtin_inff() &&
+                (ANY || !(best != __builtin_inff() && rt_prune(t0, r.dlen, best, r.eps)));
+      if (__ballot(w2) != 0) hitmask |= 1u << c;
+    }
+  }
+  // far-to-near octant order: the nearest child ends on top of the stack
+  for (int j = 7; j >= 0; --j) {
+    uint32_t o = (uint32_t)j ^ dm;
+    if (!(mask & (1u << o))) continue;
+    uint32_t c = (uint32_t)__popc(mask & ((1u << o) - 1u));
+    if (!(hitmask & (1u << c))) continue;
+    if (sp < kStack2) {
+      if (w.lane < 2) w.stk2[2 * sp + w.lane] = w.stage[2 * c + w.lane];
+      sp++;
+    } else if (w.lane == 0) {
+      wc.overflow++;  // RT_EDEPTH, never silent
+    }
+  }
+}
+
+template <bool COUNT>
+__device__ void staged_closest(const KParams& p, const Ray& r, bool act, Best& b, WaveCtx& w,
+                               WorkCount& wc) {
+  const float4* __restrict__ node = p.node;
+  const float4* __restrict__ tri = p.tri;
+  uint64_t am = __ballot(act);
+  if (am == 0) return;
+  f3 inv = inv_dir(r.d);
+  uint32_t dm = wave_near_octant(act, r.d, am);
+  int sp = 0;
+  __syncthreads();
+  if (w.lane < 2) w.stk2[w.lane] = node[w.lane];
+  sp = 1;
+  while (sp > 0) {
+    --sp;
+    __syncthreads();
+    float4 lo = w.stk2[2 * sp], hi = w.stk2[2 * sp + 1];
+    uint32_t first = uni(__float_as_uint(lo.w)), info = uni(__float_as_uint(hi.w));
+    float tn = box_enter(r, inv, lo, hi);
+    bool want = act && tn != __builtin_inff() &&
+                !(b.dist != __builtin_inff() && rt_prune(tn, r.dlen, b.dist, r.eps));
+    if (__ballot(want) == 0) continue;
+    if (COUNT && w.lane == 0) wc.nodes++;
+    if (info & RT_NODE_LEAF) {
+      uint32_t cnt = RT_LEAF_COUNT(info);
+      for (uint32_t base = 0; base < cnt; base += kStage / 3) {
+        uint32_t m = cnt - base < (uint32_t)(kStage / 3) ? cnt - base : (uint32_t)(kStage / 3);
+        stage_load(tri + 3 * (size_t)(first + base), 3 * (int)m, w);
+        for (uint32_t k = 0; k < m; k++) {
+          float4 q0 = w.stage[3 * k], q1 = w.stage[3 * k + 1], q2 = w.stage[3 * k + 2];
+          if (want) consider(r, q0, q1, q2, b);
+        }
+      }
+      if (COUNT && w.lane == 0) wc.tris += cnt;
+    } else {
+      stage_push_children<false>(node, r, inv, dm, first, info, want, b.dist, sp, w, wc);
+    }
+  }
+}
+
+template <bool COUNT>
+__device__ bool staged_any(const KParams& p, const Ray& r, bool act, WaveCtx& w, WorkCount& wc) {
+  const float4* __restrict__ node = p.node;
+  const float4* __restrict__ tri = p.tri;
+  bool alive = act, hit = false;
+  uint64_t am = __ballot(alive);
+  if (am == 0) return false;
+  f3 inv = inv_dir(r.d);
+  uint32_t dm = wave_near_octant(act, r.d, am);
+  int sp = 0;
+  __syncthreads();
+  if (w.lane < 2) w.stk2[w.lane] = node[w.lane];
+  sp = 1;
+  while (sp > 0) {
+    --sp;
+    __syncthreads();
+    float4 lo = w.stk2[2 * sp], hi = w.stk2[2 * sp + 1];
+    uint32_t first = uni(__float_as_uint(lo.w)), info = uni(__float_as_uint(hi.w));
+    bool want = alive && box_enter(r, inv, lo, hi) != __builtin_inff();
+    if (__ballot(want) == 0) continue;
+    if (COUNT && w.lane == 0) wc.nodes++;
+    if (info & RT_NODE_LEAF) {
+      uint32_t cnt = RT_LEAF_COUNT(info);
+      for (uint32_t base = 0; base < cnt && __ballot(want) != 0; base += kStage / 3) {
+        uint32_t m = cnt - base < (uint32_t)(kStage / 3) ? cnt - base : (uint32_t)(kStage / 3);
+        stage_load(tri + 3 * (size_t)(first + base), 3 * (int)m, w);
+        if (COUNT && w.lane == 0) wc.tris += m;
+        for (uint32_t k = 0; k < m; k++) {
+          float4 q0 = w.stage[3 * k], q1 = w.stage[3 * k + 1], q2 = w.stage[3 * k + 2];
+          if (want && any_hit_rec(r, q0, q1, q2)) {
+            hit = true;
+            alive = false;
+            want = false;
+          }
+          if (__ballot(want) == 0) break;
+        }
+      }
+      if (__ballot(alive) == 0) break;
+    } else {
+      stage_push_children<true>(node, r, inv, dm, first, info, want, 0.0f, sp, w, wc);
+    }
+  }
+  return hit;
+}
+
+// Traversal policy: per-lane walks (each lane its own stack) or a packet
+// walk; with TRAV_HYBRID the packet walk is used while at least
+// p.packet_min lanes of the wave have a query.
+#define RT_TRAV_LANE 0
+#define RT_TRAV_PACKET 1
+#define RT_TRAV_HYBRID 2
+#define RT_TRAV_STAGED 3         // staged packet walk always
+#define RT_TRAV_STAGED_HYBRID 4  // staged packet walk while >= packet_min lanes
+
+// Closest-hit query; converged call, act = lane has a query.
 template <int ACCEL, bool COUNT>
-__device__ __forceinline__ void closest(const KParams& p, const Ray& r, Best& b, Stack& s,
-                                        WorkCount& wc) {
-  if (ACCEL == RT_ACCEL_FLAT_D)
-    flat_closest<COUNT>(p, r, b, wc);
-  else
+__device__ __forceinline__ void closest_q(const KParams& p, const Ray& r, bool act, Best& b,
+                                          Stack& s, WaveCtx& w, WorkCount& wc) {
+  if (ACCEL == RT_ACCEL_FLAT_D) {
+    flat_closest_w<COUNT>(p, r, act, b, w, wc);
+    return;
+  }
+  bool many = __popcll(__ballot(act)) >= p.packet_min;
+  if (p.trav == RT_TRAV_STAGED || (p.trav == RT_TRAV_STAGED_HYBRID && many))
+    staged_closest<COUNT>(p, r, act, b, w, wc);
+  else if (p.trav == RT_TRAV_PACKET || (p.trav == RT_TRAV_HYBRID && many))
+    packet_closest<COUNT>(p, r, act, b, w.ws, w.lane, wc);
+  else if (act)
     oct_closest<COUNT>(p, r, b, s, wc);
 }
 
+// Shadow query (collide_dist > 0.01, cpu/light.c:24-31); converged call.
 template <int ACCEL, bool COUNT>
-__device__ __forceinline__ bool shadowed(const KParams& p, f3 o, f3 d, Stack& s, WorkCount& wc) {
-  wc.shadow++;
+__device__ __forceinline__ bool shadow_q(const KParams& p, f3 o, f3 d, bool act, Stack& s,
+                                         WaveCtx& w, WorkCount& wc) {
+  if (act) wc.shadow++;
   Ray r = make_ray(p, o, d);
-  if (ACCEL == RT_ACCEL_FLAT_D) return flat_any<COUNT>(p, r, wc);
-  return oct_any<COUNT>(p, r, s, wc);
+  if (ACCEL == RT_ACCEL_FLAT_D) return flat_any_w<COUNT>(p, r, act, w, wc);
+  bool many = __popcll(__ballot(act)) >= p.packet_min;
+  if (p.trav == RT_TRAV_STAGED || (p.trav == RT_TRAV_STAGED_HYBRID && many))
+    return staged_any<COUNT>(p, r, act, w, wc);
+  if (p.trav == RT_TRAV_PACKET || (p.trav == RT_TRAV_HYBRID && many))
+    return packet_any<COUNT>(p, r, act, w.ws, w.lane, wc);
+  return act && oct_any<COUNT>(p, r, s, wc);
 }
 
 // cpu/light.c:7-22
@@ -331,9 +673,12 @@ __device__ __forceinline__ col specular(col tmp, f3 inc_o, f3 inc_d, f3 P, f3 N,
   return color_add(tmp, k);
 }
 
-// cpu/light.c:33-100; P = hit point, N = interpolated (unnormalised) normal
+// cpu/light.c:33-100 for the lanes with hit; P = hit point, N = interpolated
+// (unnormalised) normal.  The light loop is wave-uniform so shadow queries
+// run converged.
 template <int ACCEL, bool COUNT>
-__device__ col apply_light(const KParams& p, const float* m, f3 P, f3 N, Stack& s, WorkCount& wc) {
+__device__ col apply_light(const KParams& p, bool hit, const float* m, f3 P, f3 N, Stack& s,
+                           WaveCtx& w, WorkCount& wc) {
   col acc = init_color(0.0f, 0.0f, 0.0f);
   for (uint32_t li = 0; li < p.nlight; li++) {
     const float* L = p.light + RT_LIGHT_FLOATS_D * li;
@@ -341,68 +686,85 @@ __device__ col apply_light(const KParams& p, const float* m, f3 P, f3 N, Stack& 
     col lc = init_color(L[1], L[2], L[3]);
     f3 lv = f3{L[4], L[5], L[6]};
     if (type == 0) {  // AMBIENT
-      col tmp = color_mul2(lc, init_color(m[0], m[1], m[2]));
-      acc = color_add(acc, tmp);
+      if (hit) acc = color_add(acc, color_mul2(lc, init_color(m[0], m[1], m[2])));
     } else if (type == 1) {  // DIRECTIONAL
       f3 Ldir = scale(lv, -1.0f);
-      if (shadowed<ACCEL, COUNT>(p, P, Ldir, s, wc)) continue;
-      col tmp = color_mul2(lc, init_color(m[3], m[4], m[5]));
-      tmp = color_mul(tmp, dot(Ldir, N));
-      f3 inc_o = add(P, scale(lv, -10.0f));
-      tmp = specular(tmp, inc_o, lv, P, N, m);
-      acc = color_add(acc, tmp);
+      bool sh = shadow_q<ACCEL, COUNT>(p, P, Ldir, hit, s, w, wc);
+      if (hit && !sh) {
+        col tmp = color_mul2(lc, init_color(m[3], m[4], m[5]));
+        tmp = color_mul(tmp, dot(Ldir, N));
+        f3 inc_o = add(P, scale(lv, -10.0f));
+        tmp = specular(tmp, inc_o, lv, P, N, m);
+        acc = color_add(acc, tmp);
+      }
     } else if (type == 2) {  // POINT: "L" is minus the light position
-      f3 Lp = scale(lv, -1.0f);
-      f3 Nf = N;
-      if (dot(Lp, Nf) < 0.0f) Nf = scale(Nf, -1.0f);
       f3 to_l = sub(lv, P);
-      float dist = length(sub(lv, P));
-      if (shadowed<ACCEL, COUNT>(p, P, to_l, s, wc)) continue;
-      col tmp = color_mul2(lc, init_color(m[3], m[4], m[5]));
-      tmp = color_mul(tmp, dot(Lp, Nf) * 1.0f / dist);
-      f3 inc_o = add(P, scale(to_l, -10.0f));
-      tmp = specular(tmp, inc_o, to_l, P, N, m);
-      acc = color_add(acc, tmp);
+      bool sh = shadow_q<ACCEL, COUNT>(p, P, to_l, hit, s, w, wc);
+      if (hit && !sh) {
+        f3 Lp = scale(lv, -1.0f);
+        f3 Nf = N;
+        if (dot(Lp, Nf) < 0.0f) Nf = scale(Nf, -1.0f);
+        float dist = length(sub(lv, P));
+        col tmp = color_mul2(lc, init_color(m[3], m[4], m[5]));
+        tmp = color_mul(tmp, dot(Lp, Nf) * 1.0f / dist);
+        f3 inc_o = add(P, scale(to_l, -10.0f));
+        tmp = specular(tmp, inc_o, to_l, P, N, m);
+        acc = color_add(acc, tmp);
+      }
     }
   }
   return acc;
 }
 
-// One camera sample: cpu/raytracer.c:19-34 unrolled into a loop; local terms
-// buffered and folded deepest-first.
+// One camera sample (cpu/raytracer.c:19-34) for every lane of the wave: the
+// recursion becomes a wave-uniform bounce loop; local terms are buffered and
+// folded deepest-first.  valid = the lane owns a pixel.
 template <int ACCEL, bool COUNT>
-__device__ col trace_path(const KParams& p, f3 o, f3 d, Stack& s, WorkCount& wc) {
+__device__ col trace_path(const KParams& p, bool valid, f3 o, f3 d, Stack& s, WaveCtx& w,
+                          WorkCount& wc) {
   col terms[kMaxDepth];
   int depth = 0;
   float coef = 1.0f;
+  bool alive = valid;
   for (;;) {
-    if ((double)coef < 0.01) break;
-    wc.closest++;
+    alive = alive && !((double)coef < 0.01);  // checked before the query
+    if (__ballot(alive) == 0) break;
+    if (alive) wc.closest++;
     Ray r = make_ray(p, o, d);
     Best b;
     b.dist = __builtin_inff();
     b.t_cut = __builtin_inff();
     b.prim = 0xffffffffu;
-    closest<ACCEL, COUNT>(p, r, b, s, wc);
-    if (b.dist == __builtin_inff()) break;
-    wc.hits++;
-    const float* nm = p.nrm + 9 * (size_t)b.prim;
-    float w0 = 1.0f - b.u - b.v;
-    f3 N = add(add(scale(ld3(nm), w0), scale(ld3(nm + 3), b.u)), scale(ld3(nm + 6), b.v));
-    if (is_zero(N)) {  // cpu/hit.c:79 would skip this object; see DESIGN.md
-      wc.zero_normal++;
-      break;
+    b.obj = 0;
+    b.u = b.v = 0.0f;
+    b.pt = o;
+    closest_q<ACCEL, COUNT>(p, r, alive, b, s, w, wc);
+    bool hit = alive && b.dist != __builtin_inff();
+    f3 N = f3{0.0f, 0.0f, 0.0f};
+    if (hit) {
+      wc.hits++;
+      const float* nm = p.nrm + 9 * (size_t)b.prim;
+      float w0 = 1.0f - b.u - b.v;
+      N = add(add(scale(ld3(nm), w0), scale(ld3(nm + 3), b.u)), scale(ld3(nm + 6), b.v));
+      if (is_zero(N)) {  // cpu/hit.c:79 would skip this object; see DESIGN.md
+        wc.zero_normal++;
+        hit = false;
+      }
     }
-    const float* m = p.mat + RT_MAT_FLOATS_D * b.obj;
-    col local = apply_light<ACCEL, COUNT>(p, m, b.pt, N, s, wc);
-    if (depth == kMaxDepth) {
-      wc.overflow++;
-      break;
+    const float* m = p.mat + RT_MAT_FLOATS_D * (hit ? b.obj : 0u);
+    col local = apply_light<ACCEL, COUNT>(p, hit, m, b.pt, N, s, w, wc);
+    alive = hit;
+    if (hit) {
+      if (depth == kMaxDepth) {
+        wc.overflow++;
+        alive = false;
+      } else {
+        terms[depth++] = color_mul(local, coef);
+        d = bounce_dir(d, N);
+        o = b.pt;
+        coef = m[10] * coef;
+      }
     }
-    terms[depth++] = color_mul(local, coef);
-    d = bounce_dir(d, N);
-    o = b.pt;
-    coef = m[10] * coef;
   }
   col acc = init_color(0.0f, 0.0f, 0.0f);
   for (int k = depth - 1; k >= 0; --k) acc = color_add(acc, terms[k]);
@@ -415,12 +777,20 @@ __global__ __launch_bounds__(64, MINW) void render_kernel(KParams p) {
   WorkCount wc = {};
   __shared__ uint32_t s_idx[ACCEL == RT_ACCEL_FLAT_D ? 1 : kLdsStack * 64];
   __shared__ float s_t[ACCEL == RT_ACCEL_FLAT_D ? 1 : kLdsStack * 64];
+  __shared__ uint32_t s_ws[ACCEL == RT_ACCEL_FLAT_D ? 1 : kWaveStack];
+  __shared__ float4 s_stk2[ACCEL == RT_ACCEL_FLAT_D ? 1 : 2 * kStack2];
+  __shared__ float4 s_stage[kStage];
   Stack stk;
   stk.idx = s_idx;
   stk.tt = s_t;
   stk.spill = p.spill + ((size_t)blockIdx.x * 64 + (size_t)lane) * kSpillStack;
   stk.lane = lane;
   stk.sp = 0;
+  WaveCtx w;
+  w.ws = s_ws;
+  w.stk2 = s_stk2;
+  w.stage = s_stage;
+  w.lane = lane;
   for (;;) {
     uint32_t t = 0;
     if (lane == 0) t = atomicAdd(p.tile_counter, 1u);
@@ -429,25 +799,25 @@ __global__ __launch_bounds__(64, MINW) void render_kernel(KParams p) {
     uint32_t g = t * (uint32_t)p.nranks + (uint32_t)p.rank;  // global tile index
     int ty = (int)(g / (uint32_t)p.tiles_x), tx = (int)(g % (uint32_t)p.tiles_x);
     int pr = ty * 8 + (lane >> 3), pc = tx * 8 + (lane & 7);
-    col acc = col{0.0f, 0.0f, 0.0f};
     // PPM (row, col) -> framebuffer slot (j, i) of cpu/raytracer.c:71,128-134
     int ii = p.W - pc, jj = p.H - pr;
-    if (pr < p.H && pc < p.W && ii >= 1 && ii <= 2 * (p.W / 2) && jj >= 1 && jj <= 2 * (p.H / 2)) {
-      int i = ii - p.W / 2, j = jj - p.H / 2;
-      acc = init_color(0.0f, 0.0f, 0.0f);
-      wc.pixels++;
-      // for (float k = i; k < i + 1; k += 0.5) for (float l = j; ...)  (cpu/raytracer.c:55-58)
-      for (int sk = 0; sk < 2; sk++) {
-        float k = (float)i + 0.5f * (float)sk;
-        for (int sl = 0; sl < 2; sl++) {
-          float l = (float)j + 0.5f * (float)sl;
-          f3 point = add(add(p.C, scale(p.u, k)), scale(p.v, l));
-          f3 dir = normalize(sub(p.pos, point));
-          col s = trace_path<ACCEL, COUNT>(p, point, dir, stk, wc);
-          acc = color_add(acc, color_mul(s, 0.25f));
-        }
+    bool valid = pr < p.H && pc < p.W && ii >= 1 && ii <= 2 * (p.W / 2) && jj >= 1 &&
+                 jj <= 2 * (p.H / 2);
+    int i = ii - p.W / 2, j = jj - p.H / 2;
+    col acc = init_color(0.0f, 0.0f, 0.0f);
+    if (valid) wc.pixels++;
+    // for (float k = i; k < i + 1; k += 0.5) for (float l = j; ...)  (cpu/raytracer.c:55-58)
+    for (int sk = 0; sk < 2; sk++) {
+      float k = (float)i + 0.5f * (float)sk;
+      for (int sl = 0; sl < 2; sl++) {
+        float l = (float)j + 0.5f * (float)sl;
+        f3 point = add(add(p.C, scale(p.u, k)), scale(p.v, l));
+        f3 dir = normalize(sub(p.pos, point));
+        col sc = trace_path<ACCEL, COUNT>(p, valid, point, dir, stk, w, wc);
+        acc = color_add(acc, color_mul(sc, 0.25f));
       }
     }
+    if (!valid) acc = col{0.0f, 0.0f, 0.0f};
     float* out = p.out + ((size_t)t * 64 + (size_t)lane) * 3;
     out[0] = acc.r;
     out[1] = acc.g;
