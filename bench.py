@@ -33,10 +33,16 @@ sys.path.insert(0, os.path.join(REPO, "raytracing-gpu_amd"))
 import rtgpu  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
-NODE_BYTES = 32        # octree node record (host/rt_internal.h)
-TRI_BYTES = 48         # triangle record
-RAY_BYTES = 24         # origin + direction
+# Algorithmic bytes of one render launch: every record the
+# kernel fetches (a wave-uniform fetch of the packet walk counts once) plus
+# the rays' own state and the framebuffer write.
+NODE_BYTES = 32        # octree node record (host/rt_cull.h)
+TRI_BYTES = 48         # triangle record (host/rt_internal.h)
+RAY_BYTES = 24         # origin + direction of a query
 NORMAL_BYTES = 36      # 3 vertex normals of a closest-hit winner
+PIXEL_BYTES = 12       # f32 RGB written per pixel
+N_SIMD = 1024          # 256 CUs x 4 SIMDs (MI355X_MICROARCH.md)
+N_XCD = 8
 
 WORKLOADS = {
     "c5": dict(kind="synthetic", accel="octree", W=3840, H=2160,
@@ -122,6 +128,8 @@ def main():
                     help="octree culling slack override (tuning; default = library default)")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary (tools/pmc_traffic.py) to report as roofline.traffic")
+    ap.add_argument("--valu-json", default=None,
+                    help="PMC summary (tools/pmc_pass.sh, SQ VALU counters) to report as valu")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -211,13 +219,29 @@ def main():
     queries = closest + shadow
     value = queries * args.steps / el / 1e6
     # algorithmic bytes of one render launch (per rank, averaged over ranks)
-    alg_bytes = (wq * RAY_BYTES + nodes * NODE_BYTES + tris * TRI_BYTES + whits * NORMAL_BYTES)
+    alg_bytes = (wq * RAY_BYTES + nodes * NODE_BYTES + tris * TRI_BYTES + whits * NORMAL_BYTES +
+                 pixels * PIXEL_BYTES)
     per_launch = alg_bytes / world
     achieved = per_launch / (kern_ms * 1e-3) / 1e9
     traffic = None
     if args.traffic_json and os.path.exists(args.traffic_json):
         with open(args.traffic_json) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
+    valu = None
+    if args.valu_json and os.path.exists(args.valu_json):
+        # the resource this kernel actually saturates: VALU
+        # issue.  SQ_* cycle counters count quad-cycles; GRBM_GUI_ACTIVE sums
+        # the 8 XCDs' busy clocks (MI355X_MICROARCH.md, DVFS give-back).
+        with open(args.valu_json) as f:
+            pm = json.load(f)
+        quad = pm["GRBM_GUI_ACTIVE"] / N_XCD / 4.0
+        valu = {
+            "busy_frac": round(pm["SQ_ACTIVE_INST_VALU"] / (N_SIMD * quad), 4),
+            "lane_util": round(pm["SQ_THREAD_CYCLES_VALU"] / (64.0 * pm["SQ_ACTIVE_INST_VALU"]), 4),
+            "valu_insts_per_launch": pm["SQ_INSTS_VALU"],
+            "clock_ghz": round(pm["GRBM_GUI_ACTIVE"] / N_XCD / (kern_ms * 1e-3) / 1e9, 3),
+            "source": os.path.basename(args.valu_json),
+        }
 
     if rank == 0:
         cpu = None
@@ -257,9 +281,10 @@ def main():
                 "kernel_ms": round(kern_ms, 3),
                 "algorithmic_bytes_per_launch": int(per_launch),
                 "per_query_bytes": round(alg_bytes / wq, 1) if wq else None,
-                "node_visits_per_query": round(nodes / wq, 2) if wq else None,
-                "tri_tests_per_query": round(tris / wq, 2) if wq else None,
+                "node_fetches_per_query": round(nodes / wq, 3) if wq else None,
+                "tri_fetches_per_query": round(tris / wq, 3) if wq else None,
             },
+            "valu": valu,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
