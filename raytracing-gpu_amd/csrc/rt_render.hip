@@ -53,6 +53,7 @@ struct Ray {
   f3 nd;       // normalize(d)
   float dlen;  // length(d)
   float eps;   // culling slack (world units) for this origin
+  f3 oh, ol;   // o + eps, o - eps: the grown slab planes' offsets (rt_cull.h)
 };
 
 __device__ __forceinline__ Ray make_ray(const KParams& p, f3 o, f3 d) {
@@ -63,6 +64,8 @@ __device__ __forceinline__ Ray make_ray(const KParams& p, f3 o, f3 d) {
   r.nd = f3{d.x / r.dlen, d.y / r.dlen, d.z / r.dlen};
   r.eps = rt_cull_eps(p.eps_rel, o.x - p.scene_c.x, o.y - p.scene_c.y, o.z - p.scene_c.z,
                       p.scene_cmag, p.scene_r);
+  r.oh = f3{o.x + r.eps, o.y + r.eps, o.z + r.eps};
+  r.ol = f3{o.x - r.eps, o.y - r.eps, o.z - r.eps};
   return r;
 }
 
@@ -183,11 +186,18 @@ __device__ __forceinline__ void pop(Stack& s, uint32_t& i, float& t) {
   }
 }
 
-__device__ __forceinline__ f3 inv_dir(f3 d) { return f3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z}; }
+__device__ __forceinline__ f3 inv_dir(f3 d) { return f3{rt_inv(d.x), rt_inv(d.y), rt_inv(d.z)}; }
 
+// entry parameter of the eps-grown box, +inf on a miss (rt_cull.h)
 __device__ __forceinline__ float box_enter(const Ray& r, f3 inv, float4 lo, float4 hi) {
-  return rt_box_enter(r.o.x, r.o.y, r.o.z, inv.x, inv.y, inv.z, r.eps, lo.x, lo.y, lo.z, hi.x,
-                      hi.y, hi.z);
+  float t;
+  bool hit = rt_box_hit(r.oh.x, r.oh.y, r.oh.z, r.ol.x, r.ol.y, r.ol.z, inv.x, inv.y, inv.z, lo.x,
+                        lo.y, lo.z, hi.x, hi.y, hi.z, &t);
+  return hit ? t : __builtin_inff();
+}
+
+__device__ __forceinline__ bool rt_prune(float t_enter, float dlen, float best, float eps) {
+  return t_enter * dlen > rt_prune_limit(best, eps);
 }
 
 // octant nearest to the origin side (rt_cull.h: bit a = upper half of axis a)
@@ -444,36 +454,60 @@ static constexpr int kStack2 = 128;   // wave stack entries (2 float4 each)
 struct WaveCtx {
   uint32_t* ws;    // kWaveStack node indices (packet walk)
   float4* stk2;    // kStack2 x 2 float4 (staged packet walk)
+  uint64_t* stkm;  // kStack2 lane masks: lanes that wanted the pushed node
   float4* stage;   // kStage float4
   int lane;
 };
 
-// the wave loads src[0, n) (lane k: float4 k, k+64, k+128) and stages it;
-// n <= kStage
-__device__ __forceinline__ void stage_load(const float4* __restrict__ src, int n, WaveCtx& w) {
+// A fetch in flight: the wave's lanes hold float4 k, k+64, k+128 of src[0, n)
+// in registers (issued early so its latency overlaps other work), then commit
+// it to the LDS stage; n <= kStage.
+struct Fetch {
   float4 v0, v1, v2;
+  int n;
+};
+
+__device__ __forceinline__ Fetch fetch_issue(const float4* __restrict__ src, int n, int l) {
+  Fetch f;
+  f.n = n;
+  if (l < n) f.v0 = src[l];
+  if (l + 64 < n) f.v1 = src[l + 64];
+  if (l + 128 < n) f.v2 = src[l + 128];
+  return f;
+}
+
+__device__ __forceinline__ void fetch_commit(const Fetch& f, WaveCtx& w) {
   const int l = w.lane;
-  if (l < n) v0 = src[l];
-  if (l + 64 < n) v1 = src[l + 64];
-  if (l + 128 < n) v2 = src[l + 128];
   __syncthreads();  // one-wave workgroup: orders the previous readers of stage
-  if (l < n) w.stage[l] = v0;
-  if (l + 64 < n) w.stage[l + 64] = v1;
-  if (l + 128 < n) w.stage[l + 128] = v2;
+  if (l < f.n) w.stage[l] = f.v0;
+  if (l + 64 < f.n) w.stage[l + 64] = f.v1;
+  if (l + 128 < f.n) w.stage[l + 128] = f.v2;
   __syncthreads();
+}
+
+__device__ __forceinline__ void stage_load(const float4* __restrict__ src, int n, WaveCtx& w) {
+  fetch_commit(fetch_issue(src, n, w.lane), w);
+}
+
+__device__ __forceinline__ uint32_t chunk(uint32_t n, uint32_t base) {
+  return n - base < (uint32_t)(kStage / 3) ? n - base : (uint32_t)(kStage / 3);
 }
 
 // Brute force over every triangle record (cpu/hit.c:72-109 order-free, the
 // (new_dist, prim) key makes the winner order-independent), streamed through
-// LDS 64 records at a time; converged calls.
+// LDS 64 records at a time with the next chunk's fetch in flight while the
+// current one is tested; converged calls.
 template <bool COUNT>
 __device__ void flat_closest_w(const KParams& p, const Ray& r, bool act, Best& b, WaveCtx& w,
                                WorkCount& wc) {
   if (__ballot(act) == 0) return;
   const uint32_t n = p.nrec;
+  Fetch f = fetch_issue(p.tri, 3 * (int)chunk(n, 0), w.lane);
   for (uint32_t base = 0; base < n; base += kStage / 3) {
-    uint32_t m = n - base < (uint32_t)(kStage / 3) ? n - base : (uint32_t)(kStage / 3);
-    stage_load(p.tri + 3 * (size_t)base, 3 * (int)m, w);
+    uint32_t m = chunk(n, base);
+    fetch_commit(f, w);
+    uint32_t nb = base + kStage / 3;
+    if (nb < n) f = fetch_issue(p.tri + 3 * (size_t)nb, 3 * (int)chunk(n, nb), w.lane);
     for (uint32_t k = 0; k < m; k++) {
       float4 q0 = w.stage[3 * k], q1 = w.stage[3 * k + 1], q2 = w.stage[3 * k + 2];
       if (act) consider(r, q0, q1, q2, b);
@@ -486,9 +520,13 @@ template <bool COUNT>
 __device__ bool flat_any_w(const KParams& p, const Ray& r, bool act, WaveCtx& w, WorkCount& wc) {
   bool alive = act, hit = false;
   const uint32_t n = p.nrec;
-  for (uint32_t base = 0; base < n && __ballot(alive) != 0; base += kStage / 3) {
-    uint32_t m = n - base < (uint32_t)(kStage / 3) ? n - base : (uint32_t)(kStage / 3);
-    stage_load(p.tri + 3 * (size_t)base, 3 * (int)m, w);
+  if (__ballot(alive) == 0 || n == 0) return false;
+  Fetch f = fetch_issue(p.tri, 3 * (int)chunk(n, 0), w.lane);
+  for (uint32_t base = 0; base < n; base += kStage / 3) {
+    uint32_t m = chunk(n, base);
+    fetch_commit(f, w);
+    uint32_t nb = base + kStage / 3;
+    if (nb < n) f = fetch_issue(p.tri + 3 * (size_t)nb, 3 * (int)chunk(n, nb), w.lane);
     if (COUNT && w.lane == 0) wc.tris += m;
     for (uint32_t k = 0; k < m; k++) {
       float4 q0 = w.stage[3 * k], q1 = w.stage[3 * k + 1], q2 = w.stage[3 * k + 2];
@@ -498,29 +536,32 @@ __device__ bool flat_any_w(const KParams& p, const Ray& r, bool act, WaveCtx& w,
       }
       if (__ballot(alive) == 0) break;
     }
+    if (__ballot(alive) == 0) break;
   }
   return hit;
 }
 
+// Interior node whose child boxes are staged: test them, push the ones any
+// lane wants (with the mask of the lanes that want each) far-to-near in
+// octant order, so the nearest child ends on top of the stack.
 template <bool ANY>
-__device__ __forceinline__ void stage_push_children(const float4* __restrict__ node, const Ray& r,
-                                                    f3 inv, uint32_t dm, uint32_t first,
-                                                    uint32_t info, bool want, float best,
+__device__ __forceinline__ void stage_push_children(const Ray& r, f3 inv, uint32_t dm,
+                                                    uint32_t info, bool want, float limit,
                                                     int& sp, WaveCtx& w, WorkCount& wc) {
   uint32_t mask = RT_NODE_MASK(info), cnt = RT_NODE_COUNT(info);
-  stage_load(node + 2 * (size_t)first, 2 * (int)cnt, w);
+  uint64_t lanes[8];
   uint32_t hitmask = 0;
 #pragma unroll
   for (int c = 0; c < 8; c++) {
+    lanes[c] = 0;
     if ((uint32_t)c < cnt) {
       float4 clo = w.stage[2 * c], chi = w.stage[2 * c + 1];
       float t0 = box_enter(r, inv, clo, chi);
-      bool w2 = want && t0 != __builtin_inff() &&
-                (ANY || !(best != __builtin_inff() && rt_prune(t0, r.dlen, best, r.eps)));
-      if (__ballot(w2) != 0) hitmask |= 1u << c;
+      bool w2 = want && t0 != __builtin_inff() && (ANY || !(t0 * r.dlen > limit));
+      lanes[c] = __ballot(w2);
+      if (lanes[c] != 0) hitmask |= 1u << c;
     }
   }
-  // far-to-near octant order: the nearest child ends on top of the stack
   for (int j = 7; j >= 0; --j) {
     uint32_t o = (uint32_t)j ^ dm;
     if (!(mask & (1u << o))) continue;
@@ -528,6 +569,11 @@ __device__ __forceinline__ void stage_push_children(const float4* __restrict__ n
     if (!(hitmask & (1u << c))) continue;
     if (sp < kStack2) {
       if (w.lane < 2) w.stk2[2 * sp + w.lane] = w.stage[2 * c + w.lane];
+      uint64_t lm = 0;
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        if ((uint32_t)k == c) lm = lanes[k];
+      if (w.lane == 0) w.stkm[sp] = lm;
       sp++;
     } else if (w.lane == 0) {
       wc.overflow++;  // RT_EDEPTH, never silent
@@ -547,30 +593,42 @@ __device__ void staged_closest(const KParams& p, const Ray& r, bool act, Best& b
   int sp = 0;
   __syncthreads();
   if (w.lane < 2) w.stk2[w.lane] = node[w.lane];
+  if (w.lane == 0) w.stkm[0] = am;
   sp = 1;
+  float limit = rt_prune_limit(b.dist, r.eps);
   while (sp > 0) {
     --sp;
     __syncthreads();
     float4 lo = w.stk2[2 * sp], hi = w.stk2[2 * sp + 1];
+    uint64_t lm = w.stkm[sp];
     uint32_t first = uni(__float_as_uint(lo.w)), info = uni(__float_as_uint(hi.w));
-    float tn = box_enter(r, inv, lo, hi);
-    bool want = act && tn != __builtin_inff() &&
-                !(b.dist != __builtin_inff() && rt_prune(tn, r.dlen, b.dist, r.eps));
+    bool leaf = (info & RT_NODE_LEAF) != 0;
+    uint32_t cnt = leaf ? RT_LEAF_COUNT(info) : RT_NODE_COUNT(info);
+    // issue the node's payload fetch now; its latency overlaps the re-test
+    Fetch f = leaf ? fetch_issue(tri + 3 * (size_t)first, 3 * (int)chunk(cnt, 0), w.lane)
+                   : fetch_issue(node + 2 * (size_t)first, 2 * (int)cnt, w.lane);
+    // lanes that wanted it when pushed, re-tested against their best so far
+    bool want = ((lm >> w.lane) & 1) != 0;
+    if (want && b.dist != __builtin_inff()) {
+      float tn = box_enter(r, inv, lo, hi);
+      want = !(tn * r.dlen > limit);
+    }
     if (__ballot(want) == 0) continue;
     if (COUNT && w.lane == 0) wc.nodes++;
-    if (info & RT_NODE_LEAF) {
-      uint32_t cnt = RT_LEAF_COUNT(info);
+    fetch_commit(f, w);
+    if (leaf) {
       for (uint32_t base = 0; base < cnt; base += kStage / 3) {
-        uint32_t m = cnt - base < (uint32_t)(kStage / 3) ? cnt - base : (uint32_t)(kStage / 3);
-        stage_load(tri + 3 * (size_t)(first + base), 3 * (int)m, w);
+        uint32_t m = chunk(cnt, base);
+        if (base) stage_load(tri + 3 * (size_t)(first + base), 3 * (int)m, w);
         for (uint32_t k = 0; k < m; k++) {
           float4 q0 = w.stage[3 * k], q1 = w.stage[3 * k + 1], q2 = w.stage[3 * k + 2];
           if (want) consider(r, q0, q1, q2, b);
         }
       }
+      limit = rt_prune_limit(b.dist, r.eps);
       if (COUNT && w.lane == 0) wc.tris += cnt;
     } else {
-      stage_push_children<false>(node, r, inv, dm, first, info, want, b.dist, sp, w, wc);
+      stage_push_children<false>(r, inv, dm, info, want, limit, sp, w, wc);
     }
   }
 }
@@ -587,19 +645,23 @@ __device__ bool staged_any(const KParams& p, const Ray& r, bool act, WaveCtx& w,
   int sp = 0;
   __syncthreads();
   if (w.lane < 2) w.stk2[w.lane] = node[w.lane];
+  if (w.lane == 0) w.stkm[0] = am;
   sp = 1;
   while (sp > 0) {
     --sp;
     __syncthreads();
     float4 lo = w.stk2[2 * sp], hi = w.stk2[2 * sp + 1];
+    uint64_t lm = w.stkm[sp];
     uint32_t first = uni(__float_as_uint(lo.w)), info = uni(__float_as_uint(hi.w));
-    bool want = alive && box_enter(r, inv, lo, hi) != __builtin_inff();
+    // any-hit has no pruning: the lanes that wanted the node when it was
+    // pushed and still search want it now (no re-test)
+    bool want = alive && ((lm >> w.lane) & 1) != 0;
     if (__ballot(want) == 0) continue;
     if (COUNT && w.lane == 0) wc.nodes++;
     if (info & RT_NODE_LEAF) {
       uint32_t cnt = RT_LEAF_COUNT(info);
       for (uint32_t base = 0; base < cnt && __ballot(want) != 0; base += kStage / 3) {
-        uint32_t m = cnt - base < (uint32_t)(kStage / 3) ? cnt - base : (uint32_t)(kStage / 3);
+        uint32_t m = chunk(cnt, base);
         stage_load(tri + 3 * (size_t)(first + base), 3 * (int)m, w);
         if (COUNT && w.lane == 0) wc.tris += m;
         for (uint32_t k = 0; k < m; k++) {
@@ -614,7 +676,8 @@ __device__ bool staged_any(const KParams& p, const Ray& r, bool act, WaveCtx& w,
       }
       if (__ballot(alive) == 0) break;
     } else {
-      stage_push_children<true>(node, r, inv, dm, first, info, want, 0.0f, sp, w, wc);
+      stage_load(node + 2 * (size_t)first, 2 * (int)RT_NODE_COUNT(info), w);
+      stage_push_children<true>(r, inv, dm, info, want, 0.0f, sp, w, wc);
     }
   }
   return hit;
@@ -780,6 +843,7 @@ __global__ __launch_bounds__(64, MINW) void render_kernel(KParams p) {
   __shared__ uint32_t s_ws[ACCEL == RT_ACCEL_FLAT_D ? 1 : kWaveStack];
   __shared__ float4 s_stk2[ACCEL == RT_ACCEL_FLAT_D ? 1 : 2 * kStack2];
   __shared__ float4 s_stage[kStage];
+  __shared__ uint64_t s_stkm[ACCEL == RT_ACCEL_FLAT_D ? 1 : kStack2];
   Stack stk;
   stk.idx = s_idx;
   stk.tt = s_t;
@@ -789,6 +853,7 @@ __global__ __launch_bounds__(64, MINW) void render_kernel(KParams p) {
   WaveCtx w;
   w.ws = s_ws;
   w.stk2 = s_stk2;
+  w.stkm = s_stkm;
   w.stage = s_stage;
   w.lane = lane;
   for (;;) {

@@ -21,6 +21,22 @@
 
 typedef struct { float dist; uint32_t prim; rt_vec3 pt; } winner;
 
+/* the device walk's box test and prune rule (csrc/rt_render.hip box_enter,
+ * rt_prune), on the shared rt_cull.h arithmetic */
+static float probe_box_enter(rt_vec3 o, rt_vec3 inv, float eps, float lx, float ly, float lz,
+                             float hx, float hy, float hz)
+{
+  float t;
+  int hit = rt_box_hit(o.x + eps, o.y + eps, o.z + eps, o.x - eps, o.y - eps, o.z - eps, inv.x,
+                       inv.y, inv.z, lx, ly, lz, hx, hy, hz, &t);
+  return hit ? t : INFINITY;
+}
+
+static int rt_prune(float t_enter, float dlen, float best, float eps)
+{
+  return t_enter * dlen > rt_prune_limit(best, eps);
+}
+
 static int mt_exact(rt_vec3 o, rt_vec3 d, const float *r, float *t, float *u, float *v)
 {
   const float eps = 0.0000001f;
@@ -67,11 +83,11 @@ static int probe_any(const rt_flat_scene *f, rt_vec3 o, rt_vec3 d, float eps, ui
 {
   float dlen = rt_v_length(d);
   rt_vec3 nd = { d.x / dlen, d.y / dlen, d.z / dlen };
-  rt_vec3 inv = { 1.0f / d.x, 1.0f / d.y, 1.0f / d.z };
+  rt_vec3 inv = { rt_inv(d.x), rt_inv(d.y), rt_inv(d.z) };
   uint32_t dm = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
   const float *rn = f->node;
   int sp = 0;
-  if (rt_box_enter(o.x, o.y, o.z, inv.x, inv.y, inv.z, eps, rn[0], rn[1], rn[2], rn[4], rn[5],
+  if (probe_box_enter(o, inv, eps,rn[0], rn[1], rn[2], rn[4], rn[5],
                    rn[6]) != INFINITY)
     stk[sp++] = 0;
   while (sp > 0)
@@ -101,7 +117,7 @@ static int probe_any(const rt_flat_scene *f, rt_vec3 o, rt_vec3 d, float eps, ui
         continue;
       uint32_t ci = first + (uint32_t)__builtin_popcount(mask & ((1u << oc) - 1u));
       const float *cn = f->node + RT_NODE_FLOATS * (size_t)ci;
-      if (rt_box_enter(o.x, o.y, o.z, inv.x, inv.y, inv.z, eps, cn[0], cn[1], cn[2], cn[4], cn[5],
+      if (probe_box_enter(o, inv, eps,cn[0], cn[1], cn[2], cn[4], cn[5],
                        cn[6]) != INFINITY && sp < 4096)
         stk[sp++] = ci;
     }
@@ -276,12 +292,12 @@ int rt_accel_probe(const rt_scene *s, int accel, int sample_stride, int check,
         }
         else
         {
-          rt_vec3 inv = { 1.0f / d.x, 1.0f / d.y, 1.0f / d.z };
+          rt_vec3 inv = { rt_inv(d.x), rt_inv(d.y), rt_inv(d.z) };
           uint32_t dm = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
           float eps = rt_cull_eps(eps_rel, o.x - sc[0], o.y - sc[1], o.z - sc[2], cmag, sr);
           int sp = 0;
           const float *rn = f.node;
-          float t0 = rt_box_enter(o.x, o.y, o.z, inv.x, inv.y, inv.z, eps, rn[0], rn[1], rn[2],
+          float t0 = probe_box_enter(o, inv, eps,rn[0], rn[1], rn[2],
                                   rn[4], rn[5], rn[6]);
           if (t0 != INFINITY)
           {
@@ -319,7 +335,7 @@ int rt_accel_probe(const rt_scene *s, int accel, int sample_stride, int check,
                   continue;
                 uint32_t ci = first + (uint32_t)__builtin_popcount(mask & ((1u << oc) - 1u));
                 const float *cn = f.node + RT_NODE_FLOATS * (size_t)ci;
-                float tc = rt_box_enter(o.x, o.y, o.z, inv.x, inv.y, inv.z, eps, cn[0], cn[1],
+                float tc = probe_box_enter(o, inv, eps,cn[0], cn[1],
                                         cn[2], cn[4], cn[5], cn[6]);
                 if (tc == INFINITY)
                   continue;

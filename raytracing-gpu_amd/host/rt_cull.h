@@ -12,10 +12,10 @@
  *
  * Culling (DESIGN.md "Conservative culling"): a box is grown by a per-ray
  * world-space slack eps that covers the float error of the reference's
- * Moller-Trumbore accept decision (cpu/hit.c:15-33, error ~ |o - v0| ulps),
- * and the slab interval by a relative slack covering the slab arithmetic.
- * A node is pruned only when its (grown) entry distance exceeds the current
- * best new_dist by more than 2 eps.
+ * well-conditioned Moller-Trumbore accept decisions (cpu/hit.c:15-33, error
+ * ~ |o - v0| ulps) and the rounding of the slab test itself.  A node is
+ * pruned only when its (grown) entry distance exceeds the current best
+ * new_dist by more than 2 eps.
  */
 #ifndef RT_CULL_H
 #define RT_CULL_H
@@ -46,31 +46,40 @@ RT_CULL_FN float rt_cull_eps(float eps_rel, float dx, float dy, float dz, float 
   return eps_rel * (m + R) + RT_CULL_PLANE * (cmag + R) + 1e-6f;
 }
 
-/* Slab test of the ray o + t d against [lo - eps, hi + eps]; inv = 1/d
- * component-wise.  Returns the entry parameter, or +inf when the (slack-
- * widened) interval is empty or lies behind the origin. */
-RT_CULL_FN float rt_box_enter(float ox, float oy, float oz, float ix, float iy, float iz,
-                              float eps, float lx, float ly, float lz, float hx, float hy,
-                              float hz)
+/* Per-ray slab constants: inv = 1/d with zero components clamped to a huge
+ * finite value of the same sign (no 0 * inf NaN in the slab products; the
+ * slab of an axis the ray is parallel to then reads "inside" or "never"
+ * exactly as the geometry says), oh = o + eps, ol = o - eps. */
+RT_CULL_FN float rt_inv(float d)
 {
-  float tx0 = (lx - eps - ox) * ix, tx1 = (hx + eps - ox) * ix;
-  float ty0 = (ly - eps - oy) * iy, ty1 = (hy + eps - oy) * iy;
-  float tz0 = (lz - eps - oz) * iz, tz1 = (hz + eps - oz) * iz;
-  float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
-  float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
-  /* NaN (0 * inf on an axis-parallel ray exactly on a slab plane) makes
-   * fminf/fmaxf pick the other operand: the axis is then "inside". */
-  float s = RT_CULL_TREL * fminf(fmaxf(fabsf(tmin), fabsf(tmax)), 1e30f);
-  if (tmax + s < fmaxf(tmin, 0.0f) - s)
-    return INFINITY;
-  return tmin;
+  float i = 1.0f / d;
+  return fabsf(i) < 1e30f ? i : copysignf(1e30f, d);
 }
 
-/* 1 = the node (entry parameter t_enter) cannot hold a triangle whose
- * new_dist is <= best. */
-RT_CULL_FN int rt_prune(float t_enter, float dlen, float best, float eps)
+/* Slab test of the ray o + t d against [lo - eps, hi + eps]:
+ * (lo - eps - o) is evaluated as lo - oh, (hi + eps - o) as hi - ol.  Their
+ * rounding, and that of the products, is a few ulps of |o| + |t d|, far below
+ * eps (>= 64 ulps of the origin-to-scene distance plus 4 ulps of the scene's
+ * own coordinates), so no parametric slack is needed.  Returns 1 when the
+ * interval [tmin, tmax] reaches t >= 0; *tmin = entry parameter. */
+RT_CULL_FN int rt_box_hit(float ohx, float ohy, float ohz, float olx, float oly, float olz,
+                          float ix, float iy, float iz, float lx, float ly, float lz, float hx,
+                          float hy, float hz, float *tmin_out)
 {
-  return t_enter * dlen > best + best * RT_CULL_TREL + 2.0f * eps;
+  float tx0 = (lx - ohx) * ix, tx1 = (hx - olx) * ix;
+  float ty0 = (ly - ohy) * iy, ty1 = (hy - oly) * iy;
+  float tz0 = (lz - ohz) * iz, tz1 = (hz - olz) * iz;
+  float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
+  float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+  *tmin_out = tmin;
+  return tmax >= fmaxf(tmin, 0.0f);
+}
+
+/* A node whose entry parameter t_enter satisfies t_enter * |d| > limit cannot
+ * hold a triangle whose new_dist is <= best (limit = +inf without a best). */
+RT_CULL_FN float rt_prune_limit(float best, float eps)
+{
+  return best + best * RT_CULL_TREL + 2.0f * eps;
 }
 
 #endif
