@@ -16,7 +16,8 @@
 // per-lane global overflow area of the traversal stack (entries beyond LDS)
 #define RT_SPILL_STACK 112
 
-// per-lane counters (32-bit per lane; widened to 64-bit in the wave reduction)
+// wave-total counters (wave-uniform, so they live in SGPRs; 32-bit per wave,
+// widened to 64-bit by the final atomics)
 struct WorkCount {
   uint32_t closest, shadow, pixels, nodes, tris, overflow, zero_normal, hits;
 };

@@ -161,7 +161,28 @@ struct Stack {
   int sp;
 };
 
-__device__ __forceinline__ void push(Stack& s, uint32_t i, float t, WorkCount& wc) {
+// Counters of one lane's own walk (divergent code); folded into the wave's
+// WorkCount after the walk (absorb).
+struct LaneCount {
+  uint32_t nodes, tris, overflow;
+};
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+  return __builtin_amdgcn_readfirstlane(x);
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void absorb(WorkCount& wc, const LaneCount& lc) {
+  if (COUNT) {
+    wc.nodes += wave_sum(lc.nodes);
+    wc.tris += wave_sum(lc.tris);
+  }
+  wc.overflow += wave_sum(lc.overflow);
+}
+
+__device__ __forceinline__ void push(Stack& s, uint32_t i, float t, LaneCount& wc) {
   if (s.sp < kLdsStack) {
     s.idx[s.sp * 64 + s.lane] = i;
     s.tt[s.sp * 64 + s.lane] = t;
@@ -211,7 +232,7 @@ __device__ __forceinline__ uint32_t near_octant(f3 d) {
 template <bool CLOSEST>
 __device__ __forceinline__ void push_children(const float4* __restrict__ node, const Ray& r, f3 inv,
                                               uint32_t dm, uint32_t first, uint32_t info,
-                                              float best, Stack& s, WorkCount& wc) {
+                                              float best, Stack& s, LaneCount& wc) {
   uint32_t mask = RT_NODE_MASK(info);
 #pragma unroll 1
   for (int j = 7; j >= 0; --j) {
@@ -227,7 +248,7 @@ __device__ __forceinline__ void push_children(const float4* __restrict__ node, c
 }
 
 template <bool COUNT>
-__device__ void oct_closest(const KParams& p, const Ray& r, Best& b, Stack& s, WorkCount& wc) {
+__device__ void oct_closest(const KParams& p, const Ray& r, Best& b, Stack& s, LaneCount& wc) {
   const float4* __restrict__ node = p.node;
   const float4* __restrict__ tri = p.tri;
   f3 inv = inv_dir(r.d);
@@ -259,7 +280,7 @@ __device__ void oct_closest(const KParams& p, const Ray& r, Best& b, Stack& s, W
 }
 
 template <bool COUNT>
-__device__ bool oct_any(const KParams& p, const Ray& r, Stack& s, WorkCount& wc) {
+__device__ bool oct_any(const KParams& p, const Ray& r, Stack& s, LaneCount& wc) {
   const float4* __restrict__ node = p.node;
   const float4* __restrict__ tri = p.tri;
   f3 inv = inv_dir(r.d);
@@ -354,7 +375,7 @@ __device__ void packet_closest(const KParams& p, const Ray& r, bool act, Best& b
                 !(b.dist != __builtin_inff() && rt_prune(tn, r.dlen, b.dist, r.eps));
     if (__ballot(want) == 0) continue;
     uint32_t first = __float_as_uint(lo.w), info = __float_as_uint(hi.w);
-    if (COUNT && lane == 0) wc.nodes++;
+    if (COUNT) wc.nodes++;
     if (info & RT_NODE_LEAF) {
       uint32_t cnt = RT_LEAF_COUNT(info);
       for (uint32_t k = 0; k < cnt; k++) {
@@ -362,7 +383,7 @@ __device__ void packet_closest(const KParams& p, const Ray& r, bool act, Best& b
         float4 q0 = ldu(q, 0), q1 = ldu(q, 1), q2 = ldu(q, 2);
         if (want) consider(r, q0, q1, q2, b);
       }
-      if (COUNT && lane == 0) wc.tris += cnt;
+      if (COUNT) wc.tris += cnt;
     } else {
       uint32_t mask = RT_NODE_MASK(info);
       for (int j = 7; j >= 0; --j) {
@@ -377,7 +398,7 @@ __device__ void packet_closest(const KParams& p, const Ray& r, bool act, Best& b
         if (__ballot(w2) != 0) {
           if (sp < kWaveStack)
             ws[sp++] = ci;
-          else if (lane == 0)
+          else
             wc.overflow++;  // RT_EDEPTH, never silent
         }
       }
@@ -404,13 +425,13 @@ __device__ bool packet_any(const KParams& p, const Ray& r, bool act, uint32_t* w
     bool want = alive && box_enter(r, inv, lo, hi) != __builtin_inff();
     if (__ballot(want) == 0) continue;
     uint32_t first = __float_as_uint(lo.w), info = __float_as_uint(hi.w);
-    if (COUNT && lane == 0) wc.nodes++;
+    if (COUNT) wc.nodes++;
     if (info & RT_NODE_LEAF) {
       uint32_t cnt = RT_LEAF_COUNT(info);
       for (uint32_t k = 0; k < cnt; k++) {
         const float4* q = tri + 3 * (size_t)(first + k);
         float4 q0 = ldu(q, 0), q1 = ldu(q, 1), q2 = ldu(q, 2);
-        if (COUNT && lane == 0) wc.tris++;
+        if (COUNT) wc.tris++;
         if (want && any_hit_rec(r, q0, q1, q2)) {
           hit = true;
           alive = false;
@@ -431,7 +452,7 @@ __device__ bool packet_any(const KParams& p, const Ray& r, bool act, uint32_t* w
         if (__ballot(w2) != 0) {
           if (sp < kWaveStack)
             ws[sp++] = ci;
-          else if (lane == 0)
+          else
             wc.overflow++;
         }
       }
@@ -476,13 +497,18 @@ __device__ __forceinline__ Fetch fetch_issue(const float4* __restrict__ src, int
   return f;
 }
 
+// The workgroup is one wave and a wave's LDS instructions execute in issue
+// order, so staging needs no s_barrier: only a compiler barrier that keeps
+// the LDS reads and writes in source order.
+__device__ __forceinline__ void wave_sync() { __asm__ volatile("" ::: "memory"); }
+
 __device__ __forceinline__ void fetch_commit(const Fetch& f, WaveCtx& w) {
   const int l = w.lane;
-  __syncthreads();  // one-wave workgroup: orders the previous readers of stage
+  wave_sync();  // after the previous readers of stage
   if (l < f.n) w.stage[l] = f.v0;
   if (l + 64 < f.n) w.stage[l + 64] = f.v1;
   if (l + 128 < f.n) w.stage[l + 128] = f.v2;
-  __syncthreads();
+  wave_sync();
 }
 
 __device__ __forceinline__ void stage_load(const float4* __restrict__ src, int n, WaveCtx& w) {
@@ -508,12 +534,18 @@ __device__ void flat_closest_w(const KParams& p, const Ray& r, bool act, Best& b
     fetch_commit(f, w);
     uint32_t nb = base + kStage / 3;
     if (nb < n) f = fetch_issue(p.tri + 3 * (size_t)nb, 3 * (int)chunk(n, nb), w.lane);
+    // software-pipelined: record k+1's LDS reads are in flight while k is tested
+    float4 n0 = w.stage[0], n1 = w.stage[1], n2 = w.stage[2];
     for (uint32_t k = 0; k < m; k++) {
-      float4 q0 = w.stage[3 * k], q1 = w.stage[3 * k + 1], q2 = w.stage[3 * k + 2];
+      float4 q0 = n0, q1 = n1, q2 = n2;
+      uint32_t kn = k + 1 < m ? 3 * (k + 1) : 0;
+      n0 = w.stage[kn];
+      n1 = w.stage[kn + 1];
+      n2 = w.stage[kn + 2];
       if (act) consider(r, q0, q1, q2, b);
     }
   }
-  if (COUNT && w.lane == 0) wc.tris += n;
+  if (COUNT) wc.tris += n;
 }
 
 template <bool COUNT>
@@ -527,9 +559,14 @@ __device__ bool flat_any_w(const KParams& p, const Ray& r, bool act, WaveCtx& w,
     fetch_commit(f, w);
     uint32_t nb = base + kStage / 3;
     if (nb < n) f = fetch_issue(p.tri + 3 * (size_t)nb, 3 * (int)chunk(n, nb), w.lane);
-    if (COUNT && w.lane == 0) wc.tris += m;
+    if (COUNT) wc.tris += m;
+    float4 n0 = w.stage[0], n1 = w.stage[1], n2 = w.stage[2];
     for (uint32_t k = 0; k < m; k++) {
-      float4 q0 = w.stage[3 * k], q1 = w.stage[3 * k + 1], q2 = w.stage[3 * k + 2];
+      float4 q0 = n0, q1 = n1, q2 = n2;
+      uint32_t kn = k + 1 < m ? 3 * (k + 1) : 0;
+      n0 = w.stage[kn];
+      n1 = w.stage[kn + 1];
+      n2 = w.stage[kn + 2];
       if (alive && any_hit_rec(r, q0, q1, q2)) {
         hit = true;
         alive = false;
@@ -575,7 +612,7 @@ __device__ __forceinline__ void stage_push_children(const Ray& r, f3 inv, uint32
         if ((uint32_t)k == c) lm = lanes[k];
       if (w.lane == 0) w.stkm[sp] = lm;
       sp++;
-    } else if (w.lane == 0) {
+    } else {
       wc.overflow++;  // RT_EDEPTH, never silent
     }
   }
@@ -591,14 +628,14 @@ __device__ void staged_closest(const KParams& p, const Ray& r, bool act, Best& b
   f3 inv = inv_dir(r.d);
   uint32_t dm = wave_near_octant(act, r.d, am);
   int sp = 0;
-  __syncthreads();
+  wave_sync();
   if (w.lane < 2) w.stk2[w.lane] = node[w.lane];
   if (w.lane == 0) w.stkm[0] = am;
   sp = 1;
   float limit = rt_prune_limit(b.dist, r.eps);
   while (sp > 0) {
     --sp;
-    __syncthreads();
+    wave_sync();
     float4 lo = w.stk2[2 * sp], hi = w.stk2[2 * sp + 1];
     uint64_t lm = w.stkm[sp];
     uint32_t first = uni(__float_as_uint(lo.w)), info = uni(__float_as_uint(hi.w));
@@ -614,7 +651,7 @@ __device__ void staged_closest(const KParams& p, const Ray& r, bool act, Best& b
       want = !(tn * r.dlen > limit);
     }
     if (__ballot(want) == 0) continue;
-    if (COUNT && w.lane == 0) wc.nodes++;
+    if (COUNT) wc.nodes++;
     fetch_commit(f, w);
     if (leaf) {
       for (uint32_t base = 0; base < cnt; base += kStage / 3) {
@@ -626,7 +663,7 @@ __device__ void staged_closest(const KParams& p, const Ray& r, bool act, Best& b
         }
       }
       limit = rt_prune_limit(b.dist, r.eps);
-      if (COUNT && w.lane == 0) wc.tris += cnt;
+      if (COUNT) wc.tris += cnt;
     } else {
       stage_push_children<false>(r, inv, dm, info, want, limit, sp, w, wc);
     }
@@ -643,13 +680,13 @@ __device__ bool staged_any(const KParams& p, const Ray& r, bool act, WaveCtx& w,
   f3 inv = inv_dir(r.d);
   uint32_t dm = wave_near_octant(act, r.d, am);
   int sp = 0;
-  __syncthreads();
+  wave_sync();
   if (w.lane < 2) w.stk2[w.lane] = node[w.lane];
   if (w.lane == 0) w.stkm[0] = am;
   sp = 1;
   while (sp > 0) {
     --sp;
-    __syncthreads();
+    wave_sync();
     float4 lo = w.stk2[2 * sp], hi = w.stk2[2 * sp + 1];
     uint64_t lm = w.stkm[sp];
     uint32_t first = uni(__float_as_uint(lo.w)), info = uni(__float_as_uint(hi.w));
@@ -657,13 +694,13 @@ __device__ bool staged_any(const KParams& p, const Ray& r, bool act, WaveCtx& w,
     // pushed and still search want it now (no re-test)
     bool want = alive && ((lm >> w.lane) & 1) != 0;
     if (__ballot(want) == 0) continue;
-    if (COUNT && w.lane == 0) wc.nodes++;
+    if (COUNT) wc.nodes++;
     if (info & RT_NODE_LEAF) {
       uint32_t cnt = RT_LEAF_COUNT(info);
       for (uint32_t base = 0; base < cnt && __ballot(want) != 0; base += kStage / 3) {
         uint32_t m = chunk(cnt, base);
         stage_load(tri + 3 * (size_t)(first + base), 3 * (int)m, w);
-        if (COUNT && w.lane == 0) wc.tris += m;
+        if (COUNT) wc.tris += m;
         for (uint32_t k = 0; k < m; k++) {
           float4 q0 = w.stage[3 * k], q1 = w.stage[3 * k + 1], q2 = w.stage[3 * k + 2];
           if (want && any_hit_rec(r, q0, q1, q2)) {
@@ -705,23 +742,30 @@ __device__ __forceinline__ void closest_q(const KParams& p, const Ray& r, bool a
     staged_closest<COUNT>(p, r, act, b, w, wc);
   else if (p.trav == RT_TRAV_PACKET || (p.trav == RT_TRAV_HYBRID && many))
     packet_closest<COUNT>(p, r, act, b, w.ws, w.lane, wc);
-  else if (act)
-    oct_closest<COUNT>(p, r, b, s, wc);
+  else {
+    LaneCount lc = {0, 0, 0};
+    if (act) oct_closest<COUNT>(p, r, b, s, lc);
+    absorb<COUNT>(wc, lc);
+  }
 }
 
 // Shadow query (collide_dist > 0.01, cpu/light.c:24-31); converged call.
 template <int ACCEL, bool COUNT>
 __device__ __forceinline__ bool shadow_q(const KParams& p, f3 o, f3 d, bool act, Stack& s,
                                          WaveCtx& w, WorkCount& wc) {
-  if (act) wc.shadow++;
+  uint64_t am = __ballot(act);
+  wc.shadow += (uint32_t)__popcll(am);
   Ray r = make_ray(p, o, d);
   if (ACCEL == RT_ACCEL_FLAT_D) return flat_any_w<COUNT>(p, r, act, w, wc);
-  bool many = __popcll(__ballot(act)) >= p.packet_min;
+  bool many = __popcll(am) >= p.packet_min;
   if (p.trav == RT_TRAV_STAGED || (p.trav == RT_TRAV_STAGED_HYBRID && many))
     return staged_any<COUNT>(p, r, act, w, wc);
   if (p.trav == RT_TRAV_PACKET || (p.trav == RT_TRAV_HYBRID && many))
     return packet_any<COUNT>(p, r, act, w.ws, w.lane, wc);
-  return act && oct_any<COUNT>(p, r, s, wc);
+  LaneCount lc = {0, 0, 0};
+  bool hit = act && oct_any<COUNT>(p, r, s, lc);
+  absorb<COUNT>(wc, lc);
+  return hit;
 }
 
 // cpu/light.c:7-22
@@ -791,8 +835,9 @@ __device__ col trace_path(const KParams& p, bool valid, f3 o, f3 d, Stack& s, Wa
   bool alive = valid;
   for (;;) {
     alive = alive && !((double)coef < 0.01);  // checked before the query
-    if (__ballot(alive) == 0) break;
-    if (alive) wc.closest++;
+    uint64_t am = __ballot(alive);
+    if (am == 0) break;
+    wc.closest += (uint32_t)__popcll(am);  // wave-uniform counters (SGPRs)
     Ray r = make_ray(p, o, d);
     Best b;
     b.dist = __builtin_inff();
@@ -804,22 +849,23 @@ __device__ col trace_path(const KParams& p, bool valid, f3 o, f3 d, Stack& s, Wa
     closest_q<ACCEL, COUNT>(p, r, alive, b, s, w, wc);
     bool hit = alive && b.dist != __builtin_inff();
     f3 N = f3{0.0f, 0.0f, 0.0f};
+    wc.hits += (uint32_t)__popcll(__ballot(hit));
+    bool zero = false;
     if (hit) {
-      wc.hits++;
       const float* nm = p.nrm + 9 * (size_t)b.prim;
       float w0 = 1.0f - b.u - b.v;
       N = add(add(scale(ld3(nm), w0), scale(ld3(nm + 3), b.u)), scale(ld3(nm + 6), b.v));
-      if (is_zero(N)) {  // cpu/hit.c:79 would skip this object; see DESIGN.md
-        wc.zero_normal++;
-        hit = false;
-      }
+      zero = is_zero(N);  // cpu/hit.c:79 would skip this object; see DESIGN.md
     }
+    wc.zero_normal += (uint32_t)__popcll(__ballot(zero));
+    hit = hit && !zero;
     const float* m = p.mat + RT_MAT_FLOATS_D * (hit ? b.obj : 0u);
     col local = apply_light<ACCEL, COUNT>(p, hit, m, b.pt, N, s, w, wc);
     alive = hit;
+    bool deep = hit && depth == kMaxDepth;
+    wc.overflow += (uint32_t)__popcll(__ballot(deep));
     if (hit) {
-      if (depth == kMaxDepth) {
-        wc.overflow++;
+      if (deep) {
         alive = false;
       } else {
         terms[depth++] = color_mul(local, coef);
@@ -870,7 +916,7 @@ __global__ __launch_bounds__(64, MINW) void render_kernel(KParams p) {
                  jj <= 2 * (p.H / 2);
     int i = ii - p.W / 2, j = jj - p.H / 2;
     col acc = init_color(0.0f, 0.0f, 0.0f);
-    if (valid) wc.pixels++;
+    wc.pixels += (uint32_t)__popcll(__ballot(valid));
     // for (float k = i; k < i + 1; k += 0.5) for (float l = j; ...)  (cpu/raytracer.c:55-58)
     for (int sk = 0; sk < 2; sk++) {
       float k = (float)i + 0.5f * (float)sk;
@@ -888,16 +934,12 @@ __global__ __launch_bounds__(64, MINW) void render_kernel(KParams p) {
     out[1] = acc.g;
     out[2] = acc.b;
   }
-  // wave-reduce the counters, one atomic per wave
+  // the counters are wave totals already: one atomic per counter per wave
   uint32_t v[8] = {wc.closest, wc.shadow,   wc.pixels,      wc.nodes,
                    wc.tris,    wc.overflow, wc.zero_normal, wc.hits};
 #pragma unroll
-  for (int k = 0; k < 8; k++) {
-    unsigned long long x = (unsigned long long)v[k];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
-    if (lane == 0 && x) atomicAdd(p.stats + k, x);
-  }
+  for (int k = 0; k < 8; k++)
+    if (lane == 0 && v[k]) atomicAdd(p.stats + k, (unsigned long long)v[k]);
 }
 
 // tiles of all ranks (rank-major, as gathered) -> PPM-order image
