@@ -15,6 +15,13 @@
 #define RT_NSTATS 8
 // per-lane global overflow area of the traversal stack (entries beyond LDS)
 #define RT_SPILL_STACK 112
+// tile bands and their counters in KParams::tile_counter (<= 16).  Measured
+// (C5): 8 bands, one per XCD, ran 13 % slower than 1 -- one scanline-ordered
+// band keeps all 8 XCDs on the same few tile rows, whose geometry then stays
+// in the Infinity Cache; 8 stripes at once multiply that working set.
+#ifndef RT_BANDS
+#define RT_BANDS 1
+#endif
 
 // wave-total counters (wave-uniform, so they live in SGPRs; 32-bit per wave,
 // widened to 64-bit by the final atomics)

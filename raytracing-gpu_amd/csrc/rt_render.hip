@@ -902,11 +902,25 @@ __global__ __launch_bounds__(64, MINW) void render_kernel(KParams p) {
   w.stkm = s_stkm;
   w.stage = s_stage;
   w.lane = lane;
+  // Tile scheduling: the rank's tiles are cut into RT_BANDS contiguous bands
+  // (image stripes); workgroup b starts on band b % RT_BANDS and moves on to
+  // the other bands when its own is drained.  Default one band: every wave
+  // pulls the next tile in scanline order (rt_kernels.h says why).
+  const uint32_t nt = (uint32_t)p.ntiles_local;
+  const uint32_t home = (uint32_t)blockIdx.x % RT_BANDS;
+  uint32_t probe = 0;
   for (;;) {
+    uint32_t band = (home + probe) % RT_BANDS;
+    uint32_t lo = (uint32_t)(((uint64_t)nt * band) / RT_BANDS);
+    uint32_t hi = (uint32_t)(((uint64_t)nt * (band + 1)) / RT_BANDS);
     uint32_t t = 0;
-    if (lane == 0) t = atomicAdd(p.tile_counter, 1u);
-    t = __shfl(t, 0);
-    if (t >= (uint32_t)p.ntiles_local) break;
+    if (lane == 0) t = atomicAdd(p.tile_counter + band, 1u);
+    t = uni(t);
+    if (t >= hi - lo) {
+      if (++probe == RT_BANDS) break;  // every band drained: the wave exits
+      continue;
+    }
+    t += lo;
     uint32_t g = t * (uint32_t)p.nranks + (uint32_t)p.rank;  // global tile index
     int ty = (int)(g / (uint32_t)p.tiles_x), tx = (int)(g % (uint32_t)p.tiles_x);
     int pr = ty * 8 + (lane >> 3), pc = tx * 8 + (lane & 7);
