@@ -150,7 +150,10 @@ __device__ __forceinline__ bool any_hit_rec(const Ray& r, const float4& q0, cons
 // Per-lane traversal stack: the first kLdsStack entries live in LDS, laid
 // out [entry][lane] so every lane hits its own bank; deeper entries spill to
 // a per-lane area in global memory (rare: typical depth is < 16).
-static constexpr int kLdsStack = 4;
+#ifndef RT_LDS_STACK
+#define RT_LDS_STACK 2
+#endif
+static constexpr int kLdsStack = RT_LDS_STACK;
 static constexpr int kSpillStack = RT_SPILL_STACK;
 
 struct Stack {
@@ -469,20 +472,31 @@ __device__ bool packet_any(const KParams& p, const Ray& r, bool act, uint32_t* w
 // one memory round trip instead of one per record.  The wave stack holds the
 // pushed child's whole node record (box + first/info), so a pop needs no
 // memory access before the next fetch is issued.
-static constexpr int kStage = 192;    // float4 staging slots per wave (64 triangle records)
-static constexpr int kStack2 = 128;   // wave stack entries (2 float4 each)
+// float4 staging slots per wave: FLAT streams 64 triangle records at a time;
+// the octree walk stages one node's payload (<= 8 children, or a leaf's
+// records, RT_OCT_LEAF_CAP = 32 of them in one chunk).  LDS per one-wave
+// workgroup must stay <= 10 KB for 16 workgroups per CU.
+static constexpr int kStageFlat = 192;
+#ifndef RT_STAGE_OCT
+#define RT_STAGE_OCT 96
+#endif
+static constexpr int kStageOct = RT_STAGE_OCT;
+#ifndef RT_STACK2
+#define RT_STACK2 96
+#endif
+static constexpr int kStack2 = RT_STACK2;  // wave stack entries (2 float4 each)
 
 struct WaveCtx {
   uint32_t* ws;    // kWaveStack node indices (packet walk)
   float4* stk2;    // kStack2 x 2 float4 (staged packet walk)
   uint64_t* stkm;  // kStack2 lane masks: lanes that wanted the pushed node
-  float4* stage;   // kStage float4
+  float4* stage;   // kStageFlat / kStageOct float4
   int lane;
 };
 
 // A fetch in flight: the wave's lanes hold float4 k, k+64, k+128 of src[0, n)
 // in registers (issued early so its latency overlaps other work), then commit
-// it to the LDS stage; n <= kStage.
+// it to the LDS stage; n <= kStageFlat.
 struct Fetch {
   float4 v0, v1, v2;
   int n;
@@ -515,9 +529,12 @@ __device__ __forceinline__ void stage_load(const float4* __restrict__ src, int n
   fetch_commit(fetch_issue(src, n, w.lane), w);
 }
 
+template <int RECS>
 __device__ __forceinline__ uint32_t chunk(uint32_t n, uint32_t base) {
-  return n - base < (uint32_t)(kStage / 3) ? n - base : (uint32_t)(kStage / 3);
+  return n - base < (uint32_t)RECS ? n - base : (uint32_t)RECS;
 }
+static constexpr int kFlatRecs = kStageFlat / 3;
+static constexpr int kOctRecs = kStageOct / 3;
 
 // Brute force over every triangle record (cpu/hit.c:72-109 order-free, the
 // (new_dist, prim) key makes the winner order-independent), streamed through
@@ -528,12 +545,12 @@ __device__ void flat_closest_w(const KParams& p, const Ray& r, bool act, Best& b
                                WorkCount& wc) {
   if (__ballot(act) == 0) return;
   const uint32_t n = p.nrec;
-  Fetch f = fetch_issue(p.tri, 3 * (int)chunk(n, 0), w.lane);
-  for (uint32_t base = 0; base < n; base += kStage / 3) {
-    uint32_t m = chunk(n, base);
+  Fetch f = fetch_issue(p.tri, 3 * (int)chunk<kFlatRecs>(n, 0), w.lane);
+  for (uint32_t base = 0; base < n; base += kFlatRecs) {
+    uint32_t m = chunk<kFlatRecs>(n, base);
     fetch_commit(f, w);
-    uint32_t nb = base + kStage / 3;
-    if (nb < n) f = fetch_issue(p.tri + 3 * (size_t)nb, 3 * (int)chunk(n, nb), w.lane);
+    uint32_t nb = base + kFlatRecs;
+    if (nb < n) f = fetch_issue(p.tri + 3 * (size_t)nb, 3 * (int)chunk<kFlatRecs>(n, nb), w.lane);
     // software-pipelined: record k+1's LDS reads are in flight while k is tested
     float4 n0 = w.stage[0], n1 = w.stage[1], n2 = w.stage[2];
     for (uint32_t k = 0; k < m; k++) {
@@ -553,12 +570,12 @@ __device__ bool flat_any_w(const KParams& p, const Ray& r, bool act, WaveCtx& w,
   bool alive = act, hit = false;
   const uint32_t n = p.nrec;
   if (__ballot(alive) == 0 || n == 0) return false;
-  Fetch f = fetch_issue(p.tri, 3 * (int)chunk(n, 0), w.lane);
-  for (uint32_t base = 0; base < n; base += kStage / 3) {
-    uint32_t m = chunk(n, base);
+  Fetch f = fetch_issue(p.tri, 3 * (int)chunk<kFlatRecs>(n, 0), w.lane);
+  for (uint32_t base = 0; base < n; base += kFlatRecs) {
+    uint32_t m = chunk<kFlatRecs>(n, base);
     fetch_commit(f, w);
-    uint32_t nb = base + kStage / 3;
-    if (nb < n) f = fetch_issue(p.tri + 3 * (size_t)nb, 3 * (int)chunk(n, nb), w.lane);
+    uint32_t nb = base + kFlatRecs;
+    if (nb < n) f = fetch_issue(p.tri + 3 * (size_t)nb, 3 * (int)chunk<kFlatRecs>(n, nb), w.lane);
     if (COUNT) wc.tris += m;
     float4 n0 = w.stage[0], n1 = w.stage[1], n2 = w.stage[2];
     for (uint32_t k = 0; k < m; k++) {
@@ -642,7 +659,7 @@ __device__ void staged_closest(const KParams& p, const Ray& r, bool act, Best& b
     bool leaf = (info & RT_NODE_LEAF) != 0;
     uint32_t cnt = leaf ? RT_LEAF_COUNT(info) : RT_NODE_COUNT(info);
     // issue the node's payload fetch now; its latency overlaps the re-test
-    Fetch f = leaf ? fetch_issue(tri + 3 * (size_t)first, 3 * (int)chunk(cnt, 0), w.lane)
+    Fetch f = leaf ? fetch_issue(tri + 3 * (size_t)first, 3 * (int)chunk<kOctRecs>(cnt, 0), w.lane)
                    : fetch_issue(node + 2 * (size_t)first, 2 * (int)cnt, w.lane);
     // lanes that wanted it when pushed, re-tested against their best so far
     bool want = ((lm >> w.lane) & 1) != 0;
@@ -654,8 +671,8 @@ __device__ void staged_closest(const KParams& p, const Ray& r, bool act, Best& b
     if (COUNT) wc.nodes++;
     fetch_commit(f, w);
     if (leaf) {
-      for (uint32_t base = 0; base < cnt; base += kStage / 3) {
-        uint32_t m = chunk(cnt, base);
+      for (uint32_t base = 0; base < cnt; base += kOctRecs) {
+        uint32_t m = chunk<kOctRecs>(cnt, base);
         if (base) stage_load(tri + 3 * (size_t)(first + base), 3 * (int)m, w);
         for (uint32_t k = 0; k < m; k++) {
           float4 q0 = w.stage[3 * k], q1 = w.stage[3 * k + 1], q2 = w.stage[3 * k + 2];
@@ -697,8 +714,8 @@ __device__ bool staged_any(const KParams& p, const Ray& r, bool act, WaveCtx& w,
     if (COUNT) wc.nodes++;
     if (info & RT_NODE_LEAF) {
       uint32_t cnt = RT_LEAF_COUNT(info);
-      for (uint32_t base = 0; base < cnt && __ballot(want) != 0; base += kStage / 3) {
-        uint32_t m = chunk(cnt, base);
+      for (uint32_t base = 0; base < cnt && __ballot(want) != 0; base += kOctRecs) {
+        uint32_t m = chunk<kOctRecs>(cnt, base);
         stage_load(tri + 3 * (size_t)(first + base), 3 * (int)m, w);
         if (COUNT) wc.tris += m;
         for (uint32_t k = 0; k < m; k++) {
@@ -780,9 +797,38 @@ __device__ __forceinline__ col specular(col tmp, f3 inc_o, f3 inc_d, f3 P, f3 N,
   return color_add(tmp, k);
 }
 
-// cpu/light.c:33-100 for the lanes with hit; P = hit point, N = interpolated
-// (unnormalised) normal.  The light loop is wave-uniform so shadow queries
-// run converged.
+// Shadow-ray direction of a directional (type 1) or point (type 2) light at
+// P: cpu/light.c:53,78 (unnormalised).
+__device__ __forceinline__ f3 shadow_dir(uint32_t type, f3 lv, f3 P) {
+  return type == 1 ? scale(lv, -1.0f) : sub(lv, P);
+}
+
+// The unshadowed contribution of a directional or point light,
+// cpu/light.c:49-66 and 68-98; P = hit point, N = interpolated (unnormalised)
+// normal, m = material.
+__device__ __forceinline__ col light_lit(uint32_t type, col lc, f3 lv, const float* m, f3 P,
+                                         f3 N) {
+  if (type == 1) {  // DIRECTIONAL
+    f3 Ldir = scale(lv, -1.0f);
+    col tmp = color_mul2(lc, init_color(m[3], m[4], m[5]));
+    tmp = color_mul(tmp, dot(Ldir, N));
+    f3 inc_o = add(P, scale(lv, -10.0f));
+    return specular(tmp, inc_o, lv, P, N, m);
+  }
+  // POINT: "L" is minus the light position
+  f3 to_l = sub(lv, P);
+  f3 Lp = scale(lv, -1.0f);
+  f3 Nf = N;
+  if (dot(Lp, Nf) < 0.0f) Nf = scale(Nf, -1.0f);
+  float dist = length(sub(lv, P));
+  col tmp = color_mul2(lc, init_color(m[3], m[4], m[5]));
+  tmp = color_mul(tmp, dot(Lp, Nf) * 1.0f / dist);
+  f3 inc_o = add(P, scale(to_l, -10.0f));
+  return specular(tmp, inc_o, to_l, P, N, m);
+}
+
+// cpu/light.c:33-100 for the lanes with hit.  The light loop is wave-uniform
+// so shadow queries run converged.
 template <int ACCEL, bool COUNT>
 __device__ col apply_light(const KParams& p, bool hit, const float* m, f3 P, f3 N, Stack& s,
                            WaveCtx& w, WorkCount& wc) {
@@ -794,30 +840,9 @@ __device__ col apply_light(const KParams& p, bool hit, const float* m, f3 P, f3 
     f3 lv = f3{L[4], L[5], L[6]};
     if (type == 0) {  // AMBIENT
       if (hit) acc = color_add(acc, color_mul2(lc, init_color(m[0], m[1], m[2])));
-    } else if (type == 1) {  // DIRECTIONAL
-      f3 Ldir = scale(lv, -1.0f);
-      bool sh = shadow_q<ACCEL, COUNT>(p, P, Ldir, hit, s, w, wc);
-      if (hit && !sh) {
-        col tmp = color_mul2(lc, init_color(m[3], m[4], m[5]));
-        tmp = color_mul(tmp, dot(Ldir, N));
-        f3 inc_o = add(P, scale(lv, -10.0f));
-        tmp = specular(tmp, inc_o, lv, P, N, m);
-        acc = color_add(acc, tmp);
-      }
-    } else if (type == 2) {  // POINT: "L" is minus the light position
-      f3 to_l = sub(lv, P);
-      bool sh = shadow_q<ACCEL, COUNT>(p, P, to_l, hit, s, w, wc);
-      if (hit && !sh) {
-        f3 Lp = scale(lv, -1.0f);
-        f3 Nf = N;
-        if (dot(Lp, Nf) < 0.0f) Nf = scale(Nf, -1.0f);
-        float dist = length(sub(lv, P));
-        col tmp = color_mul2(lc, init_color(m[3], m[4], m[5]));
-        tmp = color_mul(tmp, dot(Lp, Nf) * 1.0f / dist);
-        f3 inc_o = add(P, scale(to_l, -10.0f));
-        tmp = specular(tmp, inc_o, to_l, P, N, m);
-        acc = color_add(acc, tmp);
-      }
+    } else if (type == 1 || type == 2) {
+      bool sh = shadow_q<ACCEL, COUNT>(p, P, shadow_dir(type, lv, P), hit, s, w, wc);
+      if (hit && !sh) acc = color_add(acc, light_lit(type, lc, lv, m, P, N));
     }
   }
   return acc;
@@ -827,11 +852,10 @@ __device__ col apply_light(const KParams& p, bool hit, const float* m, f3 P, f3 
 // recursion becomes a wave-uniform bounce loop; local terms are buffered and
 // folded deepest-first.  valid = the lane owns a pixel.
 template <int ACCEL, bool COUNT>
-__device__ col trace_path(const KParams& p, bool valid, f3 o, f3 d, Stack& s, WaveCtx& w,
-                          WorkCount& wc) {
+__device__ __forceinline__ col trace_path(const KParams& p, bool valid, f3 o, f3 d, float coef, Stack& s,
+                          WaveCtx& w, WorkCount& wc) {
   col terms[kMaxDepth];
   int depth = 0;
-  float coef = 1.0f;
   bool alive = valid;
   for (;;) {
     alive = alive && !((double)coef < 0.01);  // checked before the query
@@ -888,7 +912,7 @@ __global__ __launch_bounds__(64, MINW) void render_kernel(KParams p) {
   __shared__ float s_t[ACCEL == RT_ACCEL_FLAT_D ? 1 : kLdsStack * 64];
   __shared__ uint32_t s_ws[ACCEL == RT_ACCEL_FLAT_D ? 1 : kWaveStack];
   __shared__ float4 s_stk2[ACCEL == RT_ACCEL_FLAT_D ? 1 : 2 * kStack2];
-  __shared__ float4 s_stage[kStage];
+  __shared__ float4 s_stage[ACCEL == RT_ACCEL_FLAT_D ? kStageFlat : kStageOct];
   __shared__ uint64_t s_stkm[ACCEL == RT_ACCEL_FLAT_D ? 1 : kStack2];
   Stack stk;
   stk.idx = s_idx;
@@ -938,7 +962,7 @@ __global__ __launch_bounds__(64, MINW) void render_kernel(KParams p) {
         float l = (float)j + 0.5f * (float)sl;
         f3 point = add(add(p.C, scale(p.u, k)), scale(p.v, l));
         f3 dir = normalize(sub(p.pos, point));
-        col sc = trace_path<ACCEL, COUNT>(p, valid, point, dir, stk, w, wc);
+        col sc = trace_path<ACCEL, COUNT>(p, valid, point, dir, 1.0f, stk, w, wc);
         acc = color_add(acc, color_mul(sc, 0.25f));
       }
     }

@@ -20,7 +20,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(HERE, "lib")
-LIB_PATH = os.path.join(LIB_DIR, "librtgpu.so")
+LIB_PATH = os.environ.get("RTGPU_LIB") or os.path.join(LIB_DIR, "librtgpu.so")
 
 RT_ACCEL_FLAT = 0
 RT_ACCEL_OCTREE = 1
