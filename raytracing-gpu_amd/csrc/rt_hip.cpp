@@ -238,6 +238,10 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
   p.trav = tv ? std::atoi(tv) : 4;
   const char* pm = std::getenv("RT_PACKET_MIN");
   p.packet_min = pm ? std::atoi(pm) : 8;
+  const char* tvs = std::getenv("RT_TRAV_SHADOW");
+  p.trav_shadow = tvs ? std::atoi(tvs) : 0;  // measured: per-lane any-hit walks win
+  const char* pms = std::getenv("RT_PACKET_MIN_SHADOW");
+  p.packet_min_shadow = pms ? std::atoi(pms) : p.packet_min;
   if (c->accel == RT_ACCEL_OCTREE && !c->d_node) {
     // empty scene: nothing to traverse, the FLAT kernel with 0 records is exact
     HIP_TRY(hipMemsetAsync(c->d_counter, 0, 64, s));

@@ -49,6 +49,7 @@ struct KParams {
   float eps_rel;                // culling slack, rt_cull.h rt_cull_eps()
   int trav;                     // RT_TRAV_LANE / _PACKET / _HYBRID (rt_render.hip)
   int packet_min;               // hybrid: packet walk while >= this many lanes query
+  int trav_shadow, packet_min_shadow;  // the same two for shadow (any-hit) queries
 };
 
 // min_waves = occupancy target per SIMD (launch bounds of the instantiation:

@@ -151,7 +151,7 @@ __device__ __forceinline__ bool any_hit_rec(const Ray& r, const float4& q0, cons
 // out [entry][lane] so every lane hits its own bank; deeper entries spill to
 // a per-lane area in global memory (rare: typical depth is < 16).
 #ifndef RT_LDS_STACK
-#define RT_LDS_STACK 2
+#define RT_LDS_STACK 6
 #endif
 static constexpr int kLdsStack = RT_LDS_STACK;
 static constexpr int kSpillStack = RT_SPILL_STACK;
@@ -772,12 +772,15 @@ __device__ __forceinline__ bool shadow_q(const KParams& p, f3 o, f3 d, bool act,
                                          WaveCtx& w, WorkCount& wc) {
   uint64_t am = __ballot(act);
   wc.shadow += (uint32_t)__popcll(am);
+#ifdef RT_DBG_NO_SHADOW  // timing breakdown only (wrong images)
+  return false;
+#endif
   Ray r = make_ray(p, o, d);
   if (ACCEL == RT_ACCEL_FLAT_D) return flat_any_w<COUNT>(p, r, act, w, wc);
-  bool many = __popcll(am) >= p.packet_min;
-  if (p.trav == RT_TRAV_STAGED || (p.trav == RT_TRAV_STAGED_HYBRID && many))
+  bool many = __popcll(am) >= p.packet_min_shadow;
+  if (p.trav_shadow == RT_TRAV_STAGED || (p.trav_shadow == RT_TRAV_STAGED_HYBRID && many))
     return staged_any<COUNT>(p, r, act, w, wc);
-  if (p.trav == RT_TRAV_PACKET || (p.trav == RT_TRAV_HYBRID && many))
+  if (p.trav_shadow == RT_TRAV_PACKET || (p.trav_shadow == RT_TRAV_HYBRID && many))
     return packet_any<COUNT>(p, r, act, w.ws, w.lane, wc);
   LaneCount lc = {0, 0, 0};
   bool hit = act && oct_any<COUNT>(p, r, s, lc);
@@ -886,6 +889,9 @@ __device__ __forceinline__ col trace_path(const KParams& p, bool valid, f3 o, f3
     const float* m = p.mat + RT_MAT_FLOATS_D * (hit ? b.obj : 0u);
     col local = apply_light<ACCEL, COUNT>(p, hit, m, b.pt, N, s, w, wc);
     alive = hit;
+#ifdef RT_DBG_NO_BOUNCE  // timing breakdown only (wrong images)
+    alive = false;
+#endif
     bool deep = hit && depth == kMaxDepth;
     wc.overflow += (uint32_t)__popcll(__ballot(deep));
     if (hit) {

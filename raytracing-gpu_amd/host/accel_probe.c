@@ -245,7 +245,7 @@ int rt_accel_probe(const rt_scene *s, int accel, int sample_stride, int check,
     sr = fmaxf(sr, 0.5f * (f.scene_hi[a] - f.scene_lo[a]));
   }
   const char *er = getenv("RT_PROBE_EPS_ULPS");
-  const float eps_rel = (er ? (float)atof(er) : 256.0f) * 5.9604645e-8f;
+  const float eps_rel = (er ? (float)atof(er) : 64.0f) * 5.9604645e-8f;
   float cmag = fmaxf(fabsf(sc[0]), fmaxf(fabsf(sc[1]), fabsf(sc[2])));
   int W = fr.width, H = fr.height;
   uint32_t *stk = malloc(4096 * sizeof(uint32_t));

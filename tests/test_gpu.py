@@ -143,8 +143,10 @@ def test_synthetic_c5_sample(gpu):
     assert_bitexact(img[pix[:, 0], pix[:, 1]], vals, "C5 sample")
 
 
-# Traversal policies of the octree walk (env RT_TRAV, read per render; see
-# csrc/rt_render.hip): per-lane, packet, hybrid, staged packet, staged hybrid.
+# Traversal policies of the octree walk (env RT_TRAV / RT_TRAV_SHADOW for
+# closest-hit / shadow queries, read per render; see csrc/rt_render.hip):
+# per-lane, packet, hybrid, staged packet, staged hybrid.  The defaults
+# (staged hybrid closest-hit, per-lane shadow) run in every other test.
 TRAV = [0, 1, 2, 3, 4]
 TRAV_SCENES = ["cube", "car-on-road", "dark-night", "island_smooth", "spheres", "susans_smooth",
                "lighthouse", "point-light"]
@@ -154,6 +156,7 @@ TRAV_SCENES = ["cube", "car-on-road", "dark-night", "island_smooth", "spheres", 
 def test_traversal_policies_bitexact(gpu, scene_dir, manifest, trav, monkeypatch):
     """Every traversal policy reproduces the reference goldens bit for bit."""
     monkeypatch.setenv("RT_TRAV", str(trav))
+    monkeypatch.setenv("RT_TRAV_SHADOW", str(trav))  # the policy for shadow queries too
     for case in manifest:
         if case["scene"] not in TRAV_SCENES or case["width"] != 96:
             continue
@@ -172,6 +175,7 @@ def test_traversal_policies_full_frame(gpu, scene_dir, trav, monkeypatch):
     f = s.frame()
     img_f, _ = gpu.Context(s, "flat").render_image(f)
     monkeypatch.setenv("RT_TRAV", str(trav))
+    monkeypatch.setenv("RT_TRAV_SHADOW", str(trav))  # the policy for shadow queries too
     img_o, _ = gpu.Context(s, "octree").render_image(f)
     assert_bitexact(img_o, img_f, f"car-on-road 1080p trav {trav}")
 
