@@ -176,6 +176,25 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
   return __builtin_amdgcn_readfirstlane(x);
 }
 
+// Number of distinct keys among the lanes executing this call (divergent
+// code: the lanes of the current loop iteration), added once to lane `first`.
+// Algorithmic-byte accounting of the per-lane walks (COUNT pass only): a
+// record that several lanes load with the same instruction counts once, the
+// same rule as the packet walk's wave-uniform fetches.
+__device__ __forceinline__ uint32_t lanes_distinct(uint32_t key) {
+  uint64_t m = __ballot(1);
+  uint32_t n = 0;
+  int me = __lane_id();
+  bool first = (int)(__ffsll((unsigned long long)m) - 1) == me;
+  while (m) {
+    int l = __ffsll((unsigned long long)m) - 1;
+    uint32_t k = __shfl(key, l);
+    m &= ~__ballot(key == k);
+    n++;
+  }
+  return first ? n : 0u;
+}
+
 template <bool COUNT>
 __device__ __forceinline__ void absorb(WorkCount& wc, const LaneCount& lc) {
   if (COUNT) {
@@ -232,7 +251,7 @@ __device__ __forceinline__ uint32_t near_octant(f3 d) {
 // Interior node: test the children's boxes and push the hits far-to-near in
 // octant order (a valid front-to-back order for the disjoint octant cells),
 // so the nearest child is popped first.  CLOSEST also prunes by best.
-template <bool CLOSEST>
+template <bool CLOSEST, bool COUNT>
 __device__ __forceinline__ void push_children(const float4* __restrict__ node, const Ray& r, f3 inv,
                                               uint32_t dm, uint32_t first, uint32_t info,
                                               float best, Stack& s, LaneCount& wc) {
@@ -242,6 +261,7 @@ __device__ __forceinline__ void push_children(const float4* __restrict__ node, c
     uint32_t o = (uint32_t)j ^ dm;
     if (mask & (1u << o)) {
       uint32_t ci = first + (uint32_t)__popc(mask & ((1u << o) - 1u));
+      if (COUNT) wc.nodes += lanes_distinct(ci);
       float t0 = box_enter(r, inv, node[2 * ci], node[2 * ci + 1]);
       if (t0 == __builtin_inff()) continue;
       if (CLOSEST && best != __builtin_inff() && rt_prune(t0, r.dlen, best, r.eps)) continue;
@@ -268,16 +288,16 @@ __device__ void oct_closest(const KParams& p, const Ray& r, Best& b, Stack& s, L
     if (b.dist != __builtin_inff() && rt_prune(tn, r.dlen, b.dist, r.eps)) continue;
     float4 lo = node[2 * ni], hi = node[2 * ni + 1];
     uint32_t first = __float_as_uint(lo.w), info = __float_as_uint(hi.w);
-    if (COUNT) wc.nodes++;
+    if (COUNT) wc.nodes += lanes_distinct(ni);
     if (info & RT_NODE_LEAF) {
       uint32_t cnt = RT_LEAF_COUNT(info);
       for (uint32_t k = 0; k < cnt; k++) {
         const float4* q = tri + 3 * (size_t)(first + k);
+        if (COUNT) wc.tris += lanes_distinct(first + k);
         consider(r, q[0], q[1], q[2], b);
       }
-      if (COUNT) wc.tris += cnt;
     } else {
-      push_children<true>(node, r, inv, dm, first, info, b.dist, s, wc);
+      push_children<true, COUNT>(node, r, inv, dm, first, info, b.dist, s, wc);
     }
   }
 }
@@ -296,19 +316,19 @@ __device__ bool oct_any(const KParams& p, const Ray& r, Stack& s, LaneCount& wc)
     pop(s, ni, tn);
     float4 lo = node[2 * ni], hi = node[2 * ni + 1];
     uint32_t first = __float_as_uint(lo.w), info = __float_as_uint(hi.w);
-    if (COUNT) wc.nodes++;
+    if (COUNT) wc.nodes += lanes_distinct(ni);
     if (info & RT_NODE_LEAF) {
       uint32_t cnt = RT_LEAF_COUNT(info);
       for (uint32_t k = 0; k < cnt; k++) {
         const float4* q = tri + 3 * (size_t)(first + k);
-        if (COUNT) wc.tris++;
+        if (COUNT) wc.tris += lanes_distinct(first + k);
         if (any_hit_rec(r, q[0], q[1], q[2])) {
           s.sp = 0;
           return true;
         }
       }
     } else {
-      push_children<false>(node, r, inv, dm, first, info, __builtin_inff(), s, wc);
+      push_children<false, COUNT>(node, r, inv, dm, first, info, __builtin_inff(), s, wc);
     }
   }
   return false;

@@ -2,6 +2,7 @@
 #ifndef RT_LEX_H
 #define RT_LEX_H
 
+#include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -83,6 +84,41 @@ static inline int rt_lex_uint(rt_lex *lx, unsigned *out)
   lx->p = e;
   *out = (unsigned)v;
   return 0;
+}
+
+/* Parallel pre-parse of `v` / `vn` lines (lex_prescan.c). */
+typedef struct rt_vline {
+  size_t off;    /* offset of the `v`/`vn` token                  */
+  uint32_t len;  /* bytes from the token to the end of the 3rd float */
+  float x, y, z;
+} rt_vline;
+
+typedef struct rt_prescan {
+  rt_vline *v;   /* increasing off; NULL = no table (small file)   */
+  size_t n, cur;
+} rt_prescan;
+
+int rt_prescan_build(const rt_lex *lx, rt_prescan *ps);
+void rt_prescan_free(rt_prescan *ps);
+int rt_host_threads(void);
+
+/* The `v`/`vn` token at `tok` was pre-parsed: store its three floats, move
+ * the cursor past them and return 1; else 0 (convert serially). */
+static inline int rt_prescan_take(rt_prescan *ps, rt_lex *lx, const char *tok, float out[3])
+{
+  if (!ps->v)
+    return 0;
+  size_t off = (size_t)(tok - lx->buf);
+  while (ps->cur < ps->n && ps->v[ps->cur].off < off)
+    ps->cur++;
+  if (ps->cur >= ps->n || ps->v[ps->cur].off != off)
+    return 0;
+  const rt_vline *l = &ps->v[ps->cur++];
+  out[0] = l->x;
+  out[1] = l->y;
+  out[2] = l->z;
+  lx->p = lx->buf + off + l->len;
+  return 1;
 }
 
 #endif

@@ -184,6 +184,8 @@ int rt_scene_append_obj(rt_scene *s, const char *path)
   st.obj_cap = s->object_count;
   rt_object_defaults(&st.mat);
   vbuf vs = { 0 }, vns = { 0 };
+  rt_prescan ps;
+  rt_prescan_build(&lx, &ps);
   mtl_lib lib = { 0 };
   const char *t;
   size_t n;
@@ -192,7 +194,11 @@ int rt_scene_append_obj(rt_scene *s, const char *path)
     if (RT_TOK_IS(t, n, "v") || RT_TOK_IS(t, n, "vn"))
     {
       rt_vec3 x;
-      if (rt_lex_float(&lx, &x.x) || rt_lex_float(&lx, &x.y) || rt_lex_float(&lx, &x.z))
+      float f[3];
+      int pre = rt_prescan_take(&ps, &lx, t, f);
+      if (pre)
+        x.x = f[0], x.y = f[1], x.z = f[2];
+      if (!pre && (rt_lex_float(&lx, &x.x) || rt_lex_float(&lx, &x.y) || rt_lex_float(&lx, &x.z)))
         rc = rt_set_error(RT_EPARSE, "%s: bad %.*s near byte %td", path, (int)n, t, lx.p - lx.buf);
       else
         rc = vpush(n == 1 ? &vs : &vns, x);
@@ -319,6 +325,7 @@ int rt_scene_append_obj(rt_scene *s, const char *path)
   free(vs.a);
   free(vns.a);
   free(lib.a);
+  rt_prescan_free(&ps);
   rt_lex_close(&lx);
   return rc;
 }

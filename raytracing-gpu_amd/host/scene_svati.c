@@ -135,7 +135,7 @@ static int lex_vec(rt_lex *lx, rt_vec3 *v)
 }
 
 /* cpu/parse_obj.c:42-92 */
-static int parse_object(rt_lex *lx, rt_object *obj, vecbuf *vs, vecbuf *ns)
+static int parse_object(rt_lex *lx, rt_prescan *ps, rt_object *obj, vecbuf *vs, vecbuf *ns)
 {
   rt_object_defaults(obj);
   unsigned declared;
@@ -160,8 +160,12 @@ static int parse_object(rt_lex *lx, rt_object *obj, vecbuf *vs, vecbuf *ns)
     else if (RT_TOK_IS(t, n, "v") || RT_TOK_IS(t, n, "vn"))
     {
       rt_vec3 x;
+      float f[3];
       seen++;
-      rc = lex_vec(lx, &x);
+      if (rt_prescan_take(ps, lx, t, f))
+        x.x = f[0], x.y = f[1], x.z = f[2];
+      else
+        rc = lex_vec(lx, &x);
       if (!rc)
         rc = vb_push(n == 2 ? ns : vs, x);
     }
@@ -226,6 +230,8 @@ int rt_scene_load_svati(const char *path, rt_scene **out)
   }
   size_t obj_cap = 0;
   vecbuf vs = { 0 }, ns = { 0 };
+  rt_prescan ps;
+  rt_prescan_build(&lx, &ps);
   const char *t;
   size_t n;
   while (!rc && rt_lex_token(&lx, &t, &n))
@@ -263,7 +269,7 @@ int rt_scene_load_svati(const char *path, rt_scene **out)
     else if (RT_TOK_IS(t, n, "object"))
     {
       rt_object o;
-      rc = parse_object(&lx, &o, &vs, &ns);
+      rc = parse_object(&lx, &ps, &o, &vs, &ns);
       if (!rc)
         rc = rt_scene_push_object(s, &o, &obj_cap);
       else
@@ -295,6 +301,7 @@ int rt_scene_load_svati(const char *path, rt_scene **out)
   }
   free(vs.a);
   free(ns.a);
+  rt_prescan_free(&ps);
   rt_lex_close(&lx);
   if (rc)
   {

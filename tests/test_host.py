@@ -200,3 +200,104 @@ def test_octree_probe_synthetic(built):
     s = rtgpu.Scene.synthetic(2, 2, 1000, seed=0x5EED, width=640, height=360)
     r = rtgpu.accel_probe(s, "octree", 53, True)
     assert r["mismatches"] == 0 and r["hits"] > 100, r
+
+
+def _threads(n):
+    """RT_HOST_THREADS is read by the library on every call (lex_prescan.c)."""
+    if n is None:
+        os.environ.pop("RT_HOST_THREADS", None)
+    else:
+        os.environ["RT_HOST_THREADS"] = str(n)
+
+
+def _load(kind, path, threads):
+    import rtgpu
+    _threads(threads)
+    try:
+        s = rtgpu.Scene.load_svati(path) if kind == "svati" else rtgpu.Scene.load_obj(path)
+        return s.triangles_array(), s.materials_array()
+    except rtgpu.RtError as e:
+        return ("error", e.code)
+    finally:
+        _threads(None)
+
+
+@pytest.mark.parametrize("kind", ["svati", "obj"])
+def test_parallel_loader_equals_serial(built, tmp_path, kind):
+    """§8f item 1: the multi-threaded v/vn pre-parse (host/lex_prescan.c,
+    files >= 4 MB) gives bit-identical scenes to the serial scanner."""
+    import rtgpu
+    s = rtgpu.Scene.synthetic(4, 4, 3000, seed=0x5EED, width=64, height=36)
+    p = str(tmp_path / ("syn." + kind))
+    (s.write_svati if kind == "svati" else s.write_obj)(p)
+    assert os.path.getsize(p) > (4 << 20)
+    a, ma = _load(kind, p, 1)
+    b, mb = _load(kind, p, 8)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert np.array_equal(ma.view(np.uint32), mb.view(np.uint32))
+    if kind == "svati":
+        assert np.array_equal(a.view(np.uint32), s.triangles_array().view(np.uint32))
+
+
+def test_parallel_loader_irregular_svati(built, tmp_path):
+    """Grammar corner cases around pre-parsed lines: a `v` line swallowed by a
+    `#` comment (cpu/parser.c:108-109 skips blanks incl. newlines, then a
+    line), numbers continued on the next line, a `v` token in mid-line,
+    blank-indented lines.  Serial and parallel parses must agree exactly."""
+    body = ["camera 64 36 0 4 -20 1 0 0 0 -1 0 70", "a_light 0.2 0.2 0.2",
+            "d_light 1 1 1 1 -1 1"]
+    rng = np.random.default_rng(7)
+    n_obj = 40
+    for o in range(n_obj):
+        nv = 3 * 600
+        body.append(f"object {nv}")
+        body.append("Kd 0.5 0.4 0.3")
+        vs = rng.normal(size=(nv, 3)).astype(np.float32).tolist()
+        for i, v in enumerate(vs):
+            line = f"v {v[0]!r} {v[1]!r} {v[2]!r}"
+            if i % 97 == 5:
+                line = f"v {v[0]!r}\n{v[1]!r} {v[2]!r}"      # continued
+            elif i % 89 == 3:
+                line = f"   \tv {v[0]!r} {v[1]!r} {v[2]!r}"  # indented
+            elif i % 83 == 7:
+                line = f"Ns 3 v {v[0]!r} {v[1]!r} {v[2]!r}"  # mid-line token
+            body.append(line)
+        for i, v in enumerate(vs):
+            body.append(f"vn {v[2]!r} {v[0]!r} {v[1]!r}")
+        body.append("#\nv 9 9 9")  # a whole v line eaten by the comment
+        body.append("# comment")
+    p = tmp_path / "odd.svati"
+    p.write_text("\n".join(body) + "\n")
+    assert os.path.getsize(p) > (4 << 20)
+    a = _load("svati", str(p), 1)
+    b = _load("svati", str(p), 8)
+    assert not isinstance(a[0], str), a
+    assert np.array_equal(a[0].view(np.uint32), b[0].view(np.uint32))
+
+
+def _ppm_expected(W, H, img):
+    f = img.reshape(-1).astype(np.float32)
+    ok = (f > np.float32(-2147483904.0)) & (f < np.float32(2147483648.0))
+    ints = np.where(ok, np.trunc(np.where(ok, f, 0)).astype(np.int64), -2147483648)
+    return (f"P3\n{W} {H}\n255\n" + "".join(f"{v} " for v in ints.tolist())).encode()
+
+
+def test_ppm_writer_parallel_chunks(built, tmp_path):
+    """§8f item 3: multi-chunk, multi-threaded P3 formatting == the
+    `"%d %d %d "` loop of cpu/printer.c:12-18 with (int) truncation."""
+    import rtgpu
+    W, H = 1000, 330  # 5 chunks of 2^16 px, the last ragged
+    rng = np.random.default_rng(3)
+    img = rng.uniform(-20, 300, size=(H, W, 3)).astype(np.float32)
+    img.reshape(-1)[::9973] = np.nan
+    img.reshape(-1)[5::7919] = np.inf
+    img.reshape(-1)[7::7717] = -3e9
+    want = _ppm_expected(W, H, img)
+    for th in (1, 3, 8):
+        _threads(th)
+        try:
+            out = tmp_path / f"o{th}.ppm"
+            rtgpu.write_ppm(str(out), img)
+        finally:
+            _threads(None)
+        assert out.read_bytes() == want, th
