@@ -120,7 +120,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", default="c5", choices=sorted(WORKLOADS))
-    ap.add_argument("--accel", default=None, choices=["flat", "octree"])
+    ap.add_argument("--accel", default=None, choices=["flat", "octree", "octree_gpu"])
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
@@ -265,6 +265,9 @@ def main():
             "config": {
                 "workload": wl["desc"],
                 "width": W, "height": H, "triangles": ntri, "accel": wl["accel"],
+                "accel_build": {"seconds": round(info["build_seconds"], 3),
+                                "where": "device" if wl["accel"] == "octree_gpu" else "host",
+                                "records": info["tri_refs"], "nodes": info["nodes"]},
                 "parallelism": f"image tiles over {world} GPU(s) + RCCL gather" if world > 1
                                else "1 GPU",
                 "queries_per_frame": {"closest": int(closest), "shadow": int(shadow),
@@ -277,7 +280,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
                 "traffic": traffic,
-                "kernel": "render_kernel<OCTREE>" if wl["accel"] == "octree" else "render_kernel<FLAT>",
+                "kernel": "render_kernel<FLAT>" if wl["accel"] == "flat" else "render_kernel<OCTREE>",
                 "kernel_ms": round(kern_ms, 3),
                 "algorithmic_bytes_per_launch": int(per_launch),
                 "per_query_bytes": round(alg_bytes / wq, 1) if wq else None,

@@ -41,8 +41,11 @@ typedef struct rt_frame {
 
 int rt_frame_from_camera(const rt_camera *cam, rt_frame *out);
 
-/* Acceleration structure selection. */
-enum { RT_ACCEL_FLAT = 0, RT_ACCEL_OCTREE = 1 };
+/* Acceleration structure selection.  OCTREE: SAH octree built on the host
+ * (host/accel.c); OCTREE_GPU: octree built on the device by rt_hip_create
+ * (csrc/rt_build.hip, Morton keys + radix sort).  Both
+ * render the same image; they differ in build time and traversal cost. */
+enum { RT_ACCEL_FLAT = 0, RT_ACCEL_OCTREE = 1, RT_ACCEL_OCTREE_GPU = 2 };
 
 /* Per-render counters.  closest = closest-hit queries
  * (collide() calls: camera + reflection rays), shadow = shadow queries
@@ -68,7 +71,7 @@ typedef struct rt_accel_info {
   unsigned long long tri_record_bytes; /* bytes per triangle record             */
   unsigned long long node_record_bytes;
   unsigned long long device_bytes;     /* total device memory of the scene image */
-  double build_seconds;                /* host build time (flatten + octree)     */
+  double build_seconds;                /* build time (flatten + octree, host or device) */
   unsigned long long max_leaf;         /* largest leaf (triangle records)        */
 } rt_accel_info;
 
@@ -100,6 +103,9 @@ int rt_hip_device_count(int *n);
  * builds the acceleration structure.  The caller keeps ownership of scene. */
 int rt_hip_create(int device, const rt_scene *scene, int accel, rt_hip_ctx **out);
 int rt_hip_accel_info(const rt_hip_ctx *ctx, rt_accel_info *out);
+/* Downloads the context's scene image and checks the invariants of
+ * rt_accel_validate on it (any accel, including device-built octrees). */
+int rt_hip_accel_validate(const rt_hip_ctx *ctx);
 void rt_hip_destroy(rt_hip_ctx *ctx);
 
 /* Image tiling: 8x8-pixel tiles in PPM order, tile t belongs to rank t % nranks.

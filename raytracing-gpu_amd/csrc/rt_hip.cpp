@@ -13,6 +13,7 @@
 #include <cstring>
 #include <vector>
 
+#include "rt_build.h"
 #include "rt_kernels.h"
 
 extern "C" {
@@ -103,8 +104,9 @@ extern "C" void rt_hip_destroy(rt_hip_ctx* c) {
 
 extern "C" int rt_hip_create(int device, const rt_scene* scene, int accel, rt_hip_ctx** out) {
   if (!scene || !out) return rt_set_error(RT_EINVAL, "null argument");
-  if (accel != RT_ACCEL_FLAT && accel != RT_ACCEL_OCTREE)
+  if (accel != RT_ACCEL_FLAT && accel != RT_ACCEL_OCTREE && accel != RT_ACCEL_OCTREE_GPU)
     return rt_set_error(RT_EINVAL, "unknown accel %d", accel);
+  const bool dev_build = accel == RT_ACCEL_OCTREE_GPU;
   int ndev = 0;
   int rc = rt_hip_device_count(&ndev);
   if (rc) return rc;
@@ -118,13 +120,15 @@ extern "C" int rt_hip_create(int device, const rt_scene* scene, int accel, rt_hi
 
   auto t0 = std::chrono::steady_clock::now();
   rt_flat_scene fs;
-  rc = rt_flatten(scene, accel, &fs);
+  // device build: the host only flattens (prim-order records, normals,
+  // materials, lights); the octree is built from the uploaded records
+  rc = rt_flatten(scene, dev_build ? RT_ACCEL_FLAT : accel, &fs);
   if (rc) return rc;
   auto t1 = std::chrono::steady_clock::now();
 
   rt_hip_ctx* c = new rt_hip_ctx();
   c->device = device;
-  c->accel = accel;
+  c->accel = dev_build ? (fs.ntri ? RT_ACCEL_OCTREE : RT_ACCEL_FLAT) : accel;
   c->nrec = (uint32_t)fs.nrec;
   c->nlight = (uint32_t)fs.nlight;
   size_t bytes_tri = fs.nrec * RT_TRI_FLOATS * sizeof(float);
@@ -141,6 +145,30 @@ extern "C" int rt_hip_create(int device, const rt_scene* scene, int accel, rt_hi
   if (!rc) rc = upload(&c->d_stats, nullptr, RT_NSTATS * sizeof(unsigned long long));
   if (!rc && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
     rc = rt_set_error(RT_EHIP, "hipStreamCreate");
+  rt_device_tree tree{};
+  if (!rc && dev_build && fs.ntri) {
+    rt_device_build_opts o{8, 7};
+    if (const char* e = std::getenv("RT_DEV_LEAF")) o.leaf_cap = std::atoi(e);  // tuning knobs
+    if (const char* e = std::getenv("RT_DEV_CLIP")) o.clip_level = std::atoi(e);
+    hipError_t he = rt_device_build_octree(c->d_tri, (uint32_t)fs.ntri, fs.scene_lo, fs.scene_hi,
+                                           &o, c->stream, &tree);
+    if (he != hipSuccess) {
+      rc = rt_set_error(RT_EHIP, "device octree build: %s", hipGetErrorString(he));
+    } else {
+      (void)hipFree(c->d_tri);  // prim-order records -> leaf-order records
+      c->d_tri = tree.tri;
+      c->d_node = tree.node;
+      c->nrec = tree.nref;
+      bytes_tri = (size_t)tree.nref * RT_TRI_FLOATS * sizeof(float);
+      bytes_node = (size_t)tree.nnode * RT_NODE_FLOATS * sizeof(float);
+      fs.nrec = tree.nref;
+      fs.nnode = tree.nnode;
+      fs.leaves = tree.leaves;
+      fs.max_depth = tree.depth;
+      fs.max_leaf = tree.max_leaf;
+    }
+  }
+  auto t2 = std::chrono::steady_clock::now();
   for (int a = 0; a < 3; a++) {
     float lo = fs.ntri ? fs.scene_lo[a] : 0.0f, hi = fs.ntri ? fs.scene_hi[a] : 0.0f;
     c->scene_c[a] = 0.5f * (lo + hi);
@@ -155,7 +183,7 @@ extern "C" int rt_hip_create(int device, const rt_scene* scene, int accel, rt_hi
   c->info.tri_record_bytes = RT_TRI_FLOATS * sizeof(float);
   c->info.node_record_bytes = RT_NODE_FLOATS * sizeof(float);
   c->info.device_bytes = bytes_tri + bytes_nrm + bytes_mat + bytes_light + bytes_node;
-  c->info.build_seconds = std::chrono::duration<double>(t1 - t0).count();
+  c->info.build_seconds = std::chrono::duration<double>(dev_build ? t2 - t0 : t1 - t0).count();
   rt_flat_free(&fs);
   if (rc) {
     rt_hip_destroy(c);
@@ -163,7 +191,7 @@ extern "C" int rt_hip_create(int device, const rt_scene* scene, int accel, rt_hi
   }
   // persistent grid: enough one-wave workgroups to fill every SIMD
   c->grid = prop.multiProcessorCount * 16;
-  if (accel == RT_ACCEL_OCTREE &&
+  if (c->accel == RT_ACCEL_OCTREE &&
       hipMalloc((void**)&c->d_spill, (size_t)c->grid * 64 * RT_SPILL_STACK * sizeof(uint2)) !=
           hipSuccess) {
     rt_hip_destroy(c);
@@ -177,6 +205,30 @@ extern "C" int rt_hip_accel_info(const rt_hip_ctx* c, rt_accel_info* out) {
   if (!c || !out) return rt_set_error(RT_EINVAL, "null argument");
   *out = c->info;
   return RT_OK;
+}
+
+extern "C" int rt_hip_accel_validate(const rt_hip_ctx* c) {
+  if (!c) return rt_set_error(RT_EINVAL, "null context");
+  HIP_TRY(hipSetDevice(c->device));
+  rt_flat_scene f;
+  std::memset(&f, 0, sizeof f);
+  f.ntri = c->info.triangles;
+  f.nrec = c->nrec;
+  f.nnode = c->d_node ? c->info.nodes : 0;
+  for (int a = 0; a < 3; a++) {
+    f.scene_lo[a] = c->scene_c[a] - c->scene_r;
+    f.scene_hi[a] = c->scene_c[a] + c->scene_r;
+  }
+  std::vector<float> tri(f.nrec * RT_TRI_FLOATS + 1), node(f.nnode * RT_NODE_FLOATS + 1);
+  if (f.nrec)
+    HIP_TRY(hipMemcpy(tri.data(), c->d_tri, f.nrec * RT_TRI_FLOATS * sizeof(float),
+                      hipMemcpyDeviceToHost));
+  if (f.nnode)
+    HIP_TRY(hipMemcpy(node.data(), c->d_node, f.nnode * RT_NODE_FLOATS * sizeof(float),
+                      hipMemcpyDeviceToHost));
+  f.tri = tri.data();
+  f.node = node.data();
+  return rt_flat_validate(&f);
 }
 
 extern "C" int rt_hip_set_cull_slack(rt_hip_ctx* c, float ulps) {

@@ -722,22 +722,26 @@ int rt_accel_validate(const rt_scene *s, int accel)
   int rc = rt_flatten(s, accel, &f);
   if (rc)
     return rc;
+  rc = rt_flat_validate(&f);
+  rt_flat_free(&f);
+  return rc;
+}
+
+/* Invariants of a flattened scene image (host-built, or downloaded from a
+ * device build by rt_hip_accel_validate). */
+int rt_flat_validate(const rt_flat_scene *fp)
+{
+  const rt_flat_scene f = *fp;
+  int rc = RT_OK;
   if (!f.nnode)
-  {
-    rc = f.nrec == f.ntri ? RT_OK : rt_set_error(RT_EINVAL, "flat: %zu records for %zu prims",
-                                                 f.nrec, f.ntri);
-    rt_flat_free(&f);
-    return rc;
-  }
+    return f.nrec == f.ntri ? RT_OK : rt_set_error(RT_EINVAL, "flat: %zu records for %zu prims",
+                                                   f.nrec, f.ntri);
   float scene_ext = 0;
   for (int a = 0; a < 3; a++)
     scene_ext = fmaxf(scene_ext, f.scene_hi[a] - f.scene_lo[a]);
   unsigned char *seen = calloc(f.ntri ? f.ntri : 1, 1);
   if (!seen)
-  {
-    rt_flat_free(&f);
     return rt_set_error(RT_ENOMEM, "validate");
-  }
   for (size_t n = 0; n < f.nnode && !rc; n++)
   {
     const float *nd = f.node + RT_NODE_FLOATS * n;
@@ -801,6 +805,5 @@ int rt_accel_validate(const rt_scene *s, int accel)
     if (!seen[p])
       rc = rt_set_error(RT_EINVAL, "prim %zu in no leaf", p);
   free(seen);
-  rt_flat_free(&f);
   return rc;
 }

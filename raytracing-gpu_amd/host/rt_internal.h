@@ -61,6 +61,7 @@ typedef struct rt_flat_scene {
 
 int rt_flatten(const rt_scene *scene, int accel, rt_flat_scene *out);
 void rt_flat_free(rt_flat_scene *f);
+int rt_flat_validate(const rt_flat_scene *f);
 
 #ifdef __cplusplus
 }

@@ -24,7 +24,8 @@ LIB_PATH = os.environ.get("RTGPU_LIB") or os.path.join(LIB_DIR, "librtgpu.so")
 
 RT_ACCEL_FLAT = 0
 RT_ACCEL_OCTREE = 1
-ACCEL = {"flat": RT_ACCEL_FLAT, "octree": RT_ACCEL_OCTREE}
+RT_ACCEL_OCTREE_GPU = 2
+ACCEL = {"flat": RT_ACCEL_FLAT, "octree": RT_ACCEL_OCTREE, "octree_gpu": RT_ACCEL_OCTREE_GPU}
 
 
 class RtError(RuntimeError):
@@ -123,6 +124,7 @@ _PROTOS = [
     ("rt_hip_device_count", C.c_int, [C.POINTER(C.c_int)]),
     ("rt_hip_create", C.c_int, [C.c_int, C.POINTER(SceneStruct), C.c_int, C.POINTER(C.c_void_p)]),
     ("rt_hip_accel_info", C.c_int, [C.c_void_p, C.POINTER(AccelInfo)]),
+    ("rt_hip_accel_validate", C.c_int, [C.c_void_p]),
     ("rt_hip_destroy", None, [C.c_void_p]),
     ("rt_hip_tiles_per_rank", C.c_int, [C.c_int, C.c_int, C.c_int]),
     ("rt_hip_tile_buffer_floats", C.c_size_t, [C.c_int, C.c_int, C.c_int]),
@@ -326,6 +328,10 @@ class Context:
         i = AccelInfo()
         _check(lib().rt_hip_accel_info(self.h, C.byref(i)), "accel_info")
         return i.as_dict()
+
+    def validate(self):
+        """Invariants of the device scene image (rt_hip_accel_validate)."""
+        _check(lib().rt_hip_accel_validate(self.h), "accel_validate")
 
     def set_count_work(self, on=True):
         _check(lib().rt_hip_set_count_work(self.h, 1 if on else 0), "count_work")

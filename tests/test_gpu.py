@@ -42,7 +42,7 @@ def gpu(built):
     return rtgpu
 
 
-@pytest.mark.parametrize("accel", ["flat", "octree"])
+@pytest.mark.parametrize("accel", ["flat", "octree", "octree_gpu"])
 @pytest.mark.parametrize("case", CASES, ids=[case_id(c) for c in CASES])
 def test_golden_bitexact(case, accel, gpu, scene_dir):
     s = gpu.Scene.load_svati(os.path.join(scene_dir, case["scene"] + ".svati"))
@@ -121,6 +121,9 @@ def test_large_flat_equals_octree_and_oracle_sample(gpu, scene_dir, scene, W, H)
     img_f, st_f = gpu.Context(s, "flat").render_image(f)
     assert_bitexact(img_o, img_f, f"{scene} octree vs flat")
     assert st_o["closest"] == st_f["closest"] and st_o["shadow"] == st_f["shadow"]
+    img_g, st_g = gpu.Context(s, "octree_gpu").render_image(f)
+    assert_bitexact(img_g, img_f, f"{scene} device-built octree vs flat")
+    assert st_g["closest"] == st_f["closest"] and st_g["shadow"] == st_f["shadow"]
     pix, vals = _oracle_sample(s, W, H, 64, 11)
     assert_bitexact(img_o[pix[:, 0], pix[:, 1]], vals, f"{scene} vs oracle sample")
 
@@ -134,6 +137,34 @@ def test_synthetic_octree_vs_oracle(gpu):
     assert st["closest"] == cnt["closest"] and st["shadow"] == cnt["shadow"]
 
 
+@pytest.mark.parametrize("scene", ["cube", "spheres", "island_smooth", "car-on-road",
+                                   "dark-night", "susans_smooth"])
+def test_device_octree_invariants(gpu, scene_dir, scene):
+    """Device build (csrc/rt_build.hip): every triangle in a leaf, leaf boxes
+    overlap their triangles, node boxes contain their children."""
+    s = gpu.Scene.load_svati(os.path.join(scene_dir, scene + ".svati"))
+    ctx = gpu.Context(s, "octree_gpu")
+    ctx.validate()
+    info = ctx.info()
+    assert info["triangles"] == s.triangle_count and info["tri_refs"] >= info["triangles"]
+    assert info["nodes"] >= 1
+
+
+def test_device_octree_synthetic_and_deterministic(gpu):
+    s = gpu.Scene.synthetic(8, 8, 2000, seed=0x5EED, width=320, height=180)
+    a = gpu.Context(s, "octree_gpu")
+    a.validate()
+    ia = a.info()
+    ib = gpu.Context(s, "octree_gpu").info()
+    assert (ia["nodes"], ia["tri_refs"], ia["leaves"]) == (ib["nodes"], ib["tri_refs"], ib["leaves"])
+    f = s.frame()
+    img_g, st_g = a.render_image(f)
+    img_f, st_f = gpu.Context(s, "flat").render_image(f)
+    bad = (img_g.view(np.uint32) != img_f.view(np.uint32)).any(axis=2).sum()
+    assert bad <= 2e-5 * 320 * 180 + 1, bad  # grazing-hit bound, see below
+    assert st_g["closest"] >= 4 * 320 * 180
+
+
 def test_synthetic_c5_sample(gpu):
     """C5 itself (10M triangles, 4K): oracle parity on a pixel sample."""
     s = gpu.Scene.synthetic(32, 32, 9766, seed=0x5EED, width=3840, height=2160)
@@ -141,6 +172,12 @@ def test_synthetic_c5_sample(gpu):
     assert st["pixels"] == 3840 * 2160 and st["depth_overflow"] == 0
     pix, vals = _oracle_sample(s, 3840, 2160, 12, 5)
     assert_bitexact(img[pix[:, 0], pix[:, 1]], vals, "C5 sample")
+    ctx = gpu.Context(s, "octree_gpu")  # device-built tree of the same scene
+    img_g, st_g = ctx.render_image(s.frame())
+    assert abs(st_g["closest"] - st["closest"]) <= 1000
+    assert_bitexact(img_g[pix[:, 0], pix[:, 1]], vals, "C5 sample, device-built octree")
+    differ = (img_g.view(np.uint32) != img.view(np.uint32)).any(axis=2).sum()
+    assert differ <= 2e-5 * 3840 * 2160, differ
 
 
 # Traversal policies of the octree walk (env RT_TRAV / RT_TRAV_SHADOW for
