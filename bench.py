@@ -45,9 +45,9 @@ N_SIMD = 1024          # 256 CUs x 4 SIMDs (MI355X_MICROARCH.md)
 N_XCD = 8
 
 WORKLOADS = {
-    "c5": dict(kind="synthetic", accel="octree", W=3840, H=2160,
+    "c5": dict(kind="synthetic", accel="octree_gpu", W=3840, H=2160,
                desc="C5 synthetic 10M-triangle sphere field (32x32 UV spheres x 9776 tris + ground, "
-                    "seed 0x5EED), 3840x2160, octree"),
+                    "seed 0x5EED), 3840x2160, device-built octree"),
     "c4": dict(kind="svati", scene="car-on-road", accel="octree", W=3840, H=2160,
                desc="C4 car-on-road.svati at 3840x2160, octree"),
     "c3": dict(kind="svati", scene="island_smooth", accel="octree", W=1920, H=1080,

@@ -16,12 +16,12 @@
 //              inflating every ancestor box (the reference's own rule leaves
 //              42-51 % of triangles near the root).
 //   2. scan    hipcub exclusive sum of the counts -> reference offsets.
-//   3. emit    30-bit Morton key (10 levels x 3 bits, octant bit a = upper
+//   3. emit    63-bit Morton key (21 levels x 3 bits, octant bit a = upper
 //              half of axis a, as rt_cull.h), triangle id and clipped box per
 //              reference.
 //   4. sort    hipcub radix sort of (key, reference) pairs, stable.
 //   5. split   breadth-first, one thread per pending node: a node whose
-//              range holds <= leaf_cap references (or is at level 10) is a
+//              range holds <= leaf_cap references (or is at level 21) is a
 //              leaf, otherwise levels where the whole range shares one octant
 //              are skipped and the range is cut into its non-empty octants
 //              by binary search on the sorted keys; a scan of the child
@@ -50,7 +50,7 @@ extern "C" {
 
 namespace rtb {
 
-constexpr int kLevels = 10;  // 30-bit keys
+constexpr int kLevels = 21;  // 63-bit keys
 
 struct BuildParams {
   const float4* rec;  // ntri records, 3 float4 each (host/rt_internal.h)
@@ -78,16 +78,17 @@ __device__ __forceinline__ void tri_box(const float4* rec, uint32_t i, float lo[
   n[2] = e1[0] * e2[1] - e1[1] * e2[0];
 }
 
-__device__ __forceinline__ uint32_t spread3(uint32_t x) {
-  x &= 0x3ffu;
-  x = (x | (x << 16)) & 0x030000ffu;
-  x = (x | (x << 8)) & 0x0300f00fu;
-  x = (x | (x << 4)) & 0x030c30c3u;
-  x = (x | (x << 2)) & 0x09249249u;
+__device__ __forceinline__ uint64_t spread3(uint32_t v) {
+  uint64_t x = v & 0x1fffffu;
+  x = (x | (x << 32)) & 0x001f00000000ffffull;
+  x = (x | (x << 16)) & 0x001f0000ff0000ffull;
+  x = (x | (x << 8)) & 0x100f00f00f00f00full;
+  x = (x | (x << 4)) & 0x10c30c30c30c30c3ull;
+  x = (x | (x << 2)) & 0x1249249249249249ull;
   return x;
 }
 // octant bit a = upper half of axis a: x in bit 0 of each 3-bit digit
-__device__ __forceinline__ uint32_t morton(uint32_t ix, uint32_t iy, uint32_t iz) {
+__device__ __forceinline__ uint64_t morton(uint32_t ix, uint32_t iy, uint32_t iz) {
   return spread3(ix) | (spread3(iy) << 1) | (spread3(iz) << 2);
 }
 
@@ -160,7 +161,7 @@ __global__ void k_count(BuildParams p, uint32_t* __restrict__ cnt) {
   cnt[i] = c;
 }
 
-__global__ void k_emit(BuildParams p, const uint32_t* __restrict__ off, uint32_t* __restrict__ key,
+__global__ void k_emit(BuildParams p, const uint32_t* __restrict__ off, uint64_t* __restrict__ key,
                        uint32_t* __restrict__ ref_idx, uint32_t* __restrict__ ref_prim,
                        float* __restrict__ ref_box) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -168,7 +169,7 @@ __global__ void k_emit(BuildParams p, const uint32_t* __restrict__ off, uint32_t
   float lo[3], hi[3], v0[3], n[3], e1[3], e2[3];
   tri_box(p.rec, i, lo, hi, v0, n, e1, e2);
   uint32_t o = off[i];
-  auto put = [&](uint32_t r, uint32_t k, const float* bl, const float* bh) {
+  auto put = [&](uint32_t r, uint64_t k, const float* bl, const float* bh) {
     key[r] = k;
     ref_idx[r] = r;
     ref_prim[r] = i;
@@ -191,7 +192,7 @@ __global__ void k_emit(BuildParams p, const uint32_t* __restrict__ off, uint32_t
       }
       // key: the cell's code, lower levels at the cell's centre
       uint32_t mid = sh > 0 ? (1u << (sh - 1)) : 0u;
-      uint32_t k = morton(((uint32_t)x << sh) | mid, ((uint32_t)y << sh) | mid,
+      uint64_t k = morton(((uint32_t)x << sh) | mid, ((uint32_t)y << sh) | mid,
                           ((uint32_t)z << sh) | mid);
       put(o + c, k, bl, bh);
       c++;
@@ -210,12 +211,12 @@ struct Pending {
   uint32_t s, e, level;
 };
 
-__device__ __forceinline__ uint32_t digit(uint32_t k, uint32_t level) {
-  return (k >> (3 * (kLevels - 1 - level))) & 7u;
+__device__ __forceinline__ uint32_t digit(uint64_t k, uint32_t level) {
+  return (uint32_t)(k >> (3 * (kLevels - 1 - level))) & 7u;
 }
 
 // first index in [s, e) whose digit at `level` is >= o (keys share the prefix)
-__device__ __forceinline__ uint32_t lower(const uint32_t* key, uint32_t s, uint32_t e,
+__device__ __forceinline__ uint32_t lower(const uint64_t* key, uint32_t s, uint32_t e,
                                          uint32_t level, uint32_t o) {
   while (s < e) {
     uint32_t m = s + (e - s) / 2;
@@ -228,7 +229,7 @@ __device__ __forceinline__ uint32_t lower(const uint32_t* key, uint32_t s, uint3
 }
 
 // 5a: classify each pending node; split[j*9 + o] = child boundaries
-__global__ void k_split(const Pending* __restrict__ pend, uint32_t np, const uint32_t* __restrict__ key,
+__global__ void k_split(const Pending* __restrict__ pend, uint32_t np, const uint64_t* __restrict__ key,
                         uint32_t leaf_cap, uint32_t* __restrict__ split,
                         uint32_t* __restrict__ level_out, uint32_t* __restrict__ nchild) {
   uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -348,7 +349,8 @@ extern "C" hipError_t rt_device_build_octree(const float4* d_rec, uint32_t ntri,
   using namespace rtb;
   hipError_t err = hipSuccess;
   *out = rt_device_tree{};
-  uint32_t *cnt = nullptr, *off = nullptr, *key = nullptr, *key2 = nullptr, *ref = nullptr,
+  uint64_t *key = nullptr, *key2 = nullptr;
+  uint32_t *cnt = nullptr, *off = nullptr, *ref = nullptr,
            *ref2 = nullptr, *ref_prim = nullptr, *split = nullptr, *lvl = nullptr,
            *nch = nullptr, *coff = nullptr, *leaf_stats = nullptr;
   float* ref_box = nullptr;
@@ -389,8 +391,8 @@ extern "C" hipError_t rt_device_build_octree(const float4* d_rec, uint32_t ntri,
   tmp = nullptr;
 
   // 3-4: keyed references, sorted
-  BTRY(hipMalloc((void**)&key, (size_t)nref * 4));
-  BTRY(hipMalloc((void**)&key2, (size_t)nref * 4));
+  BTRY(hipMalloc((void**)&key, (size_t)nref * 8));
+  BTRY(hipMalloc((void**)&key2, (size_t)nref * 8));
   BTRY(hipMalloc((void**)&ref, (size_t)nref * 4));
   BTRY(hipMalloc((void**)&ref2, (size_t)nref * 4));
   BTRY(hipMalloc((void**)&ref_prim, (size_t)nref * 4));

@@ -3,7 +3,7 @@
  *   rt file.svati output.ppm                  (cpu/rt.c:5-10, same usage error)
  * Optional flags may follow the two positional arguments:
  *   --gpus N          tile the frame over N GPUs of this node (RCCL gather)
- *   --accel flat|octree
+ *   --accel flat|octree|octree_gpu
  *   --stats           print query counters and render time to stderr
  * Errors exit with status 1 via errx(), as the reference does.
  */
@@ -26,14 +26,17 @@ int main(int argc, char *argv[])
     else if (!strcmp(argv[i], "--accel") && i + 1 < argc)
     {
       const char *a = argv[++i];
-      accel = !strcmp(a, "flat") ? RT_ACCEL_FLAT : !strcmp(a, "octree") ? RT_ACCEL_OCTREE : -2;
+      accel = !strcmp(a, "flat")         ? RT_ACCEL_FLAT
+              : !strcmp(a, "octree")     ? RT_ACCEL_OCTREE
+              : !strcmp(a, "octree_gpu") ? RT_ACCEL_OCTREE_GPU
+                                         : -2;
       if (accel == -2)
         errx(1, "unknown accel %s", a);
     }
     else if (!strcmp(argv[i], "--stats"))
       want_stats = 1;
     else
-      errx(1, "usage: %s file.svati output.ppm [--gpus N] [--accel flat|octree] [--stats]",
+      errx(1, "usage: %s file.svati output.ppm [--gpus N] [--accel flat|octree|octree_gpu] [--stats]",
            argv[0]);
   }
   rt_stats st;
