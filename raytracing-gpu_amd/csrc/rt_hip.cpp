@@ -147,7 +147,7 @@ extern "C" int rt_hip_create(int device, const rt_scene* scene, int accel, rt_hi
     rc = rt_set_error(RT_EHIP, "hipStreamCreate");
   rt_device_tree tree{};
   if (!rc && dev_build && fs.ntri) {
-    rt_device_build_opts o{16, 7};  // measured best on C5 (leaf cap 4..32)
+    rt_device_build_opts o{12, 7};  // measured best on C5 (leaf cap 4..32)
     if (const char* e = std::getenv("RT_DEV_LEAF")) o.leaf_cap = std::atoi(e);  // tuning knobs
     if (const char* e = std::getenv("RT_DEV_CLIP")) o.clip_level = std::atoi(e);
     hipError_t he = rt_device_build_octree(c->d_tri, (uint32_t)fs.ntri, fs.scene_lo, fs.scene_hi,

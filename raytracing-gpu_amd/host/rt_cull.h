@@ -57,18 +57,23 @@ RT_CULL_FN float rt_inv(float d)
 }
 
 /* Slab test of the ray o + t d against [lo - eps, hi + eps]:
- * (lo - eps - o) is evaluated as lo - oh, (hi + eps - o) as hi - ol.  Their
- * rounding, and that of the products, is a few ulps of |o| + |t d|, far below
- * eps (>= 64 ulps of the origin-to-scene distance plus 4 ulps of the scene's
- * own coordinates), so no parametric slack is needed.  Returns 1 when the
- * interval [tmin, tmax] reaches t >= 0; *tmin = entry parameter. */
+ * (lo - eps - o) / d is evaluated as fma(lo, 1/d, -(oh/d)) with oh = o + eps
+ * (and hi with ol = o - eps): one fused multiply-add per plane, the per-ray
+ * products oh/d, ol/d being loop-invariant (hoisted out of the walks).  The
+ * rounding of oh/d moves a plane by at most an ulp of |oh| along its axis,
+ * the fma's own rounding is relative to t, i.e. an ulp of |t d|; eps (>= 64
+ * ulps of the origin-to-scene distance plus 4 ulps of |c| + R, hence >= 2
+ * ulps of |o|) covers both, so no parametric slack is needed.  fmaf is the
+ * correctly rounded IEEE operation on the host (libm) and the device
+ * (v_fma_f32), so the host model decides exactly like the device.  Returns 1
+ * when the interval [tmin, tmax] reaches t >= 0; *tmin = entry parameter. */
 RT_CULL_FN int rt_box_hit(float ohx, float ohy, float ohz, float olx, float oly, float olz,
                           float ix, float iy, float iz, float lx, float ly, float lz, float hx,
                           float hy, float hz, float *tmin_out)
 {
-  float tx0 = (lx - ohx) * ix, tx1 = (hx - olx) * ix;
-  float ty0 = (ly - ohy) * iy, ty1 = (hy - oly) * iy;
-  float tz0 = (lz - ohz) * iz, tz1 = (hz - olz) * iz;
+  float tx0 = fmaf(lx, ix, -(ohx * ix)), tx1 = fmaf(hx, ix, -(olx * ix));
+  float ty0 = fmaf(ly, iy, -(ohy * iy)), ty1 = fmaf(hy, iy, -(oly * iy));
+  float tz0 = fmaf(lz, iz, -(ohz * iz)), tz1 = fmaf(hz, iz, -(olz * iz));
   float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
   float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
   *tmin_out = tmin;
