@@ -302,6 +302,28 @@ __device__ void oct_closest(const KParams& p, const Ray& r, Best& b, Stack& s, L
   }
 }
 
+// Any-hit walk: a stack entry holds the node's own (first, info) words,
+// taken from the child box record its parent already fetched, so a pop needs
+// no node fetch -- one dependent load per step (the children's boxes or the
+// leaf's triangles) instead of two.
+template <bool COUNT>
+__device__ __forceinline__ void push_children_any(const float4* __restrict__ node, const Ray& r,
+                                                  f3 inv, uint32_t dm, uint32_t first,
+                                                  uint32_t info, Stack& s, LaneCount& wc) {
+  uint32_t mask = RT_NODE_MASK(info);
+#pragma unroll 1
+  for (int j = 7; j >= 0; --j) {
+    uint32_t o = (uint32_t)j ^ dm;
+    if (mask & (1u << o)) {
+      uint32_t ci = first + (uint32_t)__popc(mask & ((1u << o) - 1u));
+      if (COUNT) wc.nodes += lanes_distinct(ci);
+      float4 clo = node[2 * ci], chi = node[2 * ci + 1];
+      if (box_enter(r, inv, clo, chi) == __builtin_inff()) continue;
+      push(s, __float_as_uint(clo.w), chi.w, wc);
+    }
+  }
+}
+
 template <bool COUNT>
 __device__ bool oct_any(const KParams& p, const Ray& r, Stack& s, LaneCount& wc) {
   const float4* __restrict__ node = p.node;
@@ -309,14 +331,16 @@ __device__ bool oct_any(const KParams& p, const Ray& r, Stack& s, LaneCount& wc)
   f3 inv = inv_dir(r.d);
   uint32_t dm = near_octant(r.d);
   s.sp = 0;
-  if (box_enter(r, inv, node[0], node[1]) != __builtin_inff()) push(s, 0, 0.0f, wc);
+  {
+    float4 lo = node[0], hi = node[1];
+    if (COUNT) wc.nodes += lanes_distinct(0);
+    if (box_enter(r, inv, lo, hi) != __builtin_inff()) push(s, __float_as_uint(lo.w), hi.w, wc);
+  }
   while (s.sp > 0) {
-    uint32_t ni;
-    float tn;
-    pop(s, ni, tn);
-    float4 lo = node[2 * ni], hi = node[2 * ni + 1];
-    uint32_t first = __float_as_uint(lo.w), info = __float_as_uint(hi.w);
-    if (COUNT) wc.nodes += lanes_distinct(ni);
+    uint32_t first;
+    float info_bits;
+    pop(s, first, info_bits);
+    uint32_t info = __float_as_uint(info_bits);
     if (info & RT_NODE_LEAF) {
       uint32_t cnt = RT_LEAF_COUNT(info);
       for (uint32_t k = 0; k < cnt; k++) {
@@ -328,7 +352,7 @@ __device__ bool oct_any(const KParams& p, const Ray& r, Stack& s, LaneCount& wc)
         }
       }
     } else {
-      push_children<false, COUNT>(node, r, inv, dm, first, info, __builtin_inff(), s, wc);
+      push_children_any<COUNT>(node, r, inv, dm, first, info, s, wc);
     }
   }
   return false;
