@@ -50,6 +50,7 @@ struct KParams {
   int trav;                     // RT_TRAV_LANE / _PACKET / _HYBRID (rt_render.hip)
   int packet_min;               // hybrid: packet walk while >= this many lanes query
   int trav_shadow, packet_min_shadow;  // the same two for shadow (any-hit) queries
+  int packet_max_depth;         // closest hit: packet walk only up to this bounce depth
 };
 
 // min_waves = occupancy target per SIMD (launch bounds of the instantiation:

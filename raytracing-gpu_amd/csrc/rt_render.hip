@@ -792,13 +792,15 @@ __device__ bool staged_any(const KParams& p, const Ray& r, bool act, WaveCtx& w,
 
 // Closest-hit query; converged call, act = lane has a query.
 template <int ACCEL, bool COUNT>
-__device__ __forceinline__ void closest_q(const KParams& p, const Ray& r, bool act, Best& b,
+__device__ __forceinline__ void closest_q(const KParams& p, const Ray& r, bool act, int depth, Best& b,
                                           Stack& s, WaveCtx& w, WorkCount& wc) {
   if (ACCEL == RT_ACCEL_FLAT_D) {
     flat_closest_w<COUNT>(p, r, act, b, w, wc);
     return;
   }
-  bool many = __popcll(__ballot(act)) >= p.packet_min;
+  // packet walk for coherent queries: enough lanes, and a bounce depth at
+  // which rays are still coherent (camera rays: depth 0)
+  bool many = __popcll(__ballot(act)) >= p.packet_min && depth <= p.packet_max_depth;
   if (p.trav == RT_TRAV_STAGED || (p.trav == RT_TRAV_STAGED_HYBRID && many))
     staged_closest<COUNT>(p, r, act, b, w, wc);
   else if (p.trav == RT_TRAV_PACKET || (p.trav == RT_TRAV_HYBRID && many))
@@ -917,7 +919,7 @@ __device__ __forceinline__ col trace_path(const KParams& p, bool valid, f3 o, f3
     b.obj = 0;
     b.u = b.v = 0.0f;
     b.pt = o;
-    closest_q<ACCEL, COUNT>(p, r, alive, b, s, w, wc);
+    closest_q<ACCEL, COUNT>(p, r, alive, depth, b, s, w, wc);
     bool hit = alive && b.dist != __builtin_inff();
     f3 N = f3{0.0f, 0.0f, 0.0f};
     wc.hits += (uint32_t)__popcll(__ballot(hit));
