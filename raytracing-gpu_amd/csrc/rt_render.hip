@@ -818,6 +818,9 @@ __device__ __forceinline__ bool shadow_q(const KParams& p, f3 o, f3 d, bool act,
                                          WaveCtx& w, WorkCount& wc) {
   uint64_t am = __ballot(act);
   wc.shadow += (uint32_t)__popcll(am);
+#ifdef RT_DBG_SHADOW_SLOTS  // lane slots of shadow calls (in zero_normal; breakdown only)
+  if (am) wc.zero_normal += 64u;
+#endif
 #ifdef RT_DBG_NO_SHADOW  // timing breakdown only (wrong images)
   return false;
 #endif
