@@ -343,6 +343,27 @@ __device__ bool oct_any(const KParams& p, const Ray& r, Stack& s, LaneCount& wc)
     uint32_t info = __float_as_uint(info_bits);
     if (info & RT_NODE_LEAF) {
       uint32_t cnt = RT_LEAF_COUNT(info);
+#ifndef RT_LEAF_PIPE
+#define RT_LEAF_PIPE 1
+#endif
+#if RT_LEAF_PIPE
+      // software-pipelined: record k+1 is in flight while record k is tested
+      const float4* q = tri + 3 * (size_t)first;
+      float4 n0 = q[0], n1 = q[1], n2 = q[2];
+      for (uint32_t k = 0; k < cnt; k++) {
+        float4 q0 = n0, q1 = n1, q2 = n2;
+        if (k + 1 < cnt) {
+          n0 = q[3 * (k + 1)];
+          n1 = q[3 * (k + 1) + 1];
+          n2 = q[3 * (k + 1) + 2];
+        }
+        if (COUNT) wc.tris += lanes_distinct(first + k);
+        if (any_hit_rec(r, q0, q1, q2)) {
+          s.sp = 0;
+          return true;
+        }
+      }
+#else
       for (uint32_t k = 0; k < cnt; k++) {
         const float4* q = tri + 3 * (size_t)(first + k);
         if (COUNT) wc.tris += lanes_distinct(first + k);
@@ -351,6 +372,7 @@ __device__ bool oct_any(const KParams& p, const Ray& r, Stack& s, LaneCount& wc)
           return true;
         }
       }
+#endif
     } else {
       push_children_any<COUNT>(node, r, inv, dm, first, info, s, wc);
     }
