@@ -162,6 +162,9 @@ struct Stack {
   uint2* spill;   // this lane's kSpillStack entries
   int lane;
   int sp;
+  uint32_t occ;   // record index of this lane's last shadow occluder (~0u: none)
+  uint32_t occ2;  // the same for the other light parity (RT_OCC_SLOTS 2)
+  uint32_t slot;  // light parity of the current shadow query (wave-uniform)
 };
 
 // Counters of one lane's own walk (divergent code); folded into the wave's
@@ -248,6 +251,18 @@ __device__ __forceinline__ uint32_t near_octant(f3 d) {
   return (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
 }
 
+#ifndef RT_CHILD_PIPE
+#define RT_CHILD_PIPE 1
+#endif
+
+// child-mask bit o moved to bit o ^ dm (the visiting order's index space)
+__device__ __forceinline__ uint32_t mask_xor(uint32_t m, uint32_t dm) {
+  if (dm & 1u) m = ((m & 0x55u) << 1) | ((m & 0xAAu) >> 1);
+  if (dm & 2u) m = ((m & 0x33u) << 2) | ((m & 0xCCu) >> 2);
+  if (dm & 4u) m = ((m & 0x0Fu) << 4) | ((m & 0xF0u) >> 4);
+  return m;
+}
+
 // Interior node: test the children's boxes and push the hits far-to-near in
 // octant order (a valid front-to-back order for the disjoint octant cells),
 // so the nearest child is popped first.  CLOSEST also prunes by best.
@@ -256,6 +271,36 @@ __device__ __forceinline__ void push_children(const float4* __restrict__ node, c
                                               uint32_t dm, uint32_t first, uint32_t info,
                                               float best, Stack& s, LaneCount& wc) {
   uint32_t mask = RT_NODE_MASK(info);
+#if RT_CHILD_PIPE
+  // same order, software-pipelined: child k+1's box is in flight while
+  // child k is tested
+  uint32_t mj = mask_xor(mask, dm);
+  if (!mj) return;
+  int j = 31 - __clz(mj);
+  mj &= ~(1u << j);
+  uint32_t ci = first + (uint32_t)__popc(mask & ((1u << ((uint32_t)j ^ dm)) - 1u));
+  float4 nlo = node[2 * ci], nhi = node[2 * ci + 1];
+  if (COUNT) wc.nodes += lanes_distinct(ci);
+  for (;;) {
+    float4 clo = nlo, chi = nhi;
+    uint32_t cc = ci;
+    bool more = mj != 0u;
+    if (more) {
+      j = 31 - __clz(mj);
+      mj &= ~(1u << j);
+      ci = first + (uint32_t)__popc(mask & ((1u << ((uint32_t)j ^ dm)) - 1u));
+      nlo = node[2 * ci];
+      nhi = node[2 * ci + 1];
+      if (COUNT) wc.nodes += lanes_distinct(ci);
+    }
+    float t0 = box_enter(r, inv, clo, chi);
+    if (t0 != __builtin_inff() &&
+        !(CLOSEST && best != __builtin_inff() && rt_prune(t0, r.dlen, best, r.eps)))
+      push(s, cc, t0, wc);
+    if (!more) break;
+  }
+  return;
+#endif
 #pragma unroll 1
   for (int j = 7; j >= 0; --j) {
     uint32_t o = (uint32_t)j ^ dm;
@@ -269,6 +314,10 @@ __device__ __forceinline__ void push_children(const float4* __restrict__ node, c
     }
   }
 }
+
+#ifndef RT_LEAF_PIPE
+#define RT_LEAF_PIPE 1
+#endif
 
 template <bool COUNT>
 __device__ void oct_closest(const KParams& p, const Ray& r, Best& b, Stack& s, LaneCount& wc) {
@@ -291,11 +340,27 @@ __device__ void oct_closest(const KParams& p, const Ray& r, Best& b, Stack& s, L
     if (COUNT) wc.nodes += lanes_distinct(ni);
     if (info & RT_NODE_LEAF) {
       uint32_t cnt = RT_LEAF_COUNT(info);
+#if RT_LEAF_PIPE
+      // software-pipelined: record k+1 is in flight while record k is tested
+      const float4* q = tri + 3 * (size_t)first;
+      float4 n0 = q[0], n1 = q[1], n2 = q[2];
+      for (uint32_t k = 0; k < cnt; k++) {
+        float4 q0 = n0, q1 = n1, q2 = n2;
+        if (k + 1 < cnt) {
+          n0 = q[3 * (k + 1)];
+          n1 = q[3 * (k + 1) + 1];
+          n2 = q[3 * (k + 1) + 2];
+        }
+        if (COUNT) wc.tris += lanes_distinct(first + k);
+        consider(r, q0, q1, q2, b);
+      }
+#else
       for (uint32_t k = 0; k < cnt; k++) {
         const float4* q = tri + 3 * (size_t)(first + k);
         if (COUNT) wc.tris += lanes_distinct(first + k);
         consider(r, q[0], q[1], q[2], b);
       }
+#endif
     } else {
       push_children<true, COUNT>(node, r, inv, dm, first, info, b.dist, s, wc);
     }
@@ -311,6 +376,34 @@ __device__ __forceinline__ void push_children_any(const float4* __restrict__ nod
                                                   f3 inv, uint32_t dm, uint32_t first,
                                                   uint32_t info, Stack& s, LaneCount& wc) {
   uint32_t mask = RT_NODE_MASK(info);
+#if RT_CHILD_PIPE
+  // Same far-to-near order as below (j = 7..0, octant j ^ dm), software-
+  // pipelined: child k+1's box is in flight while child k is tested.
+  uint32_t mj = mask_xor(mask, dm);
+  if (!mj) return;
+  int j = 31 - __clz(mj);
+  mj &= ~(1u << j);
+  uint32_t o = (uint32_t)j ^ dm;
+  uint32_t ci = first + (uint32_t)__popc(mask & ((1u << o) - 1u));
+  float4 nlo = node[2 * ci], nhi = node[2 * ci + 1];
+  if (COUNT) wc.nodes += lanes_distinct(ci);
+  for (;;) {
+    float4 clo = nlo, chi = nhi;
+    bool more = mj != 0u;
+    if (more) {
+      j = 31 - __clz(mj);
+      mj &= ~(1u << j);
+      o = (uint32_t)j ^ dm;
+      ci = first + (uint32_t)__popc(mask & ((1u << o) - 1u));
+      nlo = node[2 * ci];
+      nhi = node[2 * ci + 1];
+      if (COUNT) wc.nodes += lanes_distinct(ci);
+    }
+    if (box_enter(r, inv, clo, chi) != __builtin_inff()) push(s, __float_as_uint(clo.w), chi.w, wc);
+    if (!more) break;
+  }
+  return;
+#endif
 #pragma unroll 1
   for (int j = 7; j >= 0; --j) {
     uint32_t o = (uint32_t)j ^ dm;
@@ -324,6 +417,13 @@ __device__ __forceinline__ void push_children_any(const float4* __restrict__ nod
   }
 }
 
+#ifndef RT_OCC_CACHE
+#define RT_OCC_CACHE 0  // measured: C5 15.37/15.56 (on) vs 15.33/15.53 ms (off): a wave waits for its slowest lane
+#endif
+#ifndef RT_OCC_SLOTS
+#define RT_OCC_SLOTS 2  // one cached occluder per light parity
+#endif
+
 template <bool COUNT>
 __device__ bool oct_any(const KParams& p, const Ray& r, Stack& s, LaneCount& wc) {
   const float4* __restrict__ node = p.node;
@@ -331,6 +431,18 @@ __device__ bool oct_any(const KParams& p, const Ray& r, Stack& s, LaneCount& wc)
   f3 inv = inv_dir(r.d);
   uint32_t dm = near_octant(r.d);
   s.sp = 0;
+#if RT_OCC_CACHE
+  // Occluder cache: the triangle that blocked this lane's previous shadow ray
+  // (a neighbouring supersample's, usually) is tested first.  Any record hit
+  // with the walk's own exact test decides the query (cpu/light.c:24-31 is an
+  // any-hit predicate), so this only reorders work.
+  uint32_t oc = (RT_OCC_SLOTS == 2 && s.slot) ? s.occ2 : s.occ;
+  if (oc != 0xffffffffu) {
+    const float4* q = tri + 3 * (size_t)oc;
+    if (COUNT) wc.tris += lanes_distinct(oc);
+    if (any_hit_rec(r, q[0], q[1], q[2])) return true;
+  }
+#endif
   {
     float4 lo = node[0], hi = node[1];
     if (COUNT) wc.nodes += lanes_distinct(0);
@@ -343,9 +455,6 @@ __device__ bool oct_any(const KParams& p, const Ray& r, Stack& s, LaneCount& wc)
     uint32_t info = __float_as_uint(info_bits);
     if (info & RT_NODE_LEAF) {
       uint32_t cnt = RT_LEAF_COUNT(info);
-#ifndef RT_LEAF_PIPE
-#define RT_LEAF_PIPE 1
-#endif
 #if RT_LEAF_PIPE
       // software-pipelined: record k+1 is in flight while record k is tested
       const float4* q = tri + 3 * (size_t)first;
@@ -360,6 +469,10 @@ __device__ bool oct_any(const KParams& p, const Ray& r, Stack& s, LaneCount& wc)
         if (COUNT) wc.tris += lanes_distinct(first + k);
         if (any_hit_rec(r, q0, q1, q2)) {
           s.sp = 0;
+          if (RT_OCC_SLOTS == 2 && s.slot)
+            s.occ2 = first + k;
+          else
+            s.occ = first + k;
           return true;
         }
       }
@@ -701,6 +814,10 @@ __device__ __forceinline__ void stage_push_children(const Ray& r, f3 inv, uint32
   }
 }
 
+#ifndef RT_STAGE_PIPE
+#define RT_STAGE_PIPE 0  // measured: C5 15.34 (off) vs 15.65 ms (on)
+#endif
+
 template <bool COUNT>
 __device__ void staged_closest(const KParams& p, const Ray& r, bool act, Best& b, WaveCtx& w,
                                WorkCount& wc) {
@@ -740,10 +857,23 @@ __device__ void staged_closest(const KParams& p, const Ray& r, bool act, Best& b
       for (uint32_t base = 0; base < cnt; base += kOctRecs) {
         uint32_t m = chunk<kOctRecs>(cnt, base);
         if (base) stage_load(tri + 3 * (size_t)(first + base), 3 * (int)m, w);
+#if RT_STAGE_PIPE
+        // software-pipelined: record k+1's LDS reads are in flight while k is tested
+        float4 n0 = w.stage[0], n1 = w.stage[1], n2 = w.stage[2];
+        for (uint32_t k = 0; k < m; k++) {
+          float4 q0 = n0, q1 = n1, q2 = n2;
+          uint32_t kn = k + 1 < m ? 3 * (k + 1) : 0;
+          n0 = w.stage[kn];
+          n1 = w.stage[kn + 1];
+          n2 = w.stage[kn + 2];
+          if (want) consider(r, q0, q1, q2, b);
+        }
+#else
         for (uint32_t k = 0; k < m; k++) {
           float4 q0 = w.stage[3 * k], q1 = w.stage[3 * k + 1], q2 = w.stage[3 * k + 2];
           if (want) consider(r, q0, q1, q2, b);
         }
+#endif
       }
       limit = rt_prune_limit(b.dist, r.eps);
       if (COUNT) wc.tris += cnt;
@@ -915,6 +1045,7 @@ __device__ col apply_light(const KParams& p, bool hit, const float* m, f3 P, f3 
     if (type == 0) {  // AMBIENT
       if (hit) acc = color_add(acc, color_mul2(lc, init_color(m[0], m[1], m[2])));
     } else if (type == 1 || type == 2) {
+      s.slot = li & 1u;
       bool sh = shadow_q<ACCEL, COUNT>(p, P, shadow_dir(type, lv, P), hit, s, w, wc);
       if (hit && !sh) acc = color_add(acc, light_lit(type, lc, lv, m, P, N));
     }
@@ -997,6 +1128,8 @@ __global__ __launch_bounds__(64, MINW) void render_kernel(KParams p) {
   stk.spill = p.spill + ((size_t)blockIdx.x * 64 + (size_t)lane) * kSpillStack;
   stk.lane = lane;
   stk.sp = 0;
+  stk.occ = stk.occ2 = 0xffffffffu;
+  stk.slot = 0;
   WaveCtx w;
   w.ws = s_ws;
   w.stk2 = s_stk2;
