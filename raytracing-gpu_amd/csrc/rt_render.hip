@@ -978,6 +978,9 @@ __device__ bool staged_any(const KParams& p, const Ray& r, bool act, WaveCtx& w,
 // Traversal policy: per-lane walks (each lane its own stack) or a packet
 // walk; with TRAV_HYBRID the packet walk is used while at least
 // p.packet_min lanes of the wave have a query.
+#ifndef RT_LEAN  // 1: only the staged-hybrid closest walk and the per-lane any-hit walk
+#define RT_LEAN 0
+#endif
 #define RT_TRAV_LANE 0
 #define RT_TRAV_PACKET 1
 #define RT_TRAV_HYBRID 2
@@ -997,8 +1000,10 @@ __device__ __forceinline__ void closest_q(const KParams& p, const Ray& r, bool a
   bool many = __popcll(__ballot(act)) >= p.packet_min && depth <= p.packet_max_depth;
   if (p.trav == RT_TRAV_STAGED || (p.trav == RT_TRAV_STAGED_HYBRID && many))
     staged_closest<COUNT>(p, r, act, b, w, wc);
+#if !RT_LEAN
   else if (p.trav == RT_TRAV_PACKET || (p.trav == RT_TRAV_HYBRID && many))
     packet_closest<COUNT>(p, r, act, b, w.ws, w.lane, wc);
+#endif
   else {
     LaneCount lc = {0, 0, 0};
     if (act) oct_closest<COUNT>(p, r, b, s, lc);
@@ -1021,10 +1026,14 @@ __device__ __forceinline__ bool shadow_q(const KParams& p, f3 o, f3 d, bool act,
   Ray r = make_ray(p, o, d);
   if (ACCEL == RT_ACCEL_FLAT_D) return flat_any_w<COUNT>(p, r, act, w, wc);
   bool many = __popcll(am) >= p.packet_min_shadow;
+#if !RT_LEAN
   if (p.trav_shadow == RT_TRAV_STAGED || (p.trav_shadow == RT_TRAV_STAGED_HYBRID && many))
     return staged_any<COUNT>(p, r, act, w, wc);
   if (p.trav_shadow == RT_TRAV_PACKET || (p.trav_shadow == RT_TRAV_HYBRID && many))
     return packet_any<COUNT>(p, r, act, w.ws, w.lane, wc);
+#else
+  (void)many;
+#endif
   LaneCount lc = {0, 0, 0};
   bool hit = act && oct_any<COUNT>(p, r, s, lc);
   absorb<COUNT>(wc, lc);
