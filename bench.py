@@ -114,6 +114,13 @@ def cpu_baseline(scene, W, H, seconds, threads, gpu_img):
     }
 
 
+def latest_profile(workload, name):
+    """Newest profiles/r*_<workload>/<name> (round-letter order), or None."""
+    import glob
+    hits = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_{workload}", name)))
+    return hits[-1] if hits else None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -224,6 +231,13 @@ def main():
     per_launch = alg_bytes / world
     achieved = per_launch / (kern_ms * 1e-3) / 1e9
     traffic = None
+    if world == 1 and args.traffic_json is None and args.cull_slack is None:
+        # default run: the newest committed rocprofv3 PMC pass of this
+        # workload (profiles/r*_<workload>/, tools/gpu_profile.sh), named in
+        # roofline.traffic_source; a PMC pass cannot run inside the bench
+        args.traffic_json = latest_profile(args.workload, "traffic.json")
+        if args.valu_json is None:
+            args.valu_json = latest_profile(args.workload, "pmc_valu.json")
     if args.traffic_json and os.path.exists(args.traffic_json):
         with open(args.traffic_json) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
@@ -240,7 +254,7 @@ def main():
             "lane_util": round(pm["SQ_THREAD_CYCLES_VALU"] / (64.0 * pm["SQ_ACTIVE_INST_VALU"]), 4),
             "valu_insts_per_launch": pm["SQ_INSTS_VALU"],
             "clock_ghz": round(pm["GRBM_GUI_ACTIVE"] / N_XCD / (kern_ms * 1e-3) / 1e9, 3),
-            "source": os.path.basename(args.valu_json),
+            "source": os.path.relpath(args.valu_json, REPO),
         }
 
     if rank == 0:
@@ -280,6 +294,8 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
                 "traffic": traffic,
+                "traffic_source": (os.path.relpath(args.traffic_json, REPO)
+                                   if traffic is not None else None),
                 "kernel": "render_kernel<FLAT>" if wl["accel"] == "flat" else "render_kernel<OCTREE>",
                 "kernel_ms": round(kern_ms, 3),
                 "algorithmic_bytes_per_launch": int(per_launch),
