@@ -136,6 +136,9 @@ __device__ __forceinline__ void consider(const Ray& r, const float4& q0, const f
   }
 }
 
+#ifndef RT_ANY_DLEN_RECOMPUTE
+#define RT_ANY_DLEN_RECOMPUTE 1  // measured: C5 15.43/15.39 (on) vs 15.66/15.39 ms (off)
+#endif
 #ifndef RT_ANY_ND_RECOMPUTE
 #define RT_ANY_ND_RECOMPUTE 1  // measured: C5 15.37/15.39 (on) vs 15.53/15.50 ms (off)
 #endif
@@ -149,8 +152,13 @@ __device__ __forceinline__ bool any_hit_rec(const Ray& r, const float4& q0, cons
 #if RT_ANY_ND_RECOMPUTE
   // normalize(d) recomputed here (same IEEE divisions as make_ray, same
   // bits) instead of keeping it live through the whole any-hit walk
-  f3 nd{r.d.x / r.dlen, r.d.y / r.dlen, r.d.z / r.dlen};
-  f3 out = add(r.o, scale(nd, t * r.dlen));
+#if RT_ANY_DLEN_RECOMPUTE
+  float dlen = length(r.d);  // = make_ray's r.dlen, same operations
+#else
+  float dlen = r.dlen;
+#endif
+  f3 nd{r.d.x / dlen, r.d.y / dlen, r.d.z / dlen};
+  f3 out = add(r.o, scale(nd, t * dlen));
   return (double)length(sub(out, r.o)) > 0.01;
 #else
   f3 out;
