@@ -104,12 +104,20 @@ __device__ __forceinline__ bool mt_candidate(f3 o, f3 d, f3 v0, f3 e1, f3 e2, fl
 #endif
 }
 
+#ifndef RT_BEST_T
+#define RT_BEST_T 0  // measured: C5 15.40/15.53 (on) vs 15.63/15.36 ms (off), C3 no better
+#endif
+
 struct Best {
   float dist;  // +inf = none
   float t_cut; // parametric bound beyond which no triangle can win (+inf = none)
   uint32_t prim, obj;
   float u, v;
+#if RT_BEST_T
+  float t;  // MT t of the winner; the hit point is recomputed from it (hit_pt)
+#else
   f3 pt;
+#endif
 };
 
 __device__ __forceinline__ void consider(const Ray& r, const float4& q0, const float4& q1,
@@ -132,7 +140,11 @@ __device__ __forceinline__ void consider(const Ray& r, const float4& q0, const f
     b.obj = __float_as_uint(q2.z);
     b.u = u;
     b.v = v;
+#if RT_BEST_T
+    b.t = t;
+#else
     b.pt = out;
+#endif
   }
 }
 
@@ -1262,7 +1274,11 @@ __device__ __forceinline__ col trace_path(const KParams& p, bool valid, f3 o, f3
     b.prim = 0xffffffffu;
     b.obj = 0;
     b.u = b.v = 0.0f;
+#if RT_BEST_T
+    b.t = 0.0f;
+#else
     b.pt = o;
+#endif
     closest_q<ACCEL, COUNT>(p, r, alive, depth, b, s, w, wc);
     bool hit = alive && b.dist != __builtin_inff();
     f3 N = f3{0.0f, 0.0f, 0.0f};
@@ -1277,7 +1293,13 @@ __device__ __forceinline__ col trace_path(const KParams& p, bool valid, f3 o, f3
     wc.zero_normal += (uint32_t)__popcll(__ballot(zero));
     hit = hit && !zero;
     const float* m = p.mat + RT_MAT_FLOATS_D * (hit ? b.obj : 0u);
-    col local = apply_light<ACCEL, COUNT>(p, hit, m, b.pt, N, s, w, wc);
+#if RT_BEST_T
+    // the winner's hit point, same operations as hit_dist (same bits)
+    f3 P = hit ? add(r.o, scale(r.nd, b.t * r.dlen)) : o;
+#else
+    f3 P = b.pt;
+#endif
+    col local = apply_light<ACCEL, COUNT>(p, hit, m, P, N, s, w, wc);
     alive = hit;
 #ifdef RT_DBG_NO_BOUNCE  // timing breakdown only (wrong images)
     alive = false;
@@ -1290,7 +1312,7 @@ __device__ __forceinline__ col trace_path(const KParams& p, bool valid, f3 o, f3
       } else {
         terms[depth++] = color_mul(local, coef);
         d = bounce_dir(d, N);
-        o = b.pt;
+        o = P;
         coef = m[10] * coef;
       }
     }
