@@ -59,6 +59,10 @@ typedef struct rt_stats {
   unsigned long long zero_normal;      /* winners with an exactly-zero interpolated normal */
   unsigned long long pixels;
   unsigned long long hits;             /* closest-hit queries that hit geometry */
+  /* camera-ray exactness: triangles whose float test the
+   * octree slack cannot guarantee, their tile-list entries (each tested by
+   * the 64 pixels x 4 samples of the tile), and those every camera ray tests */
+  unsigned long long cand_prims, cand_entries, cand_global;
 } rt_stats;
 
 /* Sizes of the device-side scene image, for the roofline accounting. */
@@ -129,6 +133,22 @@ int rt_hip_stats(rt_hip_ctx *ctx, rt_stats *out);
 int rt_hip_set_cull_slack(rt_hip_ctx *ctx, float ulps);
 /* Instrumented build: also count node visits and triangle tests (slower). */
 int rt_hip_set_count_work(rt_hip_ctx *ctx, int enable);
+/* Exact camera rays (default 1): per-frame candidate lists of the triangles
+ * whose float Moller-Trumbore error region the octree slack does not cover
+ * (csrc/rt_cand.hip).  0 = octree walk only (A/B timing; cpu/rt parity is
+ * then not guaranteed for grazing camera rays). */
+int rt_hip_set_exact_camera(rt_hip_ctx *ctx, int enable);
+/* Scale of the error-bound constants the candidate lists use (1 = the
+ * proven bound of tools/mt_bound.py; smaller = a calibrated model, faster,
+ * exactness then verified rather than proven). */
+int rt_hip_set_camera_bound_scale(rt_hip_ctx *ctx, double scale);
+/* Host-only survey of the camera candidate lists of a scene's frame (no
+ * device): out = {safe, footprint, global} triangle counts, tile entries,
+ * then 16 log2 buckets of triangles by entries and 16 of their entries;
+ * use_leaves: also accept triangles whose error region fits a leaf box of the
+ * host-built octree. */
+int rt_cand_survey(const rt_scene *scene, float eps_ulps, double bound_scale, int threads,
+                   int use_leaves, unsigned long long out[36]);
 
 /* d_gathered = nranks consecutive tile buffers (rank-major, as an RCCL gather
  * delivers them); writes the PPM-order image (W*H*3 floats) to d_rgb. */

@@ -103,11 +103,17 @@ int rt_scene_write_svati(const rt_scene *scene, const char *path);
 int rt_scene_write_obj(const rt_scene *scene, const char *path);
 
 /* Deterministic synthetic scene: a grid of
- * gx*gy smooth UV spheres of `tris_per_sphere` (rounded to the nearest
- * stacks*slices*2 decomposition) triangles each plus a ground quad,
- * splitmix64(seed) jitter; camera set to width x height. */
+ * gx*gy smooth UV spheres of about `tris_per_sphere` triangles each (the
+ * 2*slices*(stacks-1) decomposition nearest to it with slices/stacks in
+ * [1.5, 2.2], i.e. near-square quads) plus a ground quad, splitmix64(seed)
+ * jitter; camera set to width x height.  C5 = 32 x 32 spheres of 9776
+ * triangles (53 stacks x 94 slices) = 10,010,626 triangles. */
 int rt_scene_synthetic(unsigned gx, unsigned gy, unsigned tris_per_sphere, unsigned long long seed,
                        int width, int height, rt_scene **out);
+/* The same field with an explicit stacks x slices tessellation (round 1's
+ * C5 was 258 x 19: 27:1 sliver triangles). */
+int rt_scene_synthetic_uv(unsigned gx, unsigned gy, unsigned stacks, unsigned slices,
+                          unsigned long long seed, int width, int height, rt_scene **out);
 
 size_t rt_scene_triangle_count(const rt_scene *scene);
 void rt_scene_free(rt_scene *scene);

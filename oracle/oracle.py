@@ -79,6 +79,49 @@ class OracleScene:
             self.ptr = None
 
 
+class DiagQuery(C.Structure):
+    """struct or_diag_query (oracle/diag.c)."""
+    _fields_ = [("kind", C.c_int), ("depth", C.c_int), ("sample", C.c_int), ("result", C.c_int),
+                ("o", C.c_float * 3), ("d", C.c_float * 3), ("obj", C.c_int), ("tri", C.c_int),
+                ("dist", C.c_float), ("naccept", C.c_int), ("u", C.c_double), ("v", C.c_double),
+                ("cosn", C.c_double), ("need", C.c_double), ("S", C.c_double),
+                ("inplane", C.c_double), ("shape", C.c_double), ("kbary", C.c_double)]
+
+    KINDS = ("camera", "reflection", "shadow_dir", "shadow_point")
+
+    def as_dict(self):
+        d = {k: getattr(self, k) for k, _ in self._fields_}
+        d["o"] = list(self.o)
+        d["d"] = list(self.d)
+        d["kind"] = self.KINDS[self.kind]
+        return d
+
+
+_diag = None
+
+
+def diag_pixel(scene_ptr, row, col, max_queries=512):
+    """Every query of one pixel's oracle path with its deciding triangle and
+    that triangle's conditioning (oracle/diag.c).  Returns (queries, rgb)."""
+    global _diag
+    if _diag is None:
+        path = os.path.join(HERE, "_build", "liboracle_diag.so")
+        if not os.path.exists(path):
+            build()
+        _diag = C.CDLL(path)
+        _diag.oracle_diag_pixel.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int,
+                                            C.c_void_p]
+        _diag.oracle_diag_pixel.restype = C.c_int
+    buf = (DiagQuery * max_queries)()
+    rgb = np.zeros(3, np.float32)
+    ptr = scene_ptr.ptr if isinstance(scene_ptr, OracleScene) else scene_ptr
+    if not isinstance(ptr, C.c_void_p):
+        ptr = C.cast(ptr, C.c_void_p)
+    n = _diag.oracle_diag_pixel(ptr, int(row), int(col), buf, max_queries,
+                                rgb.ctypes.data_as(C.c_void_p))
+    return [buf[i].as_dict() for i in range(min(n, max_queries))], rgb
+
+
 def render(scene_ptr, width, height, pixels=None, threads=0):
     """Render with the oracle.  scene_ptr: an oracle scene or a product rt_scene*
     (same C layout).  pixels: None (whole frame, PPM order) or an (N, 2) int

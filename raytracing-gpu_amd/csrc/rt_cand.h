@@ -1,0 +1,66 @@
+// rt_cand.h -- per-frame camera-ray candidate lists (csrc/rt_cand.hip).
+//
+// Exactness of the octree walk for camera rays: a triangle
+// whose float Moller-Trumbore error region (tools/mt_bound.py) fits inside
+// the walk's culling slack is found by the walk; every other triangle is
+// rasterised, with its whole error region, into the candidate lists of the
+// 8x8 tiles whose camera rays could pass through that region, and the render
+// kernel tests those candidates exactly after the walk.  Not part of the
+// public C ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+struct CandParams {
+  const float4* tri;      // prim-order triangle records (3 float4 each)
+  const float4* node;     // octree nodes (2 float4 each: box + words), may be NULL
+  const uint32_t* prim_leaf;  // nprim: a leaf holding a record of the prim (NULL: none)
+  uint32_t nprim;
+  double pos[3];          // eye (camera position)
+  double u[3], v[3];      // image-plane axes (normalised camera u, v)
+  double C[3];            // image-plane origin
+  double n[3];            // unit normal of the image plane (u x v)
+  double plane;           // (C - pos) . n
+  double ginv[3];         // inverse Gram matrix of (u, v): [g0 g1; g1 g2]
+  double gscale;          // a bound of its norm
+  double lmax;            // max |o - pos| over the frame's camera origins
+  double omax;            // max |o| over them
+  double dline;           // max distance of a float camera line from pos
+  double dorig;           // float rounding of a camera origin (world units)
+  double eps_avail;       // culling slack every camera ray gets, minus the slab test's rounding
+  double c_dot, c_a;      // error-bound constants (tools/mt_bound.py C_DOT, C_A)
+  double kmin, kmax, lmin, lmax_;  // sample coordinates of the frame
+  int W, H, tiles_x, tiles_y, rank, nranks, ntiles_local;
+  uint32_t* visits;       // nprim + 1: tile entries of each prim (pass 1)
+  const uint32_t* off;    // nprim + 1: exclusive scan of visits
+  uint32_t* keys;         // entries: local tile index (pass 2)
+  uint32_t* vals;         // entries: prim
+  uint32_t* global;       // nprim: prims whose footprint is unbounded
+  uint32_t* ctr;          // [1] global prims, [2] big footprints
+  uint32_t* big;          // nprim: prims with more than kBig entries
+  float* skip;            // nprim: depth-skip bound of each listed prim
+};
+
+// Host mirror for surveys (same classify/raster code): safe / footprint /
+// global triangle counts, tile entries of this rank, and a log2 histogram of
+// entries per footprint triangle.
+extern "C" void rt_cand_survey_host(const CandParams* p, const float* tri, const float* node,
+                                    const uint32_t* prim_leaf, int threads,
+                                    unsigned long long out[36]);
+// prim_leaf[prim] = a leaf node holding a record of prim (scene build time)
+extern "C" hipError_t rt_cand_prim_leaf(const float4* node, uint32_t nnode, const float4* tri,
+                                        uint32_t* prim_leaf, hipStream_t s);
+
+// pass 1 (per-prim tile counts) -> exclusive scan -> pass 2 ((tile, prim)
+// pairs at the prims' offsets) -> radix sort by tile -> per-tile offsets
+extern "C" hipError_t rt_cand_count(const CandParams* p, hipStream_t s);
+extern "C" hipError_t rt_cand_emit(const CandParams* p, hipStream_t s);
+extern "C" hipError_t rt_cand_big(const CandParams* p, uint32_t nbig, hipStream_t s);
+extern "C" hipError_t rt_cand_scan(const uint32_t* in, uint32_t* out, uint32_t n, void* temp,
+                                   size_t* temp_bytes, hipStream_t s);
+extern "C" hipError_t rt_cand_sort(uint32_t* keys_in, uint32_t* keys_out, uint32_t* vals_in,
+                                   uint32_t* vals_out, uint32_t n, int bits, void* temp,
+                                   size_t* temp_bytes, hipStream_t s);
+extern "C" hipError_t rt_cand_bounds(const uint32_t* keys, uint32_t n, uint32_t* start,
+                                     uint32_t ntiles, hipStream_t s);

@@ -1,0 +1,652 @@
+// rt_cand.hip -- per-frame camera-ray candidate lists: the part of the
+// closest-hit decision of camera rays that the octree's culling slack cannot
+// guarantee (DESIGN.md §2 "Exact camera rays").
+//
+// cpu/rt tests every triangle for every ray in float (/root/reference/cpu/
+// hit.c:15-33, 72-91).  For a ray nearly parallel to a triangle's plane that
+// float test accepts crossings far outside the triangle, so a walk that culls
+// by the exact geometry can lose the reference's winner.  The forward error
+// bound of the float test (tools/mt_bound.py, checked there against the float
+// test itself) says: a float accept implies the exact line crosses the
+// triangle's plane inside the expanded triangle
+//     T_D = { v0 + U e1 + V e2 : U >= -du, V >= -dv, U + V <= 1 + dw }
+// with du, dv, dw ~ eps |o - v0| |e| / |a|, |a| = |d| |e1 x e2| |cos|.
+// Camera rays all pass (within dline) through the eye, so for a triangle the
+// grazing cosine of every camera ray near it is bounded below by
+// (distance of the eye from the plane) / (distance to the eye); that bound
+// gives T_D per triangle.  If T_D lies within the walk's slack of the
+// triangle the walk finds it (the triangle is "safe"); otherwise T_D is
+// projected through the eye onto the image plane (it is planar, so its
+// footprint is the triangle of its projected corners), widened by the float
+// deviation of camera lines, and rasterised into the 8x8 tiles of this rank.
+// Triangles with an unbounded footprint (T_D reaching the eye plane) go to a
+// global list every camera ray tests.  Count pass -> rocPRIM exclusive scan
+// -> fill pass; the render kernel tests each tile's list after its walk with
+// the reference's exact arithmetic (consider()).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstring>  // rocPRIM's iterators use memset
+
+#include <rocprim/rocprim.hpp>
+
+#include "rt_cand.h"
+
+namespace rtc {
+
+constexpr double kEps = 0x1p-24;             // float unit roundoff
+constexpr double kAMin = 9.99999997e-08;     // (double)(float)1e-7, cpu/hit.c:7
+constexpr double kDMin = 1.0 - 4.0 * kEps;   // |normalize(.)| of a float vector
+constexpr double kDMax = 1.0 + 4.0 * kEps;
+
+#define RTC_FN __host__ __device__ __forceinline__
+
+RTC_FN double dot3(const double* a, const double* b) {
+  return a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
+}
+RTC_FN double norm3(const double* a) { return sqrt(dot3(a, a)); }
+RTC_FN double dist3(const double* a, const double* b) {
+  double x = a[0] - b[0], y = a[1] - b[1], z = a[2] - b[2];
+  return sqrt(x * x + y * y + z * z);
+}
+
+enum { SAFE = 0, FOOTPRINT = 1, GLOBAL = 2 };
+
+// The camera samples a triangle can be a float-MT candidate for, as a
+// superset: (projected T_D widened by dimg, if tri_ok) intersected with the
+// band of lines nearly parallel to the triangle's plane, |b0 + b1 k + b2 l|
+// <= hw (b = n . (pos - o(k, l)), world units); plus, for very large
+// triangles whose |a| error can reach the 1e-7 threshold, the thinner band
+// hw0 of the lines too parallel to bound (c_ok > 0).
+struct Footprint {
+  int tri_ok;
+  double k[3], l[3], dimg;
+  double b0, b1, b2, hw, hw0;
+  float skip;  // lower bound of (float new_dist) - |pos - o| over the candidate crossings
+};
+
+// point-triangle distance (double): closest point by the edge/interior cases
+RTC_FN double pt_tri_dist(const double* x, const double* a, const double* b, const double* c) {
+  double ab[3], ac[3], ax[3];
+  for (int i = 0; i < 3; i++) {
+    ab[i] = b[i] - a[i];
+    ac[i] = c[i] - a[i];
+    ax[i] = x[i] - a[i];
+  }
+  const double n[3] = {ab[1] * ac[2] - ab[2] * ac[1], ab[2] * ac[0] - ab[0] * ac[2],
+                       ab[0] * ac[1] - ab[1] * ac[0]};
+  const double nn = dot3(n, n);
+  if (nn > 0.0) {  // interior: barycentrics of the projection
+    double t[3] = {ab[1] * ax[2] - ab[2] * ax[1], ab[2] * ax[0] - ab[0] * ax[2],
+                   ab[0] * ax[1] - ab[1] * ax[0]};
+    double s[3] = {ax[1] * ac[2] - ax[2] * ac[1], ax[2] * ac[0] - ax[0] * ac[2],
+                   ax[0] * ac[1] - ax[1] * ac[0]};
+    const double v = dot3(t, n) / nn, u = dot3(s, n) / nn;
+    if (u >= 0.0 && v >= 0.0 && u + v <= 1.0) return fabs(dot3(ax, n)) / sqrt(nn);
+  }
+  double best = 1e300;
+  const double* P[3] = {a, b, c};
+  for (int e = 0; e < 3; e++) {
+    const double* p0 = P[e];
+    const double* p1 = P[(e + 1) % 3];
+    double d[3], w[3];
+    for (int i = 0; i < 3; i++) {
+      d[i] = p1[i] - p0[i];
+      w[i] = x[i] - p0[i];
+    }
+    const double dd = dot3(d, d);
+    double t = dd > 0.0 ? dot3(w, d) / dd : 0.0;
+    t = t < 0.0 ? 0.0 : (t > 1.0 ? 1.0 : t);
+    double z[3] = {w[0] - t * d[0], w[1] - t * d[1], w[2] - t * d[2]};
+    best = fmin(best, norm3(z));
+  }
+  return best;
+}
+
+// Classify one triangle (record r: v0, e1, e2 as floats) and build its footprint.
+RTC_FN int classify(const CandParams& p, const float* r, const float* leafbox, Footprint& fp) {
+  const double v0[3] = {r[0], r[1], r[2]}, e1[3] = {r[3], r[4], r[5]}, e2[3] = {r[6], r[7], r[8]};
+  const double v1[3] = {v0[0] + e1[0], v0[1] + e1[1], v0[2] + e1[2]};
+  const double v2[3] = {v0[0] + e2[0], v0[1] + e2[1], v0[2] + e2[2]};
+  const double l1 = norm3(e1), l2 = norm3(e2);
+  const double n[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2],
+                       e1[0] * e2[1] - e1[1] * e2[0]};
+  const double nl = norm3(n);
+  double e_a = p.c_a * kEps * l1 * l2 * kDMax;
+  if (nl * kDMax + e_a < kAMin) return SAFE;  // |a| < 1e-7 for every ray: never accepted
+  const double nh[3] = {n[0] / nl, n[1] / nl, n[2] / nl};
+  const double pv[3] = {p.pos[0] - v0[0], p.pos[1] - v0[1], p.pos[2] - v0[2]};
+  const double deye = fabs(dot3(nh, pv));
+  const double smax = p.lmax + norm3(pv);  // |o - v0| <= |o - pos| + |pos - v0|
+  double e_sh = p.c_dot * kEps * smax * kDMax * l2;
+  double e_dq = p.c_dot * kEps * smax * kDMax * l1;
+  double e_eq = p.c_dot * kEps * smax * l1 * l2;
+  // lines with grazing cosine c: |a| >= a_lb(c); the bound of
+  // tools/mt_bound.py needs rho = e_a / a_lb < 1/2, i.e. c >= c_ok
+  const double c_ok = kAMin >= 2.0 * e_a ? 0.0 : 3.0 * e_a / (kDMin * nl);
+  auto alb = [&](double c) { return fmax(kAMin, kDMin * nl * c - e_a); };
+  double P[3][3];
+  // T_D(c) corners; returns how far they reach beyond the triangle
+  auto expand = [&](double c, double& rho_o, double& a_o) {
+    const double a = alb(c), rho = e_a / a;
+    const double du = e_sh / (a * (1.0 - rho)), dv = e_dq / (a * (1.0 - rho));
+    const double dw = (4.0 * kEps + (e_sh + e_dq) / a + rho) / (1.0 - rho);
+    for (int k = 0; k < 3; k++) {
+      P[0][k] = v0[k] - du * e1[k] - dv * e2[k];
+      P[1][k] = v0[k] + (1.0 + dw + dv) * e1[k] - dv * e2[k];
+      P[2][k] = v0[k] - du * e1[k] + (1.0 + dw + du) * e2[k];
+    }
+    rho_o = rho;
+    a_o = a;
+    return fmax(dist3(P[0], v0), fmax(dist3(P[1], v1), dist3(P[2], v2)));
+  };
+  // K' >= c H(c) over every c >= c_ok: with a_lb = dmin nl c - e_a, c H(c)
+  // is a convex rational function of c, so its maximum is at an end point
+  double rho = 0.0, a_lb = 0.0, kmax_ch;
+  const double ck = fmax(c_ok, (kAMin + e_a) / (kDMin * nl));  // kink of a_lb(c)
+  {
+    double rr, aa;
+    kmax_ch = fmax(fmin(ck, 1.0) * expand(fmin(ck, 1.0), rr, aa), expand(1.0, rr, aa));
+  }
+  // smallest grazing cosine of a camera line through T_D: such a line
+  // passes within dline of the eye, so c >= (deye - dline) / (|X - pos| +
+  // dline) with |X - pos| <= max |v - pos| + H(c), and c H(c) <= K'
+  double vmax = 0.0;
+  {
+    const double* V[3] = {v0, v1, v2};
+    for (int k = 0; k < 3; k++) vmax = fmax(vmax, dist3(V[k], p.pos));
+  }
+  double cl = fmax(c_ok, (deye - p.dline - kmax_ch) / (vmax + p.dline));
+  double hreach = expand(cl, rho, a_lb);
+  // Second round, componentwise (tools/mt_bound.py stress_cw): every
+  // candidate line crosses T_D, so its direction lies in the cone from the
+  // eye to T_D's bounding sphere, which bounds each |d_i| and |S_i| =
+  // |o_i - v0_i| <= lmax |d_i| + |pos_i - v0_i|; the sums
+  //   E_sh <= 6.01 eps sum |S_i| M_i,  M_i = |d_j| |e2_k| + |d_k| |e2_j|
+  //   E_dq <= 6.01 eps sum |d_i| N_i,  N_i = |S_j| |e1_k| + |S_k| |e1_j|
+  //   E_eq <= 6.01 eps sum |e2_i| N_i, E_a <= 5.01 eps sum |e1_i| M_i
+  // are much smaller than their Cauchy-Schwarz versions for camera rays.
+  if (c_ok == 0.0) {
+    double q[3], qr = 0.0;
+    for (int a = 0; a < 3; a++) q[a] = (P[0][a] + P[1][a] + P[2][a]) / 3.0;
+    for (int k = 0; k < 3; k++) qr = fmax(qr, dist3(P[k], q));
+    const double R = dist3(q, p.pos);
+    if (R > 2.0 * (qr + p.dline)) {
+      const double st = (qr + p.dline) / R * 1.42 + 8.0 * kEps;  // |d - q^| <= 2 sin(theta / 2)
+      double dm[3], sm[3], ae1[3], ae2[3];
+      for (int a = 0; a < 3; a++) {
+        dm[a] = fmin(1.0, fabs(q[a] - p.pos[a]) / R + st) * kDMax;
+        sm[a] = ((p.lmax + p.dline) * dm[a] + fabs(pv[a]) + p.dline) * (1.0 + 1e-9);
+        ae1[a] = fabs(e1[a]);
+        ae2[a] = fabs(e2[a]);
+      }
+      double M[3], N[3];
+      for (int i = 0; i < 3; i++) {
+        const int j = (i + 1) % 3, k = (i + 2) % 3;
+        M[i] = dm[j] * ae2[k] + dm[k] * ae2[j];
+        N[i] = sm[j] * ae1[k] + sm[k] * ae1[j];
+      }
+      const double cw = p.c_dot / 8.6 * 6.01 * kEps, ca = p.c_a / 7.2 * 5.01 * kEps;
+      const double w_sh = cw * (sm[0] * M[0] + sm[1] * M[1] + sm[2] * M[2]);
+      const double w_dq = cw * (dm[0] * N[0] + dm[1] * N[1] + dm[2] * N[2]);
+      const double w_eq = cw * (ae2[0] * N[0] + ae2[1] * N[1] + ae2[2] * N[2]);
+      const double w_a = ca * (ae1[0] * M[0] + ae1[1] * M[1] + ae1[2] * M[2]);
+      if (w_sh < e_sh) e_sh = w_sh;
+      if (w_dq < e_dq) e_dq = w_dq;
+      if (w_eq < e_eq) e_eq = w_eq;
+      if (w_a < e_a) e_a = w_a;
+      double rr, aa;
+      const double ck2 = fmax(c_ok, (kAMin + e_a) / (kDMin * nl));
+      kmax_ch = fmax(fmin(ck2, 1.0) * expand(fmin(ck2, 1.0), rr, aa), expand(1.0, rr, aa));
+      cl = fmax(cl, (deye - p.dline - kmax_ch) / (vmax + p.dline));
+      hreach = expand(cl, rho, a_lb);
+    }
+  }
+  const double rmax = fmax(dist3(P[0], p.pos), fmax(dist3(P[1], p.pos), dist3(P[2], p.pos)));
+  const double derr = kDMax * e_eq / (a_lb * (1.0 - rho)) +
+                      (rmax + p.lmax) * (rho + 4.0 * kEps) / (1.0 - rho) +
+                      4.0 * kEps * (p.omax + rmax + p.lmax);
+  // safe: every crossing point lies within the slack of the box of a leaf
+  // holding the triangle (so the walk visits that leaf and tests it), and
+  // the float distance error cannot push it past the walk's pruning
+  if (c_ok == 0.0 && derr <= 2.0 * p.eps_avail) {
+    if (hreach <= p.eps_avail) return SAFE;
+    if (leafbox) {
+      const double e = p.eps_avail;
+      bool in = true;
+      for (int k = 0; k < 3 && in; k++)
+        for (int a = 0; a < 3 && in; a++)
+          in = P[k][a] >= (double)leafbox[a] - e && P[k][a] <= (double)leafbox[4 + a] + e;
+      if (in) return SAFE;
+    }
+  }
+  // band: a candidate line at cosine c crosses the plane |h'| / c from a
+  // point within dline of the eye, within H(c) of the triangle, so
+  // c (r_T - dline) - (deye + dline) <= c H(c) <= K' (max over c >= c_ok)
+  const double rT = pt_tri_dist(p.pos, v0, v1, v2);
+  if (!(rT > 2.0 * p.dline + 1e-9)) return GLOBAL;
+  const double c_band = fmin(1.0, (deye + p.dline + kmax_ch) / (rT - p.dline));
+  const double wide = p.lmax + p.dline + p.dorig;
+  fp.b0 = dot3(nh, p.pos) - dot3(nh, p.C);
+  fp.b1 = -dot3(nh, p.u);
+  fp.b2 = -dot3(nh, p.v);
+  fp.hw = c_band * wide + p.dline + p.dorig + 1e-9 * wide;
+  fp.hw0 = c_ok > 0.0 ? c_ok * wide + p.dline + p.dorig + 1e-9 * wide : -1.0;
+  // the projected T_D, valid when it stays on one side of the eye plane
+  fp.tri_ok = 0;
+  double yn[3];
+  for (int k = 0; k < 3; k++) {
+    const double Y[3] = {P[k][0] - p.pos[0], P[k][1] - p.pos[1], P[k][2] - p.pos[2]};
+    yn[k] = dot3(Y, p.n);
+  }
+  const double rmin = pt_tri_dist(p.pos, P[0], P[1], P[2]);
+  const double ymag = rmax + 1.0;
+  if (rmin > 1e-6 && (fmin(yn[0], fmin(yn[1], yn[2])) > 1e-9 * ymag ||
+                      fmax(yn[0], fmax(yn[1], yn[2])) < -1e-9 * ymag)) {
+    fp.tri_ok = 1;
+    for (int k = 0; k < 3; k++) {
+      const double lam = p.plane / yn[k];
+      double w[3];
+      for (int c = 0; c < 3; c++) w[c] = p.pos[c] + lam * (P[k][c] - p.pos[c]) - p.C[c];
+      const double b1 = dot3(w, p.u), b2 = dot3(w, p.v);
+      fp.k[k] = p.ginv[0] * b1 + p.ginv[1] * b2;
+      fp.l[k] = p.ginv[1] * b1 + p.ginv[2] * b2;
+    }
+    // a float camera line through X passes within dline of the eye: at the
+    // image plane it lands within dline (1 + lmax / |X - pos|) of X's projection
+    fp.dimg = 1.5 * p.gscale * (p.dline * (1.0 + p.lmax / rmin) + p.dorig) + 1e-3;
+  }
+  // depth skip: new_dist >= |pos - o| + |X - pos| - 2 dline - derr
+  const double sk = c_ok > 0.0 ? -1e30 : rmin - 2.0 * p.dline - derr - 1e-6 * (p.lmax + rmax) - 1e-3;
+  fp.skip = sk > 0.0 ? (float)(sk * (1.0 - 1e-6)) : -1e30f;
+  return FOOTPRINT;
+}
+
+// Fast, conservative float version of classify()'s SAFE test (no leaf box):
+// every quantity is a positive magnitude computed in a few float operations,
+// bounded with explicit margins, so a true result is a proof on its own.
+// Most triangles of a frame take this exit.
+__device__ __forceinline__ bool quick_safe(const CandParams& p, const float* r) {
+  const float fe = 5.9604645e-8f;
+  const float e1x = r[3], e1y = r[4], e1z = r[5], e2x = r[6], e2y = r[7], e2z = r[8];
+  const float l1 = sqrtf(e1x * e1x + e1y * e1y + e1z * e1z) * 1.00001f;
+  const float l2 = sqrtf(e2x * e2x + e2y * e2y + e2z * e2z) * 1.00001f;
+  const float nx = e1y * e2z - e1z * e2y, ny = e1z * e2x - e1x * e2z, nz = e1x * e2y - e1y * e2x;
+  const float nl = sqrtf(nx * nx + ny * ny + nz * nz);
+  // |n| and its direction carry an absolute error <= 4 eps |e1| |e2|
+  const float nerr = 4.0f * fe * l1 * l2;
+  if (!(nl > 64.0f * nerr)) return false;
+  const float nlo = nl - nerr;
+  float e_a = (float)p.c_a * fe * l1 * l2 * 1.0001f;
+  const float amin = 9.99999975e-08f;
+  if (amin < 2.0f * e_a) return false;
+  const float px = (float)p.pos[0] - r[0], py = (float)p.pos[1] - r[1], pz = (float)p.pos[2] - r[2];
+  const float pvl = sqrtf(px * px + py * py + pz * pz) * 1.00001f + 1e-6f;
+  const float deye = fabsf(nx * px + ny * py + nz * pz) / nl;
+  const float deye_lb = deye - pvl * (2.0f * nerr / nlo + 8.0f * fe) - 1e-6f;
+  const float smax = ((float)p.lmax + pvl) * 1.00001f;
+  float e_sh = (float)p.c_dot * fe * smax * l2 * 1.0001f;
+  float e_dq = (float)p.c_dot * fe * smax * l1 * 1.0001f;
+  float e_eq = (float)p.c_dot * fe * smax * l1 * l2 * 1.0001f;
+  const float dmin = 1.0f - 4.0f * fe;
+  // H(c) <= (du + dv + dw) (l1 + l2) with a = a_lb(c)
+  auto H = [&](float c, float& a_o, float& rho_o) {
+    const float a = fmaxf(amin, (dmin * nlo * c - e_a) * 0.99999f);
+    const float rho = e_a / a;
+    const float du = e_sh / (a * (1.0f - rho)), dv = e_dq / (a * (1.0f - rho));
+    const float dw = (4.0f * fe + (e_sh + e_dq) / a + rho) / (1.0f - rho);
+    a_o = a;
+    rho_o = rho;
+    return (du + dv + dw) * (l1 + l2) * 1.0001f;
+  };
+  float a, rho;
+  const float ck = fminf(1.0f, (amin + e_a) / (dmin * nlo) * 1.0001f);
+  const float kmax_ch = fmaxf(ck * H(ck, a, rho), H(1.0f, a, rho)) * 1.0001f;
+  float vmax = 0.0f;
+  for (int k = 0; k < 3; k++) {
+    const float ox = k == 0 ? 0.0f : (k == 1 ? e1x : e2x), oy = k == 0 ? 0.0f : (k == 1 ? e1y : e2y),
+                oz = k == 0 ? 0.0f : (k == 1 ? e1z : e2z);
+    const float qx = px - ox, qy = py - oy, qz = pz - oz;
+    vmax = fmaxf(vmax, sqrtf(qx * qx + qy * qy + qz * qz));
+  }
+  vmax = vmax * 1.00002f + 1e-6f;
+  float num = deye_lb - (float)p.dline - kmax_ch - 1e-5f * (deye + kmax_ch);
+  if (!(num > 0.0f)) return false;
+  float cl = num / (vmax + (float)p.dline) * 0.9999f;
+  float h = H(cl, a, rho);
+  // componentwise second round (see classify): the candidate lines cross
+  // T_D, inside the ball (centroid, max vertex distance + h)
+  {
+    const float cx = (e1x + e2x) / 3.0f, cy = (e1y + e2y) / 3.0f, cz = (e1z + e2z) / 3.0f;  // - v0
+    float rq = sqrtf(cx * cx + cy * cy + cz * cz);
+    rq = fmaxf(rq, sqrtf((e1x - cx) * (e1x - cx) + (e1y - cy) * (e1y - cy) + (e1z - cz) * (e1z - cz)));
+    rq = fmaxf(rq, sqrtf((e2x - cx) * (e2x - cx) + (e2y - cy) * (e2y - cy) + (e2z - cz) * (e2z - cz)));
+    rq = (rq + h) * 1.0001f + 1e-6f + (float)p.dline;
+    const float qx = cx - px, qy = cy - py, qz = cz - pz;  // centroid - pos
+    const float R = sqrtf(qx * qx + qy * qy + qz * qz) * 0.99999f;
+    if (R > 2.0f * rq) {
+      const float st = rq / R * 1.42f + 8.0f * fe + 1e-6f;
+      const float d0 = fminf(1.0f, fabsf(qx) / R + st) * 1.00001f;
+      const float d1 = fminf(1.0f, fabsf(qy) / R + st) * 1.00001f;
+      const float d2 = fminf(1.0f, fabsf(qz) / R + st) * 1.00001f;
+      const float L = ((float)p.lmax + (float)p.dline) * 1.00001f, dl = (float)p.dline + 1e-6f;
+      const float s0 = (L * d0 + fabsf(px) + dl) * 1.00001f;
+      const float s1 = (L * d1 + fabsf(py) + dl) * 1.00001f;
+      const float s2 = (L * d2 + fabsf(pz) + dl) * 1.00001f;
+      const float a1x = fabsf(e1x), a1y = fabsf(e1y), a1z = fabsf(e1z);
+      const float a2x = fabsf(e2x), a2y = fabsf(e2y), a2z = fabsf(e2z);
+      const float M0 = d1 * a2z + d2 * a2y, M1 = d2 * a2x + d0 * a2z, M2 = d0 * a2y + d1 * a2x;
+      const float N0 = s1 * a1z + s2 * a1y, N1 = s2 * a1x + s0 * a1z, N2 = s0 * a1y + s1 * a1x;
+      const float cw = (float)(p.c_dot / 8.6 * 6.01) * fe * 1.0001f;
+      const float ca = (float)(p.c_a / 7.2 * 5.01) * fe * 1.0001f;
+      e_sh = fminf(e_sh, cw * (s0 * M0 + s1 * M1 + s2 * M2));
+      e_dq = fminf(e_dq, cw * (d0 * N0 + d1 * N1 + d2 * N2));
+      e_eq = fminf(e_eq, cw * (a2x * N0 + a2y * N1 + a2z * N2));
+      e_a = fminf(e_a, ca * (a1x * M0 + a1y * M1 + a1z * M2));
+      const float ck2 = fminf(1.0f, (amin + e_a) / (dmin * nlo) * 1.0001f);
+      const float k2 = fmaxf(ck2 * H(ck2, a, rho), H(1.0f, a, rho)) * 1.0001f;
+      const float num2 = deye_lb - (float)p.dline - k2 - 1e-5f * (deye + k2);
+      if (num2 > 0.0f) cl = fmaxf(cl, num2 / (vmax + (float)p.dline) * 0.9999f);
+      h = H(cl, a, rho);
+    }
+  }
+  const float rmax = vmax + h;
+  const float derr = (e_eq / (a * (1.0f - rho)) + (rmax + (float)p.lmax) * (rho + 4.0f * fe) / (1.0f - rho) +
+                      4.0f * fe * ((float)p.omax + rmax + (float)p.lmax)) * 1.0001f;
+  return h <= (float)p.eps_avail * 0.9999f && derr <= 2.0f * (float)p.eps_avail * 0.9999f;
+}
+
+// Tiles of this rank whose camera samples can be candidates for the
+// triangle.  Pixel (r, c) samples k in [W/2 - c, W/2 - c + 1/2], l in
+// [H/2 - r, H/2 - r + 1/2] (cpu/raytracer.c:55-58 with i = W/2 - c, j = H/2 -
+// r).
+// Pixel rows [r0, r1] the footprint can reach; false: none.
+__host__ __device__ inline bool raster_rows(const CandParams& p, const Footprint& fp, int& r0, int& r1) {
+  const double hh = (double)(p.H / 2);
+  r0 = 0;
+  r1 = p.H - 1;
+  if (fp.tri_ok && fp.hw0 < 0.0) {
+    const double lmn = fmin(fp.l[0], fmin(fp.l[1], fp.l[2])) - fp.dimg;
+    const double lmx = fmax(fp.l[0], fmax(fp.l[1], fp.l[2])) + fp.dimg;
+    if (!(lmx >= p.lmin && lmn <= p.lmax_)) return false;
+    r0 = (int)fmax(0.0, ceil(hh - lmx));
+    r1 = (int)fmin((double)(p.H - 1), floor(hh - lmn + 0.5));
+  }
+  return r0 <= r1;
+}
+
+// The footprint's tiles in tile row ty (rows clipped to [r0, r1]).
+template <class F>
+__host__ __device__ void raster_row(const CandParams& p, const Footprint& fp, int ty, int r0, int r1,
+                                    F emit) {
+  const double hw_ = (double)(p.W / 2), hh = (double)(p.H / 2);
+  auto cols = [&](double a, double b, int& c0, int& c1) {  // k in [a, b] -> columns
+    c0 = (int)fmax(0.0, ceil(hw_ - b));
+    c1 = (int)fmin((double)(p.W - 1), floor(hw_ - a + 0.5));
+  };
+  // k-range of a band |b0 + b1 k + b2 l| <= hw for some l in [la, lb]
+  auto band = [&](double hw, double la, double lb, double& a, double& b) {
+    const double m = fmin(fp.b2 * la, fp.b2 * lb), M = fmax(fp.b2 * la, fp.b2 * lb);
+    const double lo = -hw - fp.b0 - M, hi = hw - fp.b0 - m;  // b1 k in [lo, hi]
+    if (fabs(fp.b1) < 1e-12) {
+      if (lo <= 0.0 && hi >= 0.0) {
+        a = -1e300;
+        b = 1e300;
+      } else {
+        a = 1e300;
+        b = -1e300;
+      }
+    } else if (fp.b1 > 0.0) {
+      a = lo / fp.b1;
+      b = hi / fp.b1;
+    } else {
+      a = hi / fp.b1;
+      b = lo / fp.b1;
+    }
+  };
+  auto put = [&](int tx) {
+    const uint32_t g = (uint32_t)ty * (uint32_t)p.tiles_x + (uint32_t)tx;
+    if ((int)(g % (uint32_t)p.nranks) == p.rank) emit(g / (uint32_t)p.nranks);
+  };
+  const int ra = ty * 8 > r0 ? ty * 8 : r0, rb = ty * 8 + 7 < r1 ? ty * 8 + 7 : r1;
+  const double la = hh - rb, lb = hh - ra + 0.5;  // l-range of the strip's samples
+  double a = -1e300, b = 1e300;
+  if (fp.tri_ok) {  // the projected T_D cut to the (widened) strip
+    const double la2 = la - fp.dimg, lb2 = lb + fp.dimg;
+    double ta = 1e300, tb = -1e300;
+    for (int i = 0; i < 3; i++) {
+      if (fp.l[i] >= la2 && fp.l[i] <= lb2) {
+        ta = fmin(ta, fp.k[i]);
+        tb = fmax(tb, fp.k[i]);
+      }
+      const int j = (i + 1) % 3;
+      const double ys[2] = {la2, lb2};
+      for (int s = 0; s < 2; s++) {
+        const double y = ys[s];
+        if ((fp.l[i] - y) * (fp.l[j] - y) < 0.0) {
+          const double t = (y - fp.l[i]) / (fp.l[j] - fp.l[i]);
+          const double x = fp.k[i] + t * (fp.k[j] - fp.k[i]);
+          ta = fmin(ta, x);
+          tb = fmax(tb, x);
+        }
+      }
+    }
+    a = ta - fp.dimg;
+    b = tb + fp.dimg;
+  }
+  double ba, bb;
+  band(fp.hw, la, lb, ba, bb);
+  a = fmax(a, ba);
+  b = fmin(b, bb);
+  int c0 = 1, c1 = 0, d0 = 1, d1 = 0;
+  if (a <= b) cols(fmax(a, p.kmin - 1.0), fmin(b, p.kmax + 1.0), c0, c1);
+  if (fp.hw0 >= 0.0) {
+    band(fp.hw0, la, lb, ba, bb);
+    if (ba <= bb) cols(fmax(ba, p.kmin - 1.0), fmin(bb, p.kmax + 1.0), d0, d1);
+  }
+  for (int tx = c0 >> 3; c0 <= c1 && tx <= (c1 >> 3); tx++) put(tx);
+  for (int tx = d0 >> 3; d0 <= d1 && tx <= (d1 >> 3); tx++)
+    if (!(c0 <= c1 && tx >= (c0 >> 3) && tx <= (c1 >> 3))) put(tx);
+}
+
+// Tiles of this rank whose camera samples can be candidates for the
+// triangle.  Pixel (r, c) samples k in [W/2 - c, W/2 - c + 1/2], l in
+// [H/2 - r, H/2 - r + 1/2] (cpu/raytracer.c:55-58 with i = W/2 - c, j = H/2 -
+// r).
+template <class F>
+__host__ __device__ void raster(const CandParams& p, const Footprint& fp, F emit) {
+  int r0, r1;
+  if (!raster_rows(p, fp, r0, r1)) return;
+  for (int ty = r0 >> 3; ty <= (r1 >> 3); ty++) raster_row(p, fp, ty, r0, r1, emit);
+}
+
+// footprints with more entries than this are emitted by a whole workgroup
+constexpr uint32_t kBig = 512;
+
+// Pass 1: classify (float fast path first), count each prim's tiles.
+__global__ __launch_bounds__(256) void count_kernel(CandParams p) {
+  const uint32_t prim = blockIdx.x * blockDim.x + threadIdx.x;
+  if (prim >= p.nprim) return;
+  const float* rec = (const float*)(p.tri + 3 * (size_t)prim);
+  uint32_t visits = 0;
+  if (!quick_safe(p, rec)) {
+    Footprint fp;
+    const float* lb = p.prim_leaf ? (const float*)(p.node + 2 * (size_t)p.prim_leaf[prim]) : nullptr;
+    const int c = classify(p, rec, lb, fp);
+    if (c == GLOBAL) {
+      p.global[atomicAdd(p.ctr + 1, 1u)] = prim;
+      p.skip[prim] = -1e30f;
+    } else if (c == FOOTPRINT) {
+      raster(p, fp, [&](uint32_t) { visits++; });
+      p.skip[prim] = fp.skip;
+      if (visits > kBig) p.big[atomicAdd(p.ctr + 2, 1u)] = prim;
+    }
+  }
+  p.visits[prim] = visits;
+}
+
+// Pass 2 (after the scan of visits): the listed prims write their (tile,
+// prim) pairs at their offsets.
+__global__ __launch_bounds__(256) void emit_kernel(CandParams p) {
+  const uint32_t prim = blockIdx.x * blockDim.x + threadIdx.x;
+  if (prim >= p.nprim) return;
+  uint32_t o = p.off[prim];
+  const uint32_t n = p.off[prim + 1] - o;
+  if (n == 0 || n > kBig) return;  // big footprints: big_kernel
+  Footprint fp;
+  const float* lb = p.prim_leaf ? (const float*)(p.node + 2 * (size_t)p.prim_leaf[prim]) : nullptr;
+  if (classify(p, (const float*)(p.tri + 3 * (size_t)prim), lb, fp) != FOOTPRINT)
+    return;  // same answer as pass 1
+  raster(p, fp, [&](uint32_t t) {
+    p.keys[o] = t;
+    p.vals[o] = prim;
+    o++;
+  });
+}
+
+// One workgroup per big footprint: its tile rows are spread over the
+// threads, a block scan places each thread's entries.
+__global__ __launch_bounds__(256) void big_kernel(CandParams p) {
+  const uint32_t prim = p.big[blockIdx.x];
+  Footprint fp;
+  const float* lb = p.prim_leaf ? (const float*)(p.node + 2 * (size_t)p.prim_leaf[prim]) : nullptr;
+  const bool ok = classify(p, (const float*)(p.tri + 3 * (size_t)prim), lb, fp) == FOOTPRINT;
+  int r0 = 0, r1 = -1;
+  const bool rows = ok && raster_rows(p, fp, r0, r1);
+  const int ty0 = r0 >> 3, ty1 = r1 >> 3, tid = threadIdx.x;
+  uint32_t cnt = 0;
+  if (rows)
+    for (int ty = ty0 + tid; ty <= ty1; ty += 256) raster_row(p, fp, ty, r0, r1, [&](uint32_t) { cnt++; });
+  __shared__ uint32_t sh[256];
+  sh[tid] = cnt;
+  __syncthreads();
+  for (int off = 1; off < 256; off <<= 1) {  // inclusive Hillis-Steele scan
+    const uint32_t y = tid >= off ? sh[tid - off] : 0u;
+    __syncthreads();
+    sh[tid] += y;
+    __syncthreads();
+  }
+  uint32_t o = p.off[prim] + sh[tid] - cnt;
+  if (rows)
+    for (int ty = ty0 + tid; ty <= ty1; ty += 256)
+      raster_row(p, fp, ty, r0, r1, [&](uint32_t t) {
+        p.keys[o] = t;
+        p.vals[o] = prim;
+        o++;
+      });
+}
+
+__global__ __launch_bounds__(256) void prim_leaf_kernel(const float4* node, uint32_t nnode,
+                                                        const float4* tri, uint32_t* prim_leaf) {
+  const uint32_t ni = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ni >= nnode) return;
+  const uint32_t first = __float_as_uint(node[2 * ni].w), info = __float_as_uint(node[2 * ni + 1].w);
+  if (!(info & 0x80000000u)) return;  // RT_NODE_LEAF
+  const uint32_t cnt = info & 0x7fffffffu;
+  for (uint32_t k = 0; k < cnt; k++) prim_leaf[__float_as_uint(tri[3 * (size_t)(first + k) + 2].y)] = ni;
+}
+
+// start[t] = first entry of tile t in the tile-sorted keys; start[n] = total
+__global__ __launch_bounds__(256) void bounds_kernel(const uint32_t* keys, uint32_t n, uint32_t* start,
+                                                     uint32_t ntiles) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t > ntiles) return;
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = lo + (hi - lo) / 2;
+    if (keys[mid] < t)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  start[t] = t == ntiles ? n : lo;
+}
+
+}  // namespace rtc
+
+#include <thread>
+#include <vector>
+
+extern "C" hipError_t rt_cand_prim_leaf(const float4* node, uint32_t nnode, const float4* tri,
+                                        uint32_t* prim_leaf, hipStream_t s) {
+  if (nnode == 0) return hipSuccess;
+  hipLaunchKernelGGL(rtc::prim_leaf_kernel, dim3((nnode + 255) / 256), dim3(256), 0, s, node, nnode,
+                     tri, prim_leaf);
+  return hipGetLastError();
+}
+
+extern "C" void rt_cand_survey_host(const CandParams* p, const float* tri, const float* node,
+                                    const uint32_t* prim_leaf, int threads,
+                                    unsigned long long out[36]) {
+  // out: [0] safe, [1] footprint, [2] global, [3] entries, [4 + k] prims
+  // with 2^k <= entries < 2^(k+1), [20 + k] their entries (k < 16)
+  if (threads < 1) threads = 1;
+  std::vector<unsigned long long> part(36 * (size_t)threads, 0);
+  std::vector<std::thread> th;
+  for (int t = 0; t < threads; t++)
+    th.emplace_back([=, &part]() {
+      unsigned long long* o = &part[36 * (size_t)t];
+      for (uint32_t i = (uint32_t)t; i < p->nprim; i += (uint32_t)threads) {
+        rtc::Footprint fp;
+        const float* lb = prim_leaf ? node + 8 * (size_t)prim_leaf[i] : nullptr;
+        const int c = rtc::classify(*p, tri + 12 * (size_t)i, lb, fp);
+        o[c]++;
+        if (c == rtc::FOOTPRINT) {
+          unsigned long long v = 0;
+          rtc::raster(*p, fp, [&](uint32_t) { v++; });
+          o[3] += v;
+          int k = 0;
+          while (k < 15 && (2ull << k) <= v) k++;
+          if (v) {
+            o[4 + k]++;
+            o[20 + k] += v;
+          }
+        }
+      }
+    });
+  for (auto& x : th) x.join();
+  for (int k = 0; k < 36; k++) {
+    out[k] = 0;
+    for (int t = 0; t < threads; t++) out[k] += part[36 * (size_t)t + k];
+  }
+}
+
+extern "C" hipError_t rt_cand_count(const CandParams* p, hipStream_t s) {
+  if (p->nprim == 0) return hipSuccess;
+  hipLaunchKernelGGL(rtc::count_kernel, dim3((p->nprim + 255) / 256), dim3(256), 0, s, *p);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t rt_cand_emit(const CandParams* p, hipStream_t s) {
+  if (p->nprim == 0) return hipSuccess;
+  hipLaunchKernelGGL(rtc::emit_kernel, dim3((p->nprim + 255) / 256), dim3(256), 0, s, *p);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t rt_cand_big(const CandParams* p, uint32_t nbig, hipStream_t s) {
+  if (nbig == 0) return hipSuccess;
+  hipLaunchKernelGGL(rtc::big_kernel, dim3(nbig), dim3(256), 0, s, *p);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t rt_cand_scan(const uint32_t* in, uint32_t* out, uint32_t n, void* temp,
+                                   size_t* temp_bytes, hipStream_t s) {
+  return rocprim::exclusive_scan(temp, *temp_bytes, in, out, 0u, (size_t)n + 1,
+                                 rocprim::plus<uint32_t>(), s);
+}
+
+extern "C" hipError_t rt_cand_sort(uint32_t* keys_in, uint32_t* keys_out, uint32_t* vals_in,
+                                   uint32_t* vals_out, uint32_t n, int bits, void* temp,
+                                   size_t* temp_bytes, hipStream_t s) {
+  return rocprim::radix_sort_pairs(temp, *temp_bytes, keys_in, keys_out, vals_in, vals_out,
+                                   (size_t)n, 0, bits, s);
+}
+
+extern "C" hipError_t rt_cand_bounds(const uint32_t* keys, uint32_t n, uint32_t* start,
+                                     uint32_t ntiles, hipStream_t s) {
+  hipLaunchKernelGGL(rtc::bounds_kernel, dim3((ntiles + 1 + 255) / 256), dim3(256), 0, s, keys, n,
+                     start, ntiles);
+  return hipGetLastError();
+}
+

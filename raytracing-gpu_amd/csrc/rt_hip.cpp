@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <cerrno>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -14,9 +15,11 @@
 #include <vector>
 
 #include "rt_build.h"
+#include "rt_cand.h"
 #include "rt_kernels.h"
 
 extern "C" {
+#include "../host/rt_cull.h"
 #include "../host/rt_internal.h"
 }
 
@@ -52,7 +55,32 @@ struct rt_hip_ctx {
   float scene_c[3]{}, scene_r = 0;
   float eps_ulps = RT_EPS_ULPS_DEFAULT;
   int min_waves = 0;  // launch-bounds variant (tuning: env RT_MIN_WAVES)
+  // exact camera rays (csrc/rt_cand.hip)
+  int exact_camera = 1;
+  double bound_scale = 1.0;  // 1 = the proven float-MT error bound (tools/mt_bound.py)
+  float4* d_tri_prim = nullptr;  // prim-order records (== d_tri for FLAT)
+  uint32_t nprim = 0;
+  uint32_t* d_cand_visits = nullptr;  // nprim + 1
+  uint32_t* d_cand_off = nullptr;     // nprim + 1
+  uint32_t* d_cand_start = nullptr;   // ntiles + 1
+  uint32_t* d_cand_keys = nullptr;    // entries (tile), emit order
+  uint32_t* d_cand_keys2 = nullptr;   // entries (tile), sorted
+  uint32_t* d_cand_vals = nullptr;    // entries (prim), emit order
+  uint32_t* d_cand_global = nullptr;  // nprim
+  uint32_t* d_cand_big = nullptr;     // nprim
+  uint32_t* d_cand_ctr = nullptr;     // 4
+  float* d_cand_skip = nullptr;       // nprim
+  uint32_t* d_prim_leaf = nullptr;    // nprim: a leaf holding each prim (camera-independent)
+  uint32_t* d_cand = nullptr;
+  size_t cand_cap = 0, cand_tiles_cap = 0;
+  void* d_scan_tmp = nullptr;
+  size_t scan_tmp_bytes = 0;
+  uint32_t* h_cand = nullptr;  // pinned: total entries, risky, global, visits
+  unsigned long long cand_prims = 0, cand_entries = 0, cand_global = 0;
 };
+
+static int cand_params(const rt_frame* f, const float scene_c[3], float scene_r, float eps_ulps,
+                       double bound_scale, int rank, int nranks, CandParams* out);
 
 static int tiles_x_of(int W) { return (W + 7) / 8; }
 static int tiles_y_of(int H) { return (H + 7) / 8; }
@@ -98,6 +126,21 @@ extern "C" void rt_hip_destroy(rt_hip_ctx* c) {
   (void)hipFree(c->d_counter);
   (void)hipFree(c->d_stats);
   (void)hipFree(c->d_spill);
+  if (c->d_tri_prim != c->d_tri) (void)hipFree(c->d_tri_prim);
+  (void)hipFree(c->d_cand_visits);
+  (void)hipFree(c->d_cand_off);
+  (void)hipFree(c->d_cand_start);
+  (void)hipFree(c->d_cand_keys);
+  (void)hipFree(c->d_cand_keys2);
+  (void)hipFree(c->d_cand_vals);
+  (void)hipFree(c->d_cand_global);
+  (void)hipFree(c->d_cand_big);
+  (void)hipFree(c->d_cand_ctr);
+  (void)hipFree(c->d_cand_skip);
+  (void)hipFree(c->d_prim_leaf);
+  (void)hipFree(c->d_cand);
+  (void)hipFree(c->d_scan_tmp);
+  if (c->h_cand) (void)hipHostFree(c->h_cand);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -155,7 +198,9 @@ extern "C" int rt_hip_create(int device, const rt_scene* scene, int accel, rt_hi
     if (he != hipSuccess) {
       rc = rt_set_error(RT_EHIP, "device octree build: %s", hipGetErrorString(he));
     } else {
-      (void)hipFree(c->d_tri);  // prim-order records -> leaf-order records
+      // leaf-order records for the walk; the prim-order ones stay for the
+      // camera candidate lists
+      c->d_tri_prim = c->d_tri;
       c->d_tri = tree.tri;
       c->d_node = tree.node;
       c->nrec = tree.nref;
@@ -169,6 +214,19 @@ extern "C" int rt_hip_create(int device, const rt_scene* scene, int accel, rt_hi
     }
   }
   auto t2 = std::chrono::steady_clock::now();
+  c->nprim = (uint32_t)fs.ntri;
+  if (!rc && !c->d_tri_prim) {
+    if (c->accel == RT_ACCEL_FLAT) {
+      c->d_tri_prim = c->d_tri;  // already prim order (no candidates needed)
+    } else {
+      rt_flat_scene fp;  // host octree: records are leaf order, with duplicates
+      rc = rt_flatten(scene, RT_ACCEL_FLAT, &fp);
+      if (!rc) {
+        rc = upload(&c->d_tri_prim, fp.tri, fp.nrec * RT_TRI_FLOATS * sizeof(float));
+        rt_flat_free(&fp);
+      }
+    }
+  }
   for (int a = 0; a < 3; a++) {
     float lo = fs.ntri ? fs.scene_lo[a] : 0.0f, hi = fs.ntri ? fs.scene_hi[a] : 0.0f;
     c->scene_c[a] = 0.5f * (lo + hi);
@@ -237,9 +295,275 @@ extern "C" int rt_hip_set_cull_slack(rt_hip_ctx* c, float ulps) {
   return RT_OK;
 }
 
+extern "C" int rt_hip_set_exact_camera(rt_hip_ctx* c, int enable) {
+  if (!c) return rt_set_error(RT_EINVAL, "null context");
+  c->exact_camera = enable ? 1 : 0;
+  return RT_OK;
+}
+
+extern "C" int rt_hip_set_camera_bound_scale(rt_hip_ctx* c, double scale) {
+  if (!c || !(scale > 0.0)) return rt_set_error(RT_EINVAL, "bad bound scale");
+  c->bound_scale = scale;
+  return RT_OK;
+}
+
+extern "C" int rt_cand_survey(const rt_scene* scene, float eps_ulps, double bound_scale, int threads,
+                              int use_leaves, unsigned long long out[36]) {
+  if (!scene || !out) return rt_set_error(RT_EINVAL, "null argument");
+  rt_frame f;
+  int rc = rt_frame_from_camera(&scene->camera, &f);
+  if (rc) return rc;
+  rt_flat_scene fs;
+  rc = rt_flatten(scene, RT_ACCEL_FLAT, &fs);
+  if (rc) return rc;
+  float sc[3], sr = 0;
+  for (int a = 0; a < 3; a++) {  // as rt_hip_create
+    float lo = fs.ntri ? fs.scene_lo[a] : 0.0f, hi = fs.ntri ? fs.scene_hi[a] : 0.0f;
+    sc[a] = 0.5f * (lo + hi);
+    sr = std::fmax(sr, 0.5f * (hi - lo));
+  }
+  CandParams cp;
+  rc = cand_params(&f, sc, sr, eps_ulps, bound_scale, 0, 1, &cp);
+  rt_flat_scene ft;  // the host octree's leaves (use_leaves)
+  std::memset(&ft, 0, sizeof ft);
+  std::vector<uint32_t> pl;
+  if (!rc && use_leaves) {
+    rc = rt_flatten(scene, RT_ACCEL_OCTREE, &ft);
+    if (!rc) {
+      pl.assign(fs.ntri + 1, 0);
+      for (size_t ni = 0; ni < ft.nnode; ni++) {
+        uint32_t first, info;
+        std::memcpy(&first, &ft.node[RT_NODE_FLOATS * ni + 3], 4);
+        std::memcpy(&info, &ft.node[RT_NODE_FLOATS * ni + 7], 4);
+        if (!(info & RT_NODE_LEAF)) continue;
+        for (uint32_t k = 0; k < RT_LEAF_COUNT(info); k++) {
+          uint32_t prim;
+          std::memcpy(&prim, &ft.tri[RT_TRI_FLOATS * (size_t)(first + k) + 9], 4);
+          pl[prim] = (uint32_t)ni;
+        }
+      }
+    }
+  }
+  if (!rc) {
+    cp.nprim = (uint32_t)fs.ntri;
+    rt_cand_survey_host(&cp, fs.tri, use_leaves ? ft.node : nullptr,
+                        use_leaves ? pl.data() : nullptr, threads, out);
+  }
+  if (use_leaves) rt_flat_free(&ft);
+  rt_flat_free(&fs);
+  return rc;
+}
+
 extern "C" int rt_hip_set_count_work(rt_hip_ctx* c, int enable) {
   if (!c) return rt_set_error(RT_EINVAL, "null context");
   c->count_work = enable ? 1 : 0;
+  return RT_OK;
+}
+
+// ---------------------------------------------------- exact camera rays
+// Frame constants of the candidate lists (csrc/rt_cand.hip) and the three
+// launches: count -> scan -> (one small read-back for the list sizes) ->
+// fill.  Everything is derived from the frame in double, rounded so that
+// each bound stays conservative.
+template <class T>
+static int grow_dev(T** p, size_t* cap, size_t need) {
+  if (need <= *cap && *p) return RT_OK;
+  (void)hipFree(*p);
+  *p = nullptr;
+  size_t n = need + need / 4 + 64;
+  HIP_TRY(hipMalloc((void**)p, n * sizeof(T)));
+  *cap = n;
+  return RT_OK;
+}
+
+static double d3dot(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+
+// Frame constants of the candidate lists for rank/nranks (no device work).
+static int cand_params(const rt_frame* f, const float scene_c[3], float scene_r, float eps_ulps,
+                       double bound_scale, int rank, int nranks, CandParams* out) {
+  const double eps = 0x1p-24;
+  CandParams& cp = *out;
+  std::memset(&cp, 0, sizeof cp);
+  const double pos[3] = {f->position.x, f->position.y, f->position.z};
+  const double u[3] = {f->u.x, f->u.y, f->u.z}, v[3] = {f->v.x, f->v.y, f->v.z};
+  const double C[3] = {f->C.x, f->C.y, f->C.z};
+  double n[3] = {u[1] * v[2] - u[2] * v[1], u[2] * v[0] - u[0] * v[2], u[0] * v[1] - u[1] * v[0]};
+  const double nn = std::sqrt(d3dot(n, n));
+  if (!(nn > 1e-6)) return rt_set_error(RT_EINVAL, "degenerate camera (u parallel to v)");
+  for (int a = 0; a < 3; a++) {
+    cp.pos[a] = pos[a];
+    cp.u[a] = u[a];
+    cp.v[a] = v[a];
+    cp.C[a] = C[a];
+    cp.n[a] = n[a] / nn;
+  }
+  const double cpos[3] = {C[0] - pos[0], C[1] - pos[1], C[2] - pos[2]};
+  cp.plane = d3dot(cpos, cp.n);
+  if (!(std::fabs(cp.plane) > 1e-6)) return rt_set_error(RT_EINVAL, "degenerate camera (L = 0)");
+  const double g00 = d3dot(u, u), g01 = d3dot(u, v), g11 = d3dot(v, v);
+  const double det = g00 * g11 - g01 * g01;
+  cp.ginv[0] = g11 / det;
+  cp.ginv[1] = -g01 / det;
+  cp.ginv[2] = g00 / det;
+  cp.gscale = std::sqrt(cp.ginv[0] * cp.ginv[0] + 2 * cp.ginv[1] * cp.ginv[1] + cp.ginv[2] * cp.ginv[2]);
+  const int W = f->width, H = f->height;
+  // samples: k = i + {0, 1/2}, i in [1 - W/2, W/2] (cpu/raytracer.c:50-58)
+  cp.kmin = 1.0 - W / 2;
+  cp.kmax = W / 2 + 0.5;
+  cp.lmin = 1.0 - H / 2;
+  cp.lmax_ = H / 2 + 0.5;
+  double lmax = 0, omax = 0;
+  for (int ci = 0; ci < 4; ci++) {  // |o - pos| and |o| are convex: corners bound them
+    const double k = (ci & 1) ? cp.kmax : cp.kmin, l = (ci & 2) ? cp.lmax_ : cp.lmin;
+    double o[3], d[3];
+    for (int a = 0; a < 3; a++) {
+      o[a] = C[a] + u[a] * k + v[a] * l;
+      d[a] = o[a] - pos[a];
+    }
+    lmax = std::fmax(lmax, std::sqrt(d3dot(d, d)));
+    omax = std::fmax(omax, std::sqrt(d3dot(o, o)));
+  }
+  cp.lmax = lmax * (1 + 1e-9) + 1e-9;
+  cp.omax = omax * (1 + 1e-9) + 1e-9;
+  // float camera line (o_f, normalize(pos - o_f)): within 2.5 eps rad of the
+  // direction towards pos, so within dline of pos; o_f within dorig of o
+  cp.dline = 6.0 * eps * cp.lmax + 1e-12;
+  cp.dorig = 8.0 * eps * (std::sqrt(d3dot(C, C)) + std::fabs(cp.kmin) + cp.kmax + std::fabs(cp.lmin) +
+                          cp.lmax_) * 1.8;
+  // smallest culling slack of a camera ray: rt_cull_eps with the max-norm
+  // |o - c| bounded below per axis over the sample rectangle
+  double mlb = 0;
+  for (int a = 0; a < 3; a++) {
+    double lo = 1e300, hi = -1e300;
+    for (int ci = 0; ci < 4; ci++) {
+      const double k = (ci & 1) ? cp.kmax : cp.kmin, l = (ci & 2) ? cp.lmax_ : cp.lmin;
+      const double x = C[a] + u[a] * k + v[a] * l - scene_c[a];
+      lo = std::fmin(lo, x);
+      hi = std::fmax(hi, x);
+    }
+    const double m = (lo <= 0 && hi >= 0) ? 0.0 : std::fmin(std::fabs(lo), std::fabs(hi));
+    mlb = std::fmax(mlb, m);
+  }
+  const double R = scene_r;
+  const double cmag = std::fmax(std::fabs(scene_c[0]), std::fmax(std::fabs(scene_c[1]),
+                                                                std::fabs(scene_c[2])));
+  const double eps_rel = (double)(eps_ulps * 5.9604645e-8f);
+  const double eps_min = (eps_rel * (std::fmax(mlb - cp.dorig, 0.0) + R) +
+                          (double)RT_CULL_PLANE * (cmag + R) + 1e-6) * (1.0 - 1e-5);
+  // the slab test's own rounding (rt_cull.h: a few ulps of |o| and of |t d|)
+  // takes 4 ulps of |o| + the scene's extent out of that slack
+  cp.eps_avail = eps_min - 8.0 * eps * (cp.omax + 2.0 * (cmag + R));
+  // tools/mt_bound.py: C_DOT = 6 sqrt 2 -> 8.6, C_A = 5 sqrt 2 -> 7.2 (scale 1 = the proven bound)
+  cp.c_dot = 8.6 * bound_scale;
+  cp.c_a = 7.2 * bound_scale;
+  cp.W = W;
+  cp.H = H;
+  cp.tiles_x = tiles_x_of(W);
+  cp.tiles_y = tiles_y_of(H);
+  cp.rank = rank;
+  cp.nranks = nranks;
+  const int ntot = cp.tiles_x * cp.tiles_y;
+  cp.ntiles_local = (ntot - rank + nranks - 1) / nranks;
+  return RT_OK;
+}
+
+static int ensure_tmp(rt_hip_ctx* c, size_t bytes) {
+  if (bytes <= c->scan_tmp_bytes && c->d_scan_tmp) return RT_OK;
+  (void)hipFree(c->d_scan_tmp);
+  c->d_scan_tmp = nullptr;
+  HIP_TRY(hipMalloc(&c->d_scan_tmp, bytes));
+  c->scan_tmp_bytes = bytes;
+  return RT_OK;
+}
+
+// count -> scan -> (read back the entry total: the only host sync) -> emit
+// -> radix sort by tile -> per-tile offsets.  No contended atomics; the list
+// order is deterministic.
+static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream_t s) {
+  CandParams cp;
+  int rc = cand_params(f, c->scene_c, c->scene_r, c->eps_ulps, c->bound_scale, kp->rank, kp->nranks, &cp);
+  if (rc) return rc;
+  cp.tri = c->d_tri_prim;
+  cp.nprim = c->nprim;
+  const size_t nt = (size_t)kp->ntiles_local;
+  const size_t np = c->nprim;
+  if (!c->d_prim_leaf && c->d_node) {  // once per scene: which leaf holds each prim
+    HIP_TRY(hipMalloc((void**)&c->d_prim_leaf, (np + 1) * sizeof(uint32_t)));
+    HIP_TRY(rt_cand_prim_leaf(c->d_node, (uint32_t)c->info.nodes, c->d_tri, c->d_prim_leaf, s));
+  }
+  cp.node = c->d_node;
+  cp.prim_leaf = c->d_prim_leaf;
+  if (!c->d_cand_global) {
+    HIP_TRY(hipMalloc((void**)&c->d_cand_visits, (np + 1) * sizeof(uint32_t)));
+    HIP_TRY(hipMalloc((void**)&c->d_cand_off, (np + 1) * sizeof(uint32_t)));
+    HIP_TRY(hipMalloc((void**)&c->d_cand_global, (np + 1) * sizeof(uint32_t)));
+    HIP_TRY(hipMalloc((void**)&c->d_cand_big, (np + 1) * sizeof(uint32_t)));
+    HIP_TRY(hipMalloc((void**)&c->d_cand_ctr, 4 * sizeof(uint32_t)));
+    HIP_TRY(hipMalloc((void**)&c->d_cand_skip, (np + 1) * sizeof(float)));
+    HIP_TRY(hipHostMalloc((void**)&c->h_cand, 4 * sizeof(uint32_t), hipHostMallocDefault));
+  }
+  if (nt + 1 > c->cand_tiles_cap) {
+    size_t cap = c->cand_tiles_cap;
+    rc = grow_dev(&c->d_cand_start, &cap, nt + 1);
+    if (rc) return rc;
+    c->cand_tiles_cap = cap;
+  }
+  cp.visits = c->d_cand_visits;
+  cp.off = c->d_cand_off;
+  cp.global = c->d_cand_global;
+  cp.big = c->d_cand_big;
+  cp.ctr = c->d_cand_ctr;
+  cp.skip = c->d_cand_skip;
+  HIP_TRY(hipMemsetAsync(c->d_cand_visits + np, 0, sizeof(uint32_t), s));
+  HIP_TRY(hipMemsetAsync(c->d_cand_ctr, 0, 4 * sizeof(uint32_t), s));
+  HIP_TRY(rt_cand_count(&cp, s));
+  size_t tb = 0;
+  HIP_TRY(rt_cand_scan(c->d_cand_visits, c->d_cand_off, (uint32_t)np, nullptr, &tb, s));
+  rc = ensure_tmp(c, tb);
+  if (rc) return rc;
+  tb = c->scan_tmp_bytes;
+  HIP_TRY(rt_cand_scan(c->d_cand_visits, c->d_cand_off, (uint32_t)np, c->d_scan_tmp, &tb, s));
+  HIP_TRY(hipMemcpyAsync(c->h_cand, c->d_cand_off + np, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(c->h_cand + 1, c->d_cand_ctr + 1, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  const uint32_t total = c->h_cand[0], nglobal = c->h_cand[1], nbig = c->h_cand[2];
+  if (total + 1 > c->cand_cap) {
+    for (uint32_t** b : {&c->d_cand_keys, &c->d_cand_vals, &c->d_cand_keys2, &c->d_cand}) {
+      (void)hipFree(*b);
+      *b = nullptr;
+    }
+    size_t cap = 0;
+    rc = grow_dev(&c->d_cand_keys, &cap, total + 1);
+    if (rc) return rc;
+    c->cand_cap = cap;
+    for (uint32_t** b : {&c->d_cand_vals, &c->d_cand_keys2, &c->d_cand})
+      HIP_TRY(hipMalloc((void**)b, c->cand_cap * sizeof(uint32_t)));
+  }
+  cp.keys = c->d_cand_keys;
+  cp.vals = c->d_cand_vals;
+  HIP_TRY(rt_cand_emit(&cp, s));
+  HIP_TRY(rt_cand_big(&cp, nbig, s));
+  int bits = 1;
+  while ((1ull << bits) <= nt) bits++;
+  tb = 0;
+  HIP_TRY(rt_cand_sort(c->d_cand_keys, c->d_cand_keys2, c->d_cand_vals, c->d_cand, total, bits,
+                       nullptr, &tb, s));
+  rc = ensure_tmp(c, tb);
+  if (rc) return rc;
+  tb = c->scan_tmp_bytes;
+  if (total)
+    HIP_TRY(rt_cand_sort(c->d_cand_keys, c->d_cand_keys2, c->d_cand_vals, c->d_cand, total, bits,
+                         c->d_scan_tmp, &tb, s));
+  HIP_TRY(rt_cand_bounds(c->d_cand_keys2, total, c->d_cand_start, (uint32_t)nt, s));
+  kp->cand_start = c->d_cand_start;
+  kp->cand = c->d_cand;
+  kp->cand_global = c->d_cand_global;
+  kp->n_cand_global = nglobal;
+  kp->tri_prim = c->d_tri_prim;
+  kp->cand_skip = c->d_cand_skip;
+  c->cand_entries = total;
+  c->cand_global = nglobal;
+  c->cand_prims = 0;  // not counted separately (entries and globals are)
   return RT_OK;
 }
 
@@ -298,6 +622,11 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
   // measured (C5): packet walks for camera rays and first reflections only;
   // deeper reflections are incoherent and walk per lane (18.9 -> 17.9 ms)
   p.packet_max_depth = pmd ? std::atoi(pmd) : 1;
+  c->cand_prims = c->cand_entries = c->cand_global = 0;
+  if (c->accel == RT_ACCEL_OCTREE && c->d_node && c->exact_camera) {
+    int rc = cand_prepare(c, f, &p, s);
+    if (rc) return rc;
+  }
   if (c->accel == RT_ACCEL_OCTREE && !c->d_node) {
     // empty scene: nothing to traverse, the FLAT kernel with 0 records is exact
     HIP_TRY(hipMemsetAsync(c->d_counter, 0, 64, s));
@@ -329,6 +658,9 @@ extern "C" int rt_hip_stats(rt_hip_ctx* c, rt_stats* out) {
   out->depth_overflow = h[5];
   out->zero_normal = h[6];
   out->hits = h[7];
+  out->cand_prims = c->cand_prims;
+  out->cand_entries = c->cand_entries;
+  out->cand_global = c->cand_global;
   if (out->depth_overflow)
     return rt_set_error(RT_EDEPTH, "%llu paths overflowed the depth/stack buffers",
                         out->depth_overflow);
@@ -420,6 +752,16 @@ extern "C" int rt_raytrace_multi(const char* input, const char* output, int ngpu
   rt_scene* scene = nullptr;
   int rc = rt_scene_load_svati(input, &scene);
   if (rc) return rc;
+  // the reference opens (truncates) the output right after parsing, before
+  // rendering, and fails there with strerror (cpu/raytracer.c:88,
+  // cpu/printer.c:5-7); the P3 text itself is written after the render
+  if (FILE* fo = std::fopen(output, "w+")) {
+    std::fclose(fo);
+  } else {
+    rc = rt_set_error(RT_EIO, "%s", std::strerror(errno));
+    rt_scene_free(scene);
+    return rc;
+  }
   rt_frame f;
   rc = rt_frame_from_camera(&scene->camera, &f);
   if (rc) {
@@ -485,6 +827,9 @@ extern "C" int rt_raytrace_multi(const char* input, const char* output, int ngpu
     sum.depth_overflow += st.depth_overflow;
     sum.zero_normal += st.zero_normal;
     sum.hits += st.hits;
+    sum.cand_prims += st.cand_prims;
+    sum.cand_entries += st.cand_entries;
+    sum.cand_global += st.cand_global;
   }
   t1 = std::chrono::steady_clock::now();
   if (rc) goto out;

@@ -51,6 +51,13 @@ struct KParams {
   int packet_min;               // hybrid: packet walk while >= this many lanes query
   int trav_shadow, packet_min_shadow;  // the same two for shadow (any-hit) queries
   int packet_max_depth;         // closest hit: packet walk only up to this bounce depth
+  // camera-ray candidate lists (csrc/rt_cand.hip); cand_start == NULL: none
+  const uint32_t* cand_start;   // ntiles_local + 1 offsets into cand
+  const uint32_t* cand;         // prims
+  const uint32_t* cand_global;  // prims every camera ray tests
+  uint32_t n_cand_global;
+  const float4* tri_prim;       // prim-order triangle records
+  const float* cand_skip;       // per prim: lower bound of new_dist - |pos - o| (depth skip)
 };
 
 // min_waves = occupancy target per SIMD (launch bounds of the instantiation:

@@ -1253,12 +1253,61 @@ __device__ col apply_light(const KParams& p, bool hit, const float* m, f3 P, f3 
   return acc;
 }
 
+// Camera rays: the triangles of this tile's candidate list (csrc/rt_cand.hip)
+// and of the global list, tested with the reference's exact arithmetic after
+// the walk -- the ones whose float Moller-Trumbore error region reaches
+// beyond the walk's culling slack.  Wave-uniform loop, scalar record loads.
+template <bool COUNT>
+__device__ __forceinline__ void cand_closest(const KParams& p, const Ray& r, bool act, uint32_t tile,
+                                             Best& b, WorkCount& wc) {
+  if (!p.cand_start || __ballot(act) == 0) return;
+  // Depth skip: a candidate's float new_dist is at least |pos - o| +
+  // cand_skip[prim] (csrc/rt_cand.hip), so one whose bound exceeds every
+  // lane's best - |pos - o| (plus the float error of that difference)
+  // cannot win here -- one scalar compare instead of a test.
+  float bl = -__builtin_inff();
+  if (act)
+    bl = b.dist == __builtin_inff() ? __builtin_inff()
+                                    : (b.dist - length(sub(p.pos, r.o))) + (2e-3f + 4e-7f * b.dist);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) bl = fmaxf(bl, __shfl_xor(bl, off));
+  const float bmax = __uint_as_float(uni(__float_as_uint(bl)));
+  const uint32_t s = uni(p.cand_start[tile]), e = uni(p.cand_start[tile + 1]);
+  const int lane = __lane_id();
+  uint32_t tested = 0;
+  // 64 entries per round trip: each lane loads one entry and its skip bound,
+  // the wave then tests the survivors one after another
+  for (uint32_t base = s; base < e; base += 64) {
+    uint32_t prim = 0;
+    bool keep = false;
+    if (base + lane < e) {
+      prim = p.cand[base + lane];
+      keep = !(p.cand_skip[prim] > bmax);
+    }
+    uint64_t m = __ballot(keep);
+    while (m) {
+      const int j = __ffsll((unsigned long long)m) - 1;
+      m &= m - 1;
+      const float4* q = p.tri_prim + 3 * (size_t)uni(__shfl(prim, j));
+      float4 q0 = ldu(q, 0), q1 = ldu(q, 1), q2 = ldu(q, 2);
+      if (act) consider(r, q0, q1, q2, b);
+      tested++;
+    }
+  }
+  for (uint32_t k = 0; k < p.n_cand_global; k++) {
+    const float4* q = p.tri_prim + 3 * (size_t)uni(p.cand_global[k]);
+    float4 q0 = ldu(q, 0), q1 = ldu(q, 1), q2 = ldu(q, 2);
+    if (act) consider(r, q0, q1, q2, b);
+  }
+  if (COUNT) wc.tris += tested + p.n_cand_global;
+}
+
 // One camera sample (cpu/raytracer.c:19-34) for every lane of the wave: the
 // recursion becomes a wave-uniform bounce loop; local terms are buffered and
 // folded deepest-first.  valid = the lane owns a pixel.
 template <int ACCEL, bool COUNT>
 __device__ __forceinline__ col trace_path(const KParams& p, bool valid, f3 o, f3 d, float coef, Stack& s,
-                          WaveCtx& w, WorkCount& wc) {
+                          WaveCtx& w, WorkCount& wc, uint32_t tile) {
   col terms[kMaxDepth];
   int depth = 0;
   bool alive = valid;
@@ -1280,6 +1329,7 @@ __device__ __forceinline__ col trace_path(const KParams& p, bool valid, f3 o, f3
     b.pt = o;
 #endif
     closest_q<ACCEL, COUNT>(p, r, alive, depth, b, s, w, wc);
+    if (ACCEL != RT_ACCEL_FLAT_D && depth == 0) cand_closest<COUNT>(p, r, alive, tile, b, wc);
     bool hit = alive && b.dist != __builtin_inff();
     f3 N = f3{0.0f, 0.0f, 0.0f};
     wc.hits += (uint32_t)__popcll(__ballot(hit));
@@ -1382,7 +1432,7 @@ __global__ __launch_bounds__(64, MINW) void render_kernel(KParams p) {
         float l = (float)j + 0.5f * (float)sl;
         f3 point = add(add(p.C, scale(p.u, k)), scale(p.v, l));
         f3 dir = normalize(sub(p.pos, point));
-        col sc = trace_path<ACCEL, COUNT>(p, valid, point, dir, 1.0f, stk, w, wc);
+        col sc = trace_path<ACCEL, COUNT>(p, valid, point, dir, 1.0f, stk, w, wc, t);
         acc = color_add(acc, color_mul(sc, 0.25f));
       }
     }

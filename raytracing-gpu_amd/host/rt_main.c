@@ -42,6 +42,11 @@ int main(int argc, char *argv[])
   rt_stats st;
   double ms = 0;
   int rc = rt_raytrace_multi(argv[1], argv[2], gpus, accel, &st, &ms);
+  /* input/output and parse errors print the reference's own text and
+   * newline (cpu/parser.c:70-71,110-111, cpu/parse_obj.c:80-81,
+   * cpu/printer.c:6-7: errx(1, "%s\n", ...)); device errors name the code */
+  if (rc == RT_EIO || rc == RT_EPARSE)
+    errx(1, "%s\n", rt_last_error());
   if (rc)
     errx(1, "%s: %s", rt_strerror(rc), rt_last_error());
   if (want_stats)

@@ -29,8 +29,8 @@ int rt_lex_open(const char *path, rt_lex *lx)
 {
   memset(lx, 0, sizeof *lx);
   FILE *f = fopen(path, "rb");
-  if (!f)
-    return rt_set_error(RT_EIO, "%s: %s", path, strerror(errno));
+  if (!f) /* the reference's text: errx(1, "%s\n", strerror(errno)) (cpu/parser.c:70-71) */
+    return rt_set_error(RT_EIO, "%s", strerror(errno));
   if (fseek(f, 0, SEEK_END) != 0)
   {
     fclose(f);
@@ -169,12 +169,19 @@ static int parse_object(rt_lex *lx, rt_prescan *ps, rt_object *obj, vecbuf *vs, 
       if (!rc)
         rc = vb_push(n == 2 ? ns : vs, x);
     }
-    else
+    else /* cpu/parse_obj.c:80-81 (object level: "parsing", not "the parsing") */
       rc = rt_set_error(RT_EPARSE, "Error during parsing %.*s", (int)n, t);
   }
   if (rc)
     return rc;
   size_t nv = vs->n;
+  /* Deliberately stricter than the reference, which has no defined result
+   * here: it pops 3 v + 3 vn per triangle until the v stack is empty
+   * (cpu/parse_obj.c:83-88; a NULL head is dereferenced when v is not a
+   * multiple of 3 or vn runs out first, cpu/stack.c:36-39) and then sets
+   * triangle_count = declared / 3 (cpu/parse_obj.c:89) whatever it popped,
+   * so fewer v lines than declared leave triangles it never allocated.  Such
+   * files are rejected (tests/test_host.py). */
   if (nv % 3 != 0 || ns->n < nv || nv != declared)
     return rt_set_error(RT_EPARSE, "%s: object declares %u vertices, has %zu v / %zu vn",
                         lx->path, declared, nv, ns->n);

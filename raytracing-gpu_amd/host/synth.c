@@ -34,24 +34,32 @@ static rt_vec3 mk(double x, double y, double z)
   return v;
 }
 
-/* triangles of a stacks x slices UV sphere: 2*slices*(stacks-1) */
+/* triangles of a stacks x slices UV sphere: 2*slices*(stacks-1).
+ * slices / stacks is kept in [1.5, 2.2] so the quads stay near square at the
+ * equator (a slice spans 2 pi / slices, a stack pi / stacks); among those
+ * shapes the triangle count nearest the target wins, ties towards 1.8.
+ * (Round 1 only bounded the ratio from above and picked 258 x 19, i.e.
+ * 27:1 sliver triangles -- DESIGN.md §2; rt_scene_synthetic_uv still builds
+ * that tessellation on request.) */
 static void sphere_shape(unsigned target, unsigned *stacks, unsigned *slices)
 {
-  unsigned best_st = 3, best_sl = 4;
+  unsigned best_st = 3, best_sl = 5;
   unsigned long best_err = ~0ul;
+  double best_dev = 1e30;
   for (unsigned st = 3; st < 4096; st++)
   {
-    /* slices ~ 1.8 * stacks keeps the quads near square */
     unsigned sl = (unsigned)((double)target / (2.0 * (st - 1)) + 0.5);
     if (sl < 4)
       break;
-    if (sl > 2 * st + 8)
-      continue;
+    if (10 * sl > 22 * st || 2 * sl < 3 * st)
+      continue; /* slices / stacks outside [1.5, 2.2] */
     unsigned long n = 2ul * sl * (st - 1);
     unsigned long err = n > target ? n - target : target - n;
-    if (err < best_err || (err == best_err && sl * 10 < st * 18))
+    double dev = fabs((double)sl / st - 1.8);
+    if (err < best_err || (err == best_err && dev < best_dev))
     {
       best_err = err;
+      best_dev = dev;
       best_st = st;
       best_sl = sl;
     }
@@ -98,10 +106,18 @@ static void emit_sphere(rt_triangle *out, unsigned stacks, unsigned slices, doub
 int rt_scene_synthetic(unsigned gx, unsigned gy, unsigned tris_per_sphere, unsigned long long seed,
                        int width, int height, rt_scene **out)
 {
-  if (!out || gx == 0 || gy == 0 || tris_per_sphere < 8 || width <= 0 || height <= 0)
+  if (tris_per_sphere < 8)
     return rt_set_error(RT_EINVAL, "rt_scene_synthetic: bad argument");
   unsigned stacks, slices;
   sphere_shape(tris_per_sphere, &stacks, &slices);
+  return rt_scene_synthetic_uv(gx, gy, stacks, slices, seed, width, height, out);
+}
+
+int rt_scene_synthetic_uv(unsigned gx, unsigned gy, unsigned stacks, unsigned slices,
+                          unsigned long long seed, int width, int height, rt_scene **out)
+{
+  if (!out || gx == 0 || gy == 0 || stacks < 3 || slices < 3 || width <= 0 || height <= 0)
+    return rt_set_error(RT_EINVAL, "rt_scene_synthetic: bad argument");
   unsigned per = 2 * slices * (stacks - 1);
   rt_scene *s = calloc(1, sizeof *s);
   if (!s)

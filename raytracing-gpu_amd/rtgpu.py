@@ -85,7 +85,9 @@ class Stats(C.Structure):
     _fields_ = [("closest", C.c_ulonglong), ("shadow", C.c_ulonglong), ("camera", C.c_ulonglong),
                 ("node_visits", C.c_ulonglong), ("tri_tests", C.c_ulonglong),
                 ("depth_overflow", C.c_ulonglong), ("zero_normal", C.c_ulonglong),
-                ("pixels", C.c_ulonglong), ("hits", C.c_ulonglong)]
+                ("pixels", C.c_ulonglong), ("hits", C.c_ulonglong),
+                ("cand_prims", C.c_ulonglong), ("cand_entries", C.c_ulonglong),
+                ("cand_global", C.c_ulonglong)]
 
     def as_dict(self):
         return {k: int(getattr(self, k)) for k, _ in self._fields_}
@@ -113,6 +115,8 @@ _PROTOS = [
     ("rt_scene_write_obj", C.c_int, [C.POINTER(SceneStruct), C.c_char_p]),
     ("rt_scene_synthetic", C.c_int, [C.c_uint, C.c_uint, C.c_uint, C.c_ulonglong, C.c_int,
                                      C.c_int, C.POINTER(C.POINTER(SceneStruct))]),
+    ("rt_scene_synthetic_uv", C.c_int, [C.c_uint, C.c_uint, C.c_uint, C.c_uint, C.c_ulonglong,
+                                        C.c_int, C.c_int, C.POINTER(C.POINTER(SceneStruct))]),
     ("rt_scene_triangle_count", C.c_size_t, [C.POINTER(SceneStruct)]),
     ("rt_scene_free", None, [C.POINTER(SceneStruct)]),
     ("rt_ppm_write", C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_void_p]),
@@ -133,6 +137,10 @@ _PROTOS = [
     ("rt_hip_stats", C.c_int, [C.c_void_p, C.POINTER(Stats)]),
     ("rt_hip_set_count_work", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_set_cull_slack", C.c_int, [C.c_void_p, C.c_float]),
+    ("rt_hip_set_exact_camera", C.c_int, [C.c_void_p, C.c_int]),
+    ("rt_hip_set_camera_bound_scale", C.c_int, [C.c_void_p, C.c_double]),
+    ("rt_cand_survey", C.c_int, [C.POINTER(SceneStruct), C.c_float, C.c_double, C.c_int, C.c_int,
+                                 C.POINTER(C.c_ulonglong)]),
     ("rt_hip_assemble", C.c_int, [C.c_void_p, C.POINTER(Frame), C.c_void_p, C.c_int, C.c_void_p,
                                   C.c_void_p]),
     ("rt_hip_render_image", C.c_int, [C.c_void_p, C.POINTER(Frame), C.c_void_p,
@@ -199,6 +207,14 @@ class Scene:
         p = C.POINTER(SceneStruct)()
         _check(lib().rt_scene_synthetic(gx, gy, tris_per_sphere, seed, width, height, C.byref(p)),
                "synthetic scene")
+        return cls(p)
+
+    @classmethod
+    def synthetic_uv(cls, gx, gy, stacks, slices, seed=0x5EED, width=3840, height=2160):
+        """Explicit tessellation (round 1's C5 was 258 stacks x 19 slices)."""
+        p = C.POINTER(SceneStruct)()
+        _check(lib().rt_scene_synthetic_uv(gx, gy, stacks, slices, seed, width, height,
+                                           C.byref(p)), "synthetic scene")
         return cls(p)
 
     @property
@@ -300,6 +316,17 @@ def accel_probe(scene, accel="octree", stride=97, check=True):
     return r.as_dict()
 
 
+def cand_survey(scene, eps_ulps=64.0, bound_scale=1.0, threads=8, leaves=False):
+    """Host-only: {safe, footprint, global, entries} of the camera candidate
+    lists of the scene's frame (csrc/rt_cand.hip classify + raster)."""
+    out = (C.c_ulonglong * 36)()
+    _check(lib().rt_cand_survey(scene.ptr, eps_ulps, bound_scale, threads, 1 if leaves else 0, out),
+           "cand_survey")
+    r = dict(zip(("safe", "footprint", "global", "entries"), (int(x) for x in out[:4])))
+    r["hist"] = [(1 << k, int(out[4 + k]), int(out[20 + k])) for k in range(16) if out[4 + k]]
+    return r
+
+
 def device_count():
     n = C.c_int(0)
     rc = lib().rt_hip_device_count(C.byref(n))
@@ -335,6 +362,12 @@ class Context:
 
     def set_count_work(self, on=True):
         _check(lib().rt_hip_set_count_work(self.h, 1 if on else 0), "count_work")
+
+    def set_exact_camera(self, on=True):
+        _check(lib().rt_hip_set_exact_camera(self.h, 1 if on else 0), "exact_camera")
+
+    def set_camera_bound_scale(self, scale):
+        _check(lib().rt_hip_set_camera_bound_scale(self.h, float(scale)), "bound_scale")
 
     def set_cull_slack(self, ulps):
         _check(lib().rt_hip_set_cull_slack(self.h, float(ulps)), "cull_slack")

@@ -24,11 +24,12 @@ def pytest_configure(config):
 
 @pytest.fixture(scope="session")
 def built():
-    """Build the product library and the oracle once per session."""
+    """Bring the product library and the oracle up to date once per session
+    (incremental make: a no-op when the in-tree build matches the sources)."""
     import oracle as orc
     import rtgpu
-    if not os.path.exists(rtgpu.LIB_PATH):
-        rtgpu.build()
+    rtgpu.build()
+    orc.build()
     orc.lib()
     return True
 
