@@ -138,6 +138,12 @@ int rt_hip_set_count_work(rt_hip_ctx *ctx, int enable);
  * (csrc/rt_cand.hip).  0 = octree walk only (A/B timing; cpu/rt parity is
  * then not guaranteed for grazing camera rays). */
 int rt_hip_set_exact_camera(rt_hip_ctx *ctx, int enable);
+/* Octree traversal policy (default 0): 0 = staged packet walk for coherent
+ * closest-hit queries, per-lane walks otherwise; 1 = every query per lane;
+ * 2 = every query as a staged packet; 3 = 0 plus staged packet walks for
+ * directional-light shadow rays.  All are exact; 1-3 exist for tests and A/B
+ * measurements (each is its own kernel, so the default has no switch). */
+int rt_hip_set_policy(rt_hip_ctx *ctx, int policy);
 /* Scale of the error-bound constants the candidate lists use (1 = the
  * proven bound of tools/mt_bound.py; smaller = a calibrated model, faster,
  * exactness then verified rather than proven). */

@@ -54,7 +54,8 @@ struct rt_hip_ctx {
   rt_accel_info info{};
   float scene_c[3]{}, scene_r = 0;
   float eps_ulps = RT_EPS_ULPS_DEFAULT;
-  int min_waves = 0;  // launch-bounds variant (tuning: env RT_MIN_WAVES)
+  int policy = RT_POLICY_DEFAULT;  // traversal policy (tests / A/B only: rt_hip_set_policy)
+  float* d_terms = nullptr;        // deep reflection terms (KParams::terms)
   // exact camera rays (csrc/rt_cand.hip)
   int exact_camera = 1;
   double bound_scale = 1.0;  // 1 = the proven float-MT error bound (tools/mt_bound.py)
@@ -126,6 +127,7 @@ extern "C" void rt_hip_destroy(rt_hip_ctx* c) {
   (void)hipFree(c->d_counter);
   (void)hipFree(c->d_stats);
   (void)hipFree(c->d_spill);
+  (void)hipFree(c->d_terms);
   if (c->d_tri_prim != c->d_tri) (void)hipFree(c->d_tri_prim);
   (void)hipFree(c->d_cand_visits);
   (void)hipFree(c->d_cand_off);
@@ -255,6 +257,11 @@ extern "C" int rt_hip_create(int device, const rt_scene* scene, int accel, rt_hi
     rt_hip_destroy(c);
     return rt_set_error(RT_EHIP, "hipMalloc traversal spill stack");
   }
+  if (hipMalloc((void**)&c->d_terms, (size_t)c->grid * 64 * 3 * (RT_MAX_DEPTH - RT_LDS_TERMS) *
+                                         sizeof(float)) != hipSuccess) {
+    rt_hip_destroy(c);
+    return rt_set_error(RT_EHIP, "hipMalloc reflection terms");
+  }
   *out = c;
   return RT_OK;
 }
@@ -298,6 +305,14 @@ extern "C" int rt_hip_set_cull_slack(rt_hip_ctx* c, float ulps) {
 extern "C" int rt_hip_set_exact_camera(rt_hip_ctx* c, int enable) {
   if (!c) return rt_set_error(RT_EINVAL, "null context");
   c->exact_camera = enable ? 1 : 0;
+  return RT_OK;
+}
+
+extern "C" int rt_hip_set_policy(rt_hip_ctx* c, int policy) {
+  if (!c) return rt_set_error(RT_EINVAL, "null context");
+  if (policy < RT_POLICY_DEFAULT || policy > RT_POLICY_DIR_STAGED)
+    return rt_set_error(RT_EINVAL, "unknown traversal policy %d", policy);
+  c->policy = policy;
   return RT_OK;
 }
 
@@ -606,22 +621,7 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
   // culling slack: eps_ulps ulps of the origin-to-geometry distance
   // (DESIGN.md "Conservative culling")
   p.eps_rel = c->eps_ulps * 5.9604645e-8f;
-  // launch-bounds variant: a tuning knob read per render (tools/sweep.py)
-  const char* mw = std::getenv("RT_MIN_WAVES");
-  c->min_waves = mw ? std::atoi(mw) : 0;
-  // traversal policy (tuning knobs, tools/sweep.py): 0 lane, 1 packet, 2 hybrid
-  const char* tv = std::getenv("RT_TRAV");
-  p.trav = tv ? std::atoi(tv) : 4;
-  const char* pm = std::getenv("RT_PACKET_MIN");
-  p.packet_min = pm ? std::atoi(pm) : 8;
-  const char* tvs = std::getenv("RT_TRAV_SHADOW");
-  p.trav_shadow = tvs ? std::atoi(tvs) : 0;  // measured: per-lane any-hit walks win
-  const char* pms = std::getenv("RT_PACKET_MIN_SHADOW");
-  p.packet_min_shadow = pms ? std::atoi(pms) : p.packet_min;
-  const char* pmd = std::getenv("RT_PACKET_DEPTH");
-  // measured (C5): packet walks for camera rays and first reflections only;
-  // deeper reflections are incoherent and walk per lane (18.9 -> 17.9 ms)
-  p.packet_max_depth = pmd ? std::atoi(pmd) : 1;
+  p.terms = c->d_terms;
   c->cand_prims = c->cand_entries = c->cand_global = 0;
   if (c->accel == RT_ACCEL_OCTREE && c->d_node && c->exact_camera) {
     int rc = cand_prepare(c, f, &p, s);
@@ -631,11 +631,11 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
     // empty scene: nothing to traverse, the FLAT kernel with 0 records is exact
     HIP_TRY(hipMemsetAsync(c->d_counter, 0, 64, s));
     HIP_TRY(hipMemsetAsync(c->d_stats, 0, RT_NSTATS * sizeof(unsigned long long), s));
-    HIP_TRY(rt_launch_render(&p, RT_ACCEL_FLAT_D, c->count_work, c->min_waves, c->grid, s));
+    HIP_TRY(rt_launch_render(&p, RT_ACCEL_FLAT_D, c->count_work, c->policy, c->grid, s));
   } else {
     HIP_TRY(hipMemsetAsync(c->d_counter, 0, 64, s));
     HIP_TRY(hipMemsetAsync(c->d_stats, 0, RT_NSTATS * sizeof(unsigned long long), s));
-    HIP_TRY(rt_launch_render(&p, c->accel, c->count_work, c->min_waves, c->grid, s));
+    HIP_TRY(rt_launch_render(&p, c->accel, c->count_work, c->policy, c->grid, s));
   }
   c->last_stream = s;
   return RT_OK;

@@ -15,13 +15,16 @@
 #define RT_NSTATS 8
 // per-lane global overflow area of the traversal stack (entries beyond LDS)
 #define RT_SPILL_STACK 112
-// tile bands and their counters in KParams::tile_counter (<= 16).  Measured
-// (C5): 8 bands, one per XCD, ran 13 % slower than 1 -- one scanline-ordered
-// band keeps all 8 XCDs on the same few tile rows, whose geometry then stays
-// in the Infinity Cache; 8 stripes at once multiply that working set.
-#ifndef RT_BANDS
-#define RT_BANDS 1
-#endif
+// reflection terms of a path kept in LDS (deeper ones: KParams::terms)
+#define RT_LDS_TERMS 4
+// occupancy target of the render kernels' launch bounds (waves per SIMD)
+#define RT_MIN_WAVES 4
+// traversal policies (one kernel instantiation each, rt_render.hip); the
+// others exist for tests and A/B measurements
+#define RT_POLICY_DEFAULT 0     // staged packet closest hit for coherent queries, per-lane shadows
+#define RT_POLICY_LANE 1        // every octree query per lane
+#define RT_POLICY_STAGED 2      // every octree query as a staged packet
+#define RT_POLICY_DIR_STAGED 3  // default + staged packet directional-light shadows
 
 // wave-total counters (wave-uniform, so they live in SGPRs; 32-bit per wave,
 // widened to 64-bit by the final atomics)
@@ -40,17 +43,14 @@ struct KParams {
   int W, H;
   int tiles_x, ntiles_total, rank, nranks, ntiles_local;
   float* out;                   // rank's tile buffer
-  uint32_t* tile_counter;       // zeroed before launch
+  uint32_t* tile_counter;       // zeroed before launch (one counter)
   unsigned long long* stats;    // RT_NSTATS counters, zeroed before launch
   uint2* spill;                 // grid*64 lanes x RT_SPILL_STACK stack entries
   rt::f3 scene_c;               // scene box centre
   float scene_cmag;             // max-norm of scene_c
   float scene_r;                // scene box half-extent (max-norm)
   float eps_rel;                // culling slack, rt_cull.h rt_cull_eps()
-  int trav;                     // RT_TRAV_LANE / _PACKET / _HYBRID (rt_render.hip)
-  int packet_min;               // hybrid: packet walk while >= this many lanes query
-  int trav_shadow, packet_min_shadow;  // the same two for shadow (any-hit) queries
-  int packet_max_depth;         // closest hit: packet walk only up to this bounce depth
+  float* terms;                 // (RT_MAX_DEPTH - RT_LDS_TERMS) x grid*64 lanes x 3: deep reflection terms
   // camera-ray candidate lists (csrc/rt_cand.hip); cand_start == NULL: none
   const uint32_t* cand_start;   // ntiles_local + 1 offsets into cand
   const uint32_t* cand;         // prims
@@ -60,9 +60,8 @@ struct KParams {
   const float* cand_skip;       // per prim: lower bound of new_dist - |pos - o| (depth skip)
 };
 
-// min_waves = occupancy target per SIMD (launch bounds of the instantiation:
-// 2..5); 0 = default
-extern "C" hipError_t rt_launch_render(const KParams* p, int accel, int count_work, int min_waves,
+// policy = RT_POLICY_* (octree only)
+extern "C" hipError_t rt_launch_render(const KParams* p, int accel, int count_work, int policy,
                                        int grid, hipStream_t stream);
 extern "C" hipError_t rt_launch_assemble(const float* tiles, float* rgb, int W, int H, int tiles_x,
                                          int ntiles, int nranks, int tiles_per_rank,

@@ -14,9 +14,11 @@
 //   * reflection terms are buffered and summed deepest-first.
 //
 // Acceleration: FLAT tests every triangle record (the reference's brute
-// force, cpu/hit.c:72-109) with wave-uniform scalar loads of each record;
-// OCTREE walks the octree built by host/accel.c with a per-lane stack,
-// front-to-back child order and conservative distance culling.
+// force, cpu/hit.c:72-109) streamed through LDS; OCTREE walks the octree
+// (host/accel.c or csrc/rt_build.hip) front to back with conservative
+// distance culling, as a wave-wide staged packet (coherent queries) or one
+// stack per lane (incoherent ones), then tests the camera-ray candidate
+// lists of csrc/rt_cand.hip.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -27,6 +29,11 @@
 namespace rt {
 
 static constexpr float kEps = 0.0000001f;  // cpu/hit.c:7 (float)1e-7
+
+// The workgroup is one wave and a wave's LDS instructions execute in issue
+// order, so LDS staging needs no s_barrier: only a compiler barrier that
+// keeps the LDS reads and writes in source order.
+__device__ __forceinline__ void wave_sync() { __asm__ volatile("" ::: "memory"); }
 static constexpr int kMaxDepth = RT_MAX_DEPTH;
 
 __device__ __forceinline__ f3 ld3(const float* p) { return f3{p[0], p[1], p[2]}; }
@@ -50,7 +57,6 @@ __device__ __forceinline__ bool mt_test(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float& 
 
 struct Ray {
   f3 o, d;     // origin, direction (as the reference holds them)
-  f3 nd;       // normalize(d)
   float dlen;  // length(d)
   float eps;   // culling slack (world units) for this origin
   f3 oh, ol;   // o + eps, o - eps: the grown slab planes' offsets (rt_cull.h)
@@ -61,7 +67,6 @@ __device__ __forceinline__ Ray make_ray(const KParams& p, f3 o, f3 d) {
   r.o = o;
   r.d = d;
   r.dlen = length(d);
-  r.nd = f3{d.x / r.dlen, d.y / r.dlen, d.z / r.dlen};
   r.eps = rt_cull_eps(p.eps_rel, o.x - p.scene_c.x, o.y - p.scene_c.y, o.z - p.scene_c.z,
                       p.scene_cmag, p.scene_r);
   r.oh = f3{o.x + r.eps, o.y + r.eps, o.z + r.eps};
@@ -69,10 +74,17 @@ __device__ __forceinline__ Ray make_ray(const KParams& p, f3 o, f3 d) {
   return r;
 }
 
-// new_dist = |(o + nd * (t*|d|)) - o| (cpu/hit.c:35-37,58); returns the hit point too.
-__device__ __forceinline__ float hit_dist(const Ray& r, float t, f3& out) {
-  out = add(r.o, scale(r.nd, t * r.dlen));
-  return length(sub(out, r.o));
+// The hit point o + normalize(d) * (t*|d|) (cpu/hit.c:35-37,58), with
+// normalize(d) recomputed here (the same IEEE divisions every time, so the
+// same bits) rather than kept live through the walks.
+__device__ __forceinline__ f3 hit_point(const Ray& r, float t) {
+  f3 nd{r.d.x / r.dlen, r.d.y / r.dlen, r.d.z / r.dlen};
+  return add(r.o, scale(nd, t * r.dlen));
+}
+
+// new_dist = |hit point - o| (cpu/hit.c:58)
+__device__ __forceinline__ float hit_dist(const Ray& r, float t) {
+  return length(sub(hit_point(r, t), r.o));
 }
 
 // Conservative pre-filter of the Moller-Trumbore test.  h, a, s.h, d.q, e2.q
@@ -83,9 +95,6 @@ __device__ __forceinline__ float hit_dist(const Ray& r, float t, f3& out) {
 // t_cut (closest hit: it cannot beat the current winner, ties included);
 // survivors are re-tested exactly.  DESIGN.md "Exact MT with a cheap reject".
 __device__ __forceinline__ bool mt_candidate(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float t_cut) {
-#ifdef RT_EXACT_ONLY
-  return true;
-#else
   // same staging as cpu/hit.c:15-33, so a wave whose lanes all fail u skips
   // the v and t work (coherent packets mostly agree)
   const float m = 1e-5f;  // >> the few-ulp gap between (u,v,t) and the reference's
@@ -101,23 +110,14 @@ __device__ __forceinline__ bool mt_candidate(f3 o, f3 d, f3 v0, f3 e1, f3 e2, fl
   if (v < -1e-30f || u + v > 1.0f + m) return false;
   float t = dot(e2, q) * r;
   return !(t < kEps * (1.0f - m) || t > t_cut);
-#endif
 }
-
-#ifndef RT_BEST_T
-#define RT_BEST_T 0  // measured: C5 15.40/15.53 (on) vs 15.63/15.36 ms (off), C3 no better
-#endif
 
 struct Best {
   float dist;  // +inf = none
   float t_cut; // parametric bound beyond which no triangle can win (+inf = none)
   uint32_t prim, obj;
   float u, v;
-#if RT_BEST_T
-  float t;  // MT t of the winner; the hit point is recomputed from it (hit_pt)
-#else
-  f3 pt;
-#endif
+  float t;  // the winner's MT t; its hit point is hit_point(r, t)
 };
 
 __device__ __forceinline__ void consider(const Ray& r, const float4& q0, const float4& q1,
@@ -126,8 +126,7 @@ __device__ __forceinline__ void consider(const Ray& r, const float4& q0, const f
   if (!mt_candidate(r.o, r.d, v0, e1, e2, b.t_cut)) return;
   float t, u, v;
   if (!mt_test(r.o, r.d, v0, e1, e2, t, u, v)) return;
-  f3 out;
-  float nd = hit_dist(r, t, out);
+  float nd = hit_dist(r, t);
   if (!((double)nd > 0.01)) return;
   uint32_t prim = __float_as_uint(q2.y);
   if (nd < b.dist || (nd == b.dist && prim < b.prim)) {
@@ -140,20 +139,9 @@ __device__ __forceinline__ void consider(const Ray& r, const float4& q0, const f
     b.obj = __float_as_uint(q2.z);
     b.u = u;
     b.v = v;
-#if RT_BEST_T
     b.t = t;
-#else
-    b.pt = out;
-#endif
   }
 }
-
-#ifndef RT_ANY_DLEN_RECOMPUTE
-#define RT_ANY_DLEN_RECOMPUTE 1  // measured: C5 15.43/15.39 (on) vs 15.66/15.39 ms (off)
-#endif
-#ifndef RT_ANY_ND_RECOMPUTE
-#define RT_ANY_ND_RECOMPUTE 1  // measured: C5 15.37/15.39 (on) vs 15.53/15.50 ms (off)
-#endif
 
 __device__ __forceinline__ bool any_hit_rec(const Ray& r, const float4& q0, const float4& q1,
                                             const float4& q2) {
@@ -161,31 +149,14 @@ __device__ __forceinline__ bool any_hit_rec(const Ray& r, const float4& q0, cons
   if (!mt_candidate(r.o, r.d, v0, e1, e2, __builtin_inff())) return false;
   float t, u, v;
   if (!mt_test(r.o, r.d, v0, e1, e2, t, u, v)) return false;
-#if RT_ANY_ND_RECOMPUTE
-  // normalize(d) recomputed here (same IEEE divisions as make_ray, same
-  // bits) instead of keeping it live through the whole any-hit walk
-#if RT_ANY_DLEN_RECOMPUTE
-  float dlen = length(r.d);  // = make_ray's r.dlen, same operations
-#else
-  float dlen = r.dlen;
-#endif
-  f3 nd{r.d.x / dlen, r.d.y / dlen, r.d.z / dlen};
-  f3 out = add(r.o, scale(nd, t * dlen));
-  return (double)length(sub(out, r.o)) > 0.01;
-#else
-  f3 out;
-  return (double)hit_dist(r, t, out) > 0.01;
-#endif
+  return (double)hit_dist(r, t) > 0.01;
 }
 
 // -------------------------------------------------------------- OCTREE
 // Per-lane traversal stack: the first kLdsStack entries live in LDS, laid
 // out [entry][lane] so every lane hits its own bank; deeper entries spill to
 // a per-lane area in global memory (rare: typical depth is < 16).
-#ifndef RT_LDS_STACK
-#define RT_LDS_STACK 6
-#endif
-static constexpr int kLdsStack = RT_LDS_STACK;
+static constexpr int kLdsStack = 6;
 static constexpr int kSpillStack = RT_SPILL_STACK;
 
 struct Stack {
@@ -194,9 +165,6 @@ struct Stack {
   uint2* spill;   // this lane's kSpillStack entries
   int lane;
   int sp;
-  uint32_t occ;   // record index of this lane's last shadow occluder (~0u: none)
-  uint32_t occ2;  // the same for the other light parity (RT_OCC_SLOTS 2)
-  uint32_t slot;  // light parity of the current shadow query (wave-uniform)
 };
 
 // Counters of one lane's own walk (divergent code); folded into the wave's
@@ -283,9 +251,6 @@ __device__ __forceinline__ uint32_t near_octant(f3 d) {
   return (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
 }
 
-#ifndef RT_CHILD_PIPE
-#define RT_CHILD_PIPE 1
-#endif
 
 // child-mask bit o moved to bit o ^ dm (the visiting order's index space)
 __device__ __forceinline__ uint32_t mask_xor(uint32_t m, uint32_t dm) {
@@ -296,16 +261,17 @@ __device__ __forceinline__ uint32_t mask_xor(uint32_t m, uint32_t dm) {
 }
 
 // Interior node: test the children's boxes and push the hits far-to-near in
-// octant order (a valid front-to-back order for the disjoint octant cells),
-// so the nearest child is popped first.  CLOSEST also prunes by best.
+// octant order (j = 7..0, octant j ^ dm: a valid front-to-back order for the
+// disjoint octant cells), so the nearest child is popped first.  Software-
+// pipelined: child k+1's box is in flight while child k is tested.
+// CLOSEST pushes (node, entry t) and prunes by best; any-hit pushes the
+// child's own (first, info) words from its box record, so a pop needs no
+// node fetch -- one dependent load per step instead of two.
 template <bool CLOSEST, bool COUNT>
 __device__ __forceinline__ void push_children(const float4* __restrict__ node, const Ray& r, f3 inv,
                                               uint32_t dm, uint32_t first, uint32_t info,
                                               float best, Stack& s, LaneCount& wc) {
   uint32_t mask = RT_NODE_MASK(info);
-#if RT_CHILD_PIPE
-  // same order, software-pipelined: child k+1's box is in flight while
-  // child k is tested
   uint32_t mj = mask_xor(mask, dm);
   if (!mj) return;
   int j = 31 - __clz(mj);
@@ -326,38 +292,48 @@ __device__ __forceinline__ void push_children(const float4* __restrict__ node, c
       if (COUNT) wc.nodes += lanes_distinct(ci);
     }
     float t0 = box_enter(r, inv, clo, chi);
-    if (t0 != __builtin_inff() &&
-        !(CLOSEST && best != __builtin_inff() && rt_prune(t0, r.dlen, best, r.eps)))
-      push(s, cc, t0, wc);
-    if (!more) break;
-  }
-  return;
-#endif
-#pragma unroll 1
-  for (int j = 7; j >= 0; --j) {
-    uint32_t o = (uint32_t)j ^ dm;
-    if (mask & (1u << o)) {
-      uint32_t ci = first + (uint32_t)__popc(mask & ((1u << o) - 1u));
-      if (COUNT) wc.nodes += lanes_distinct(ci);
-      float t0 = box_enter(r, inv, node[2 * ci], node[2 * ci + 1]);
-      if (t0 == __builtin_inff()) continue;
-      if (CLOSEST && best != __builtin_inff() && rt_prune(t0, r.dlen, best, r.eps)) continue;
-      push(s, ci, t0, wc);
+    if (CLOSEST) {
+      if (t0 != __builtin_inff() && !(best != __builtin_inff() && rt_prune(t0, r.dlen, best, r.eps)))
+        push(s, cc, t0, wc);
+    } else if (t0 != __builtin_inff()) {
+      push(s, __float_as_uint(clo.w), chi.w, wc);
     }
+    if (!more) break;
   }
 }
 
-#ifndef RT_LEAF_PIPE
-#define RT_LEAF_PIPE 1
-#endif
+// A leaf's records, software-pipelined: record k+1 is in flight while record
+// k is tested.  ANY: returns true at the first any-hit.
+template <bool ANY, bool COUNT>
+__device__ __forceinline__ bool leaf_lane(const float4* __restrict__ tri, uint32_t first,
+                                          uint32_t cnt, const Ray& r, Best& b, LaneCount& wc) {
+  const float4* q = tri + 3 * (size_t)first;
+  float4 n0 = q[0], n1 = q[1], n2 = q[2];
+  for (uint32_t k = 0; k < cnt; k++) {
+    float4 q0 = n0, q1 = n1, q2 = n2;
+    if (k + 1 < cnt) {
+      n0 = q[3 * (k + 1)];
+      n1 = q[3 * (k + 1) + 1];
+      n2 = q[3 * (k + 1) + 2];
+    }
+    if (COUNT) wc.tris += lanes_distinct(first + k);
+    if (ANY) {
+      if (any_hit_rec(r, q0, q1, q2)) return true;
+    } else {
+      consider(r, q0, q1, q2, b);
+    }
+  }
+  return false;
+}
 
+// Per-lane closest-hit walk (each lane its own stack).
 template <bool COUNT>
 __device__ void oct_closest(const KParams& p, const Ray& r, Best& b, Stack& s, LaneCount& wc) {
   const float4* __restrict__ node = p.node;
-  const float4* __restrict__ tri = p.tri;
   f3 inv = inv_dir(r.d);
   uint32_t dm = near_octant(r.d);
   s.sp = 0;
+  wave_sync();
   {
     float t0 = box_enter(r, inv, node[0], node[1]);
     if (t0 != __builtin_inff()) push(s, 0, t0, wc);
@@ -370,336 +346,48 @@ __device__ void oct_closest(const KParams& p, const Ray& r, Best& b, Stack& s, L
     float4 lo = node[2 * ni], hi = node[2 * ni + 1];
     uint32_t first = __float_as_uint(lo.w), info = __float_as_uint(hi.w);
     if (COUNT) wc.nodes += lanes_distinct(ni);
-    if (info & RT_NODE_LEAF) {
-      uint32_t cnt = RT_LEAF_COUNT(info);
-#if RT_LEAF_PIPE
-      // software-pipelined: record k+1 is in flight while record k is tested
-      const float4* q = tri + 3 * (size_t)first;
-      float4 n0 = q[0], n1 = q[1], n2 = q[2];
-      for (uint32_t k = 0; k < cnt; k++) {
-        float4 q0 = n0, q1 = n1, q2 = n2;
-        if (k + 1 < cnt) {
-          n0 = q[3 * (k + 1)];
-          n1 = q[3 * (k + 1) + 1];
-          n2 = q[3 * (k + 1) + 2];
-        }
-        if (COUNT) wc.tris += lanes_distinct(first + k);
-        consider(r, q0, q1, q2, b);
-      }
-#else
-      for (uint32_t k = 0; k < cnt; k++) {
-        const float4* q = tri + 3 * (size_t)(first + k);
-        if (COUNT) wc.tris += lanes_distinct(first + k);
-        consider(r, q[0], q[1], q[2], b);
-      }
-#endif
-    } else {
+    if (info & RT_NODE_LEAF)
+      leaf_lane<false, COUNT>(p.tri, first, RT_LEAF_COUNT(info), r, b, wc);
+    else
       push_children<true, COUNT>(node, r, inv, dm, first, info, b.dist, s, wc);
-    }
   }
+  wave_sync();
 }
 
-// Any-hit walk: a stack entry holds the node's own (first, info) words,
-// taken from the child box record its parent already fetched, so a pop needs
-// no node fetch -- one dependent load per step (the children's boxes or the
-// leaf's triangles) instead of two.
-#ifndef RT_PREFETCH
-#define RT_PREFETCH 0  // measured: C5 16.8 (on) vs 15.5-15.7 ms (off); VGPR spills 40 -> 50
-#endif
-
-// first child (in visiting order) of an interior node, for the prefetch
-__device__ __forceinline__ uint32_t first_child(uint32_t first, uint32_t info, uint32_t dm) {
-  uint32_t mask = RT_NODE_MASK(info);
-  uint32_t mj = mask_xor(mask, dm);
-  int j = 31 - __clz(mj | 1u);
-  return first + (uint32_t)__popc(mask & ((1u << ((uint32_t)j ^ dm)) - 1u));
-}
-
-// push_children_any with the first child's box already loaded (plo, phi);
-// returns true when it pushed, with the last pushed entry (the new stack
-// top) in (tf, ti).
-template <bool COUNT>
-__device__ __forceinline__ bool push_children_any_pf(const float4* __restrict__ node, const Ray& r,
-                                                     f3 inv, uint32_t dm, uint32_t first,
-                                                     uint32_t info, float4 plo, float4 phi,
-                                                     Stack& s, LaneCount& wc, uint32_t& tf,
-                                                     uint32_t& ti) {
-  uint32_t mask = RT_NODE_MASK(info);
-  uint32_t mj = mask_xor(mask, dm);
-  if (!mj) return false;
-  int j = 31 - __clz(mj);
-  mj &= ~(1u << j);
-  uint32_t ci = first + (uint32_t)__popc(mask & ((1u << ((uint32_t)j ^ dm)) - 1u));
-  float4 nlo = plo, nhi = phi;
-  if (COUNT) wc.nodes += lanes_distinct(ci);
-  int sp0 = s.sp;
-  for (;;) {
-    float4 clo = nlo, chi = nhi;
-    bool more = mj != 0u;
-    if (more) {
-      j = 31 - __clz(mj);
-      mj &= ~(1u << j);
-      ci = first + (uint32_t)__popc(mask & ((1u << ((uint32_t)j ^ dm)) - 1u));
-      nlo = node[2 * ci];
-      nhi = node[2 * ci + 1];
-      if (COUNT) wc.nodes += lanes_distinct(ci);
-    }
-    if (box_enter(r, inv, clo, chi) != __builtin_inff()) {
-      int sp1 = s.sp;
-      push(s, __float_as_uint(clo.w), chi.w, wc);
-      if (s.sp != sp1) {
-        tf = __float_as_uint(clo.w);
-        ti = __float_as_uint(chi.w);
-      }
-    }
-    if (!more) break;
-  }
-  return s.sp != sp0;
-}
-
-template <bool COUNT>
-__device__ __forceinline__ void push_children_any(const float4* __restrict__ node, const Ray& r,
-                                                  f3 inv, uint32_t dm, uint32_t first,
-                                                  uint32_t info, Stack& s, LaneCount& wc) {
-  uint32_t mask = RT_NODE_MASK(info);
-#if RT_CHILD_PIPE
-  // Same far-to-near order as below (j = 7..0, octant j ^ dm), software-
-  // pipelined: child k+1's box is in flight while child k is tested.
-  uint32_t mj = mask_xor(mask, dm);
-  if (!mj) return;
-  int j = 31 - __clz(mj);
-  mj &= ~(1u << j);
-  uint32_t o = (uint32_t)j ^ dm;
-  uint32_t ci = first + (uint32_t)__popc(mask & ((1u << o) - 1u));
-  float4 nlo = node[2 * ci], nhi = node[2 * ci + 1];
-  if (COUNT) wc.nodes += lanes_distinct(ci);
-  for (;;) {
-    float4 clo = nlo, chi = nhi;
-    bool more = mj != 0u;
-    if (more) {
-      j = 31 - __clz(mj);
-      mj &= ~(1u << j);
-      o = (uint32_t)j ^ dm;
-      ci = first + (uint32_t)__popc(mask & ((1u << o) - 1u));
-      nlo = node[2 * ci];
-      nhi = node[2 * ci + 1];
-      if (COUNT) wc.nodes += lanes_distinct(ci);
-    }
-    if (box_enter(r, inv, clo, chi) != __builtin_inff()) push(s, __float_as_uint(clo.w), chi.w, wc);
-    if (!more) break;
-  }
-  return;
-#endif
-#pragma unroll 1
-  for (int j = 7; j >= 0; --j) {
-    uint32_t o = (uint32_t)j ^ dm;
-    if (mask & (1u << o)) {
-      uint32_t ci = first + (uint32_t)__popc(mask & ((1u << o) - 1u));
-      if (COUNT) wc.nodes += lanes_distinct(ci);
-      float4 clo = node[2 * ci], chi = node[2 * ci + 1];
-      if (box_enter(r, inv, clo, chi) == __builtin_inff()) continue;
-      push(s, __float_as_uint(clo.w), chi.w, wc);
-    }
-  }
-}
-
-#ifndef RT_OCC_CACHE
-#define RT_OCC_CACHE 0  // measured: C5 15.37/15.56 (on) vs 15.33/15.53 ms (off): a wave waits for its slowest lane
-#endif
-#ifndef RT_OCC_SLOTS
-#define RT_OCC_SLOTS 2  // one cached occluder per light parity
-#endif
-#ifndef RT_WHILE_WHILE
-#define RT_WHILE_WHILE 0  // measured: C5 15.89/16.00 (on) vs 15.46/15.57 ms (off)
-#endif
-
+// Per-lane any-hit walk; a stack entry holds the node's own (first, info).
 template <bool COUNT>
 __device__ bool oct_any(const KParams& p, const Ray& r, Stack& s, LaneCount& wc) {
   const float4* __restrict__ node = p.node;
-  const float4* __restrict__ tri = p.tri;
   f3 inv = inv_dir(r.d);
   uint32_t dm = near_octant(r.d);
   s.sp = 0;
-#if RT_OCC_CACHE
-  // Occluder cache: the triangle that blocked this lane's previous shadow ray
-  // (a neighbouring supersample's, usually) is tested first.  Any record hit
-  // with the walk's own exact test decides the query (cpu/light.c:24-31 is an
-  // any-hit predicate), so this only reorders work.
-  uint32_t oc = (RT_OCC_SLOTS == 2 && s.slot) ? s.occ2 : s.occ;
-  if (oc != 0xffffffffu) {
-    const float4* q = tri + 3 * (size_t)oc;
-    if (COUNT) wc.tris += lanes_distinct(oc);
-    if (any_hit_rec(r, q[0], q[1], q[2])) return true;
-  }
-#endif
+  wave_sync();
   {
     float4 lo = node[0], hi = node[1];
     if (COUNT) wc.nodes += lanes_distinct(0);
     if (box_enter(r, inv, lo, hi) != __builtin_inff()) push(s, __float_as_uint(lo.w), hi.w, wc);
   }
-#if RT_PREFETCH && !RT_WHILE_WHILE
-  // Prefetch: when a node's children were pushed, the new stack top is known
-  // (the nearest child) and its first payload -- its first child's box, or
-  // its first triangle record -- is loaded at once, so the next iteration's
-  // pop does not start with a dependent load.  Same visiting order and
-  // results as the loop below; only the load issue moves earlier.
-  {
-    bool pf = false;
-    float4 p0, p1, p2;
-    while (s.sp > 0) {
-      uint32_t first;
-      float info_bits;
-      pop(s, first, info_bits);
-      uint32_t info = __float_as_uint(info_bits);
-      bool have = pf;
-      pf = false;
-      if (info & RT_NODE_LEAF) {
-        uint32_t cnt = RT_LEAF_COUNT(info);
-        const float4* q = tri + 3 * (size_t)first;
-        if (!have) {
-          p0 = q[0];
-          p1 = q[1];
-          p2 = q[2];
-        }
-        float4 n0 = p0, n1 = p1, n2 = p2;
-        for (uint32_t k = 0; k < cnt; k++) {
-          float4 q0 = n0, q1 = n1, q2 = n2;
-          if (k + 1 < cnt) {
-            n0 = q[3 * (k + 1)];
-            n1 = q[3 * (k + 1) + 1];
-            n2 = q[3 * (k + 1) + 2];
-          }
-          if (COUNT) wc.tris += lanes_distinct(first + k);
-          if (any_hit_rec(r, q0, q1, q2)) {
-            s.sp = 0;
-            return true;
-          }
-        }
-      } else {
-        if (!have) {
-          uint32_t c0 = first_child(first, info, dm);
-          p0 = node[2 * c0];
-          p1 = node[2 * c0 + 1];
-        }
-        uint32_t tf = 0, ti = 0;
-        if (push_children_any_pf<COUNT>(node, r, inv, dm, first, info, p0, p1, s, wc, tf, ti)) {
-          pf = true;
-          if (ti & RT_NODE_LEAF) {
-            const float4* q = tri + 3 * (size_t)tf;
-            p0 = q[0];
-            p1 = q[1];
-            p2 = q[2];
-          } else {
-            uint32_t c0 = first_child(tf, ti, dm);
-            p0 = node[2 * c0];
-            p1 = node[2 * c0 + 1];
-          }
-        }
-      }
-    }
-    return false;
-  }
-#endif
-#if RT_WHILE_WHILE
-  // "while-while" order (Aila & Laine 2009): each lane descends interior
-  // nodes until it holds a leaf (or its stack is empty); the leaf tests then
-  // run with every lane that found one active at once, instead of the leaf
-  // loop and the child loop alternating as divergent branches.
-  for (;;) {
-    uint32_t lf = 0, lcnt = 0;
-    bool have = false;
-    while (!have && s.sp > 0) {
-      uint32_t first;
-      float info_bits;
-      pop(s, first, info_bits);
-      uint32_t info = __float_as_uint(info_bits);
-      if (info & RT_NODE_LEAF) {
-        have = true;
-        lf = first;
-        lcnt = RT_LEAF_COUNT(info);
-      } else {
-        push_children_any<COUNT>(node, r, inv, dm, first, info, s, wc);
-      }
-    }
-    if (!have) return false;
-    const float4* q = tri + 3 * (size_t)lf;
-    float4 n0 = q[0], n1 = q[1], n2 = q[2];
-    for (uint32_t k = 0; k < lcnt; k++) {
-      float4 q0 = n0, q1 = n1, q2 = n2;
-      if (k + 1 < lcnt) {
-        n0 = q[3 * (k + 1)];
-        n1 = q[3 * (k + 1) + 1];
-        n2 = q[3 * (k + 1) + 2];
-      }
-      if (COUNT) wc.tris += lanes_distinct(lf + k);
-      if (any_hit_rec(r, q0, q1, q2)) {
-        s.sp = 0;
-        return true;
-      }
-    }
-  }
-#endif
+  Best unused;
   while (s.sp > 0) {
     uint32_t first;
     float info_bits;
     pop(s, first, info_bits);
     uint32_t info = __float_as_uint(info_bits);
     if (info & RT_NODE_LEAF) {
-      uint32_t cnt = RT_LEAF_COUNT(info);
-#if RT_LEAF_PIPE
-      // software-pipelined: record k+1 is in flight while record k is tested
-      const float4* q = tri + 3 * (size_t)first;
-      float4 n0 = q[0], n1 = q[1], n2 = q[2];
-      for (uint32_t k = 0; k < cnt; k++) {
-        float4 q0 = n0, q1 = n1, q2 = n2;
-        if (k + 1 < cnt) {
-          n0 = q[3 * (k + 1)];
-          n1 = q[3 * (k + 1) + 1];
-          n2 = q[3 * (k + 1) + 2];
-        }
-        if (COUNT) wc.tris += lanes_distinct(first + k);
-        if (any_hit_rec(r, q0, q1, q2)) {
-          s.sp = 0;
-          if (RT_OCC_SLOTS == 2 && s.slot)
-            s.occ2 = first + k;
-          else
-            s.occ = first + k;
-          return true;
-        }
+      if (leaf_lane<true, COUNT>(p.tri, first, RT_LEAF_COUNT(info), r, unused, wc)) {
+        s.sp = 0;
+        wave_sync();
+        return true;
       }
-#else
-      for (uint32_t k = 0; k < cnt; k++) {
-        const float4* q = tri + 3 * (size_t)(first + k);
-        if (COUNT) wc.tris += lanes_distinct(first + k);
-        if (any_hit_rec(r, q[0], q[1], q[2])) {
-          s.sp = 0;
-          return true;
-        }
-      }
-#endif
     } else {
-      push_children_any<COUNT>(node, r, inv, dm, first, info, s, wc);
+      push_children<false, COUNT>(node, r, inv, dm, first, info, 0.0f, s, wc);
     }
   }
+  wave_sync();
   return false;
 }
 
-// ------------------------------------------------------ PACKET (wave) walk
-// The 64 lanes of a wave walk the octree together: one wave-uniform stack of
-// node indices in LDS, node and triangle records fetched once per wave with
-// wave-uniform addresses (broadcast to every lane), each lane testing its own
-// ray, and __ballot deciding which children any lane still needs.  Camera
-// rays of an 8x8 tile and shadow rays toward one light are coherent, so the
-// union of the lanes' walks is barely larger than each one's.
-static constexpr int kWaveStack = 192;
-
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
-__device__ __forceinline__ float4 uni4(float4 v) {
-  return make_float4(__uint_as_float(uni(__float_as_uint(v.x))),
-                     __uint_as_float(uni(__float_as_uint(v.y))),
-                     __uint_as_float(uni(__float_as_uint(v.z))),
-                     __uint_as_float(uni(__float_as_uint(v.w))));
-}
 // Wave-uniform loads through the constant address space: with a uniform
 // address they become scalar (SMEM) loads straight into SGPRs.  The scene
 // image is read-only for the whole launch.
@@ -710,11 +398,6 @@ __device__ __forceinline__ float4 ldu(const float4* p, size_t i) {
 #else
   return p[i];  // host pass only parses device code
 #endif
-}
-__device__ __forceinline__ void node_u(const float4* __restrict__ node, uint32_t ni, float4& lo,
-                                       float4& hi) {
-  lo = ldu(node, 2 * (size_t)ni);
-  hi = ldu(node, 2 * (size_t)ni + 1);
 }
 
 // majority ray-direction octant of the active lanes (child push order)
@@ -727,138 +410,32 @@ __device__ __forceinline__ uint32_t wave_near_octant(bool act, f3 d, uint64_t am
   return dm;
 }
 
-// Must be called by all 64 lanes (converged); act = this lane has a query.
-template <bool COUNT>
-__device__ void packet_closest(const KParams& p, const Ray& r, bool act, Best& b, uint32_t* ws,
-                               int lane, WorkCount& wc) {
-  const float4* __restrict__ node = p.node;
-  const float4* __restrict__ tri = p.tri;
-  uint64_t am = __ballot(act);
-  if (am == 0) return;
-  f3 inv = inv_dir(r.d);
-  uint32_t dm = wave_near_octant(act, r.d, am);
-  int sp = 0;
-  ws[sp++] = 0;
-  while (sp > 0) {
-    uint32_t ni = uni(ws[--sp]);
-    float4 lo, hi;
-    node_u(node, ni, lo, hi);
-    float tn = box_enter(r, inv, lo, hi);
-    bool want = act && tn != __builtin_inff() &&
-                !(b.dist != __builtin_inff() && rt_prune(tn, r.dlen, b.dist, r.eps));
-    if (__ballot(want) == 0) continue;
-    uint32_t first = __float_as_uint(lo.w), info = __float_as_uint(hi.w);
-    if (COUNT) wc.nodes++;
-    if (info & RT_NODE_LEAF) {
-      uint32_t cnt = RT_LEAF_COUNT(info);
-      for (uint32_t k = 0; k < cnt; k++) {
-        const float4* q = tri + 3 * (size_t)(first + k);
-        float4 q0 = ldu(q, 0), q1 = ldu(q, 1), q2 = ldu(q, 2);
-        if (want) consider(r, q0, q1, q2, b);
-      }
-      if (COUNT) wc.tris += cnt;
-    } else {
-      uint32_t mask = RT_NODE_MASK(info);
-      for (int j = 7; j >= 0; --j) {
-        uint32_t o = (uint32_t)j ^ dm;
-        if (!(mask & (1u << o))) continue;
-        uint32_t ci = first + (uint32_t)__popc(mask & ((1u << o) - 1u));
-        float4 clo, chi;
-        node_u(node, ci, clo, chi);
-        float t0 = box_enter(r, inv, clo, chi);
-        bool w2 = want && t0 != __builtin_inff() &&
-                  !(b.dist != __builtin_inff() && rt_prune(t0, r.dlen, b.dist, r.eps));
-        if (__ballot(w2) != 0) {
-          if (sp < kWaveStack)
-            ws[sp++] = ci;
-          else
-            wc.overflow++;  // RT_EDEPTH, never silent
-        }
-      }
-    }
-  }
-}
-
-template <bool COUNT>
-__device__ bool packet_any(const KParams& p, const Ray& r, bool act, uint32_t* ws, int lane,
-                           WorkCount& wc) {
-  const float4* __restrict__ node = p.node;
-  const float4* __restrict__ tri = p.tri;
-  bool alive = act, hit = false;
-  uint64_t am = __ballot(alive);
-  if (am == 0) return false;
-  f3 inv = inv_dir(r.d);
-  uint32_t dm = wave_near_octant(act, r.d, am);
-  int sp = 0;
-  ws[sp++] = 0;
-  while (sp > 0) {
-    uint32_t ni = uni(ws[--sp]);
-    float4 lo, hi;
-    node_u(node, ni, lo, hi);
-    bool want = alive && box_enter(r, inv, lo, hi) != __builtin_inff();
-    if (__ballot(want) == 0) continue;
-    uint32_t first = __float_as_uint(lo.w), info = __float_as_uint(hi.w);
-    if (COUNT) wc.nodes++;
-    if (info & RT_NODE_LEAF) {
-      uint32_t cnt = RT_LEAF_COUNT(info);
-      for (uint32_t k = 0; k < cnt; k++) {
-        const float4* q = tri + 3 * (size_t)(first + k);
-        float4 q0 = ldu(q, 0), q1 = ldu(q, 1), q2 = ldu(q, 2);
-        if (COUNT) wc.tris++;
-        if (want && any_hit_rec(r, q0, q1, q2)) {
-          hit = true;
-          alive = false;
-          want = false;
-        }
-        if (__ballot(want) == 0) break;
-      }
-      if (__ballot(alive) == 0) break;
-    } else {
-      uint32_t mask = RT_NODE_MASK(info);
-      for (int j = 7; j >= 0; --j) {
-        uint32_t o = (uint32_t)j ^ dm;
-        if (!(mask & (1u << o))) continue;
-        uint32_t ci = first + (uint32_t)__popc(mask & ((1u << o) - 1u));
-        float4 clo, chi;
-        node_u(node, ci, clo, chi);
-        bool w2 = want && box_enter(r, inv, clo, chi) != __builtin_inff();
-        if (__ballot(w2) != 0) {
-          if (sp < kWaveStack)
-            ws[sp++] = ci;
-          else
-            wc.overflow++;
-        }
-      }
-    }
-  }
-  return hit;
-}
-
 // ------------------------------------------- PACKET walk, LDS-staged records
-// Same wave walk, but every fetch is one coalesced vector load by the lanes
-// (lane k loads float4 k of the records) staged in LDS, then read back as
-// broadcasts: a leaf's triangle records (3 float4 each, 21 per chunk) or an
-// interior node's child boxes (2 float4 each, <= 8 children, contiguous) cost
-// one memory round trip instead of one per record.  The wave stack holds the
-// pushed child's whole node record (box + first/info), so a pop needs no
-// memory access before the next fetch is issued.
+// The 64 lanes of a wave walk the octree together: every fetch is one
+// coalesced vector load by the lanes (lane k loads float4 k of the records)
+// staged in LDS, then read back as broadcasts: a leaf's triangle records (3
+// float4 each, 32 per chunk) or an interior node's child boxes (2 float4
+// each, <= 8 children, contiguous) cost one memory round trip instead of one
+// per record.  The wave stack holds the pushed child's whole node record (box
+// + first/info) and the mask of the lanes that wanted it, so a pop needs no
+// memory access before the next fetch is issued.  Camera rays of an 8x8 tile
+// are coherent, so the union of the lanes' walks is barely larger than each
+// one's.
 // float4 staging slots per wave: FLAT streams 64 triangle records at a time;
 // the octree walk stages one node's payload (<= 8 children, or a leaf's
 // records, RT_OCT_LEAF_CAP = 32 of them in one chunk).  LDS per one-wave
 // workgroup must stay <= 10 KB for 16 workgroups per CU.
 static constexpr int kStageFlat = 192;
-#ifndef RT_STAGE_OCT
-#define RT_STAGE_OCT 96
-#endif
-static constexpr int kStageOct = RT_STAGE_OCT;
-#ifndef RT_STACK2
-#define RT_STACK2 96
-#endif
-static constexpr int kStack2 = RT_STACK2;  // wave stack entries (2 float4 each)
+static constexpr int kStageOct = 96;
+static constexpr int kStack2 = 96;  // wave stack entries (2 float4 each)
+// float4 slots of the stack area: the staged walk's kStack2 x (2 float4 + a
+// lane mask), or the per-lane stacks' kLdsStack x 64 x (index, t)
+static constexpr int kStackArea = (2 * kStack2 * 16 + kStack2 * 8 > kLdsStack * 64 * 8
+                                       ? 2 * kStack2 * 16 + kStack2 * 8
+                                       : kLdsStack * 64 * 8) / 16;
 
 struct WaveCtx {
-  uint32_t* ws;    // kWaveStack node indices (packet walk)
-  float4* stk2;    // kStack2 x 2 float4 (staged packet walk)
+  float4* stk2;    // kStack2 x 2 float4
   uint64_t* stkm;  // kStack2 lane masks: lanes that wanted the pushed node
   float4* stage;   // kStageFlat / kStageOct float4
   int lane;
@@ -881,10 +458,6 @@ __device__ __forceinline__ Fetch fetch_issue(const float4* __restrict__ src, int
   return f;
 }
 
-// The workgroup is one wave and a wave's LDS instructions execute in issue
-// order, so staging needs no s_barrier: only a compiler barrier that keeps
-// the LDS reads and writes in source order.
-__device__ __forceinline__ void wave_sync() { __asm__ volatile("" ::: "memory"); }
 
 __device__ __forceinline__ void fetch_commit(const Fetch& f, WaveCtx& w) {
   const int l = w.lane;
@@ -1005,10 +578,6 @@ __device__ __forceinline__ void stage_push_children(const Ray& r, f3 inv, uint32
   }
 }
 
-#ifndef RT_STAGE_PIPE
-#define RT_STAGE_PIPE 0  // measured: C5 15.34 (off) vs 15.65 ms (on)
-#endif
-
 template <bool COUNT>
 __device__ void staged_closest(const KParams& p, const Ray& r, bool act, Best& b, WaveCtx& w,
                                WorkCount& wc) {
@@ -1048,23 +617,10 @@ __device__ void staged_closest(const KParams& p, const Ray& r, bool act, Best& b
       for (uint32_t base = 0; base < cnt; base += kOctRecs) {
         uint32_t m = chunk<kOctRecs>(cnt, base);
         if (base) stage_load(tri + 3 * (size_t)(first + base), 3 * (int)m, w);
-#if RT_STAGE_PIPE
-        // software-pipelined: record k+1's LDS reads are in flight while k is tested
-        float4 n0 = w.stage[0], n1 = w.stage[1], n2 = w.stage[2];
-        for (uint32_t k = 0; k < m; k++) {
-          float4 q0 = n0, q1 = n1, q2 = n2;
-          uint32_t kn = k + 1 < m ? 3 * (k + 1) : 0;
-          n0 = w.stage[kn];
-          n1 = w.stage[kn + 1];
-          n2 = w.stage[kn + 2];
-          if (want) consider(r, q0, q1, q2, b);
-        }
-#else
         for (uint32_t k = 0; k < m; k++) {
           float4 q0 = w.stage[3 * k], q1 = w.stage[3 * k + 1], q2 = w.stage[3 * k + 2];
           if (want) consider(r, q0, q1, q2, b);
         }
-#endif
       }
       limit = rt_prune_limit(b.dist, r.eps);
       if (COUNT) wc.tris += cnt;
@@ -1124,70 +680,56 @@ __device__ bool staged_any(const KParams& p, const Ray& r, bool act, WaveCtx& w,
   return hit;
 }
 
-// Traversal policy: per-lane walks (each lane its own stack) or a packet
-// walk; with TRAV_HYBRID the packet walk is used while at least
-// p.packet_min lanes of the wave have a query.
-#ifndef RT_LEAN  // 1: only the staged-hybrid closest walk and the per-lane any-hit walk
-#define RT_LEAN 0
-#endif
-#define RT_TRAV_LANE 0
-#define RT_TRAV_PACKET 1
-#define RT_TRAV_HYBRID 2
-#define RT_TRAV_STAGED 3         // staged packet walk always
-#define RT_TRAV_STAGED_HYBRID 4  // staged packet walk while >= packet_min lanes
+// Traversal policy of an instantiation (RT_POLICY_*, rt_kernels.h).  The
+// default: closest-hit queries walk as a staged packet while at least
+// kPacketMin lanes query at a bounce depth <= kPacketMaxDepth (camera rays
+// and first reflections; deeper reflections are incoherent), else per lane;
+// shadow queries walk per lane, except directional-light shadows (parallel
+// rays, cpu/light.c:53) under RT_POLICY_DIR_STAGED.
+static constexpr int kPacketMin = 8;
+static constexpr int kPacketMaxDepth = 1;
 
 // Closest-hit query; converged call, act = lane has a query.
-template <int ACCEL, bool COUNT>
+template <int ACCEL, bool COUNT, int POL>
 __device__ __forceinline__ void closest_q(const KParams& p, const Ray& r, bool act, int depth, Best& b,
                                           Stack& s, WaveCtx& w, WorkCount& wc) {
   if (ACCEL == RT_ACCEL_FLAT_D) {
     flat_closest_w<COUNT>(p, r, act, b, w, wc);
     return;
   }
-  // packet walk for coherent queries: enough lanes, and a bounce depth at
-  // which rays are still coherent (camera rays: depth 0)
-  bool many = __popcll(__ballot(act)) >= p.packet_min && depth <= p.packet_max_depth;
-  if (p.trav == RT_TRAV_STAGED || (p.trav == RT_TRAV_STAGED_HYBRID && many))
+  bool staged = POL == RT_POLICY_STAGED ||
+                (POL != RT_POLICY_LANE && __popcll(__ballot(act)) >= kPacketMin &&
+                 depth <= kPacketMaxDepth);
+  if (staged) {
     staged_closest<COUNT>(p, r, act, b, w, wc);
-#if !RT_LEAN
-  else if (p.trav == RT_TRAV_PACKET || (p.trav == RT_TRAV_HYBRID && many))
-    packet_closest<COUNT>(p, r, act, b, w.ws, w.lane, wc);
-#endif
-  else {
+  } else {
     LaneCount lc = {0, 0, 0};
     if (act) oct_closest<COUNT>(p, r, b, s, lc);
     absorb<COUNT>(wc, lc);
   }
 }
 
-// Shadow query (collide_dist > 0.01, cpu/light.c:24-31); converged call.
-template <int ACCEL, bool COUNT>
-__device__ __forceinline__ bool shadow_q(const KParams& p, f3 o, f3 d, bool act, Stack& s,
-                                         WaveCtx& w, WorkCount& wc) {
+// Shadow query (collide_dist > 0.01, cpu/light.c:24-31) of a light of the
+// given type; converged call.
+template <int ACCEL, bool COUNT, int POL>
+__device__ __forceinline__ bool shadow_q(const KParams& p, f3 o, f3 d, uint32_t type, bool act,
+                                         Stack& s, WaveCtx& w, WorkCount& wc) {
   uint64_t am = __ballot(act);
   wc.shadow += (uint32_t)__popcll(am);
-#ifdef RT_DBG_SHADOW_SLOTS  // lane slots of shadow calls (in zero_normal; breakdown only)
-  if (am) wc.zero_normal += 64u;
-#endif
-#ifdef RT_DBG_NO_SHADOW  // timing breakdown only (wrong images)
-  return false;
-#endif
   Ray r = make_ray(p, o, d);
   if (ACCEL == RT_ACCEL_FLAT_D) return flat_any_w<COUNT>(p, r, act, w, wc);
-  bool many = __popcll(am) >= p.packet_min_shadow;
-#if !RT_LEAN
-  if (p.trav_shadow == RT_TRAV_STAGED || (p.trav_shadow == RT_TRAV_STAGED_HYBRID && many))
-    return staged_any<COUNT>(p, r, act, w, wc);
-  if (p.trav_shadow == RT_TRAV_PACKET || (p.trav_shadow == RT_TRAV_HYBRID && many))
-    return packet_any<COUNT>(p, r, act, w.ws, w.lane, wc);
-#else
-  (void)many;
-#endif
+  bool staged = POL == RT_POLICY_STAGED ||
+                (POL == RT_POLICY_DIR_STAGED && type == 1 && __popcll(am) >= kPacketMin);
+  if (staged) return staged_any<COUNT>(p, r, act, w, wc);
   LaneCount lc = {0, 0, 0};
   bool hit = act && oct_any<COUNT>(p, r, s, lc);
   absorb<COUNT>(wc, lc);
   return hit;
 }
+
+// pow of cpu/light.c:20, out of line: inlined, its f64 polynomial
+// coefficients were hoisted out of the path loop and spilled to scratch.
+__device__ __noinline__ float spec_pow(double x, double e) { return (float)pow(fmax(x, 0.0), e); }
 
 // cpu/light.c:7-22
 __device__ __forceinline__ col specular(col tmp, f3 inc_o, f3 inc_d, f3 P, f3 N, const float* m) {
@@ -1196,7 +738,7 @@ __device__ __forceinline__ col specular(col tmp, f3 inc_o, f3 inc_d, f3 P, f3 N,
   f3 R = sub(inc_d, scale(N, 2.0f * dot(N, inc_d)));
   R = normalize(R);
   V = normalize(V);
-  float ls = (float)pow(fmax((double)dot(R, V), 0.0), (double)m[9]);
+  float ls = spec_pow((double)dot(R, V), (double)m[9]);
   k = color_mul(k, ls);
   return color_add(tmp, k);
 }
@@ -1233,7 +775,7 @@ __device__ __forceinline__ col light_lit(uint32_t type, col lc, f3 lv, const flo
 
 // cpu/light.c:33-100 for the lanes with hit.  The light loop is wave-uniform
 // so shadow queries run converged.
-template <int ACCEL, bool COUNT>
+template <int ACCEL, bool COUNT, int POL>
 __device__ col apply_light(const KParams& p, bool hit, const float* m, f3 P, f3 N, Stack& s,
                            WaveCtx& w, WorkCount& wc) {
   col acc = init_color(0.0f, 0.0f, 0.0f);
@@ -1245,8 +787,7 @@ __device__ col apply_light(const KParams& p, bool hit, const float* m, f3 P, f3 
     if (type == 0) {  // AMBIENT
       if (hit) acc = color_add(acc, color_mul2(lc, init_color(m[0], m[1], m[2])));
     } else if (type == 1 || type == 2) {
-      s.slot = li & 1u;
-      bool sh = shadow_q<ACCEL, COUNT>(p, P, shadow_dir(type, lv, P), hit, s, w, wc);
+      bool sh = shadow_q<ACCEL, COUNT, POL>(p, P, shadow_dir(type, lv, P), type, hit, s, w, wc);
       if (hit && !sh) acc = color_add(acc, light_lit(type, lc, lv, m, P, N));
     }
   }
@@ -1302,13 +843,50 @@ __device__ __forceinline__ void cand_closest(const KParams& p, const Ray& r, boo
   if (COUNT) wc.tris += tested + p.n_cand_global;
 }
 
+// Reflection terms of one path, folded deepest-first at the end
+// (cpu/raytracer.c:19-34 returns color_add(local, reflected) from the
+// deepest call outwards).  The first kLdsTerms live in LDS, [term][channel]
+// [lane] so a wave's accesses are conflict-free (in registers they were
+// spilled around every walk: the walks need all 128 VGPRs); deeper ones --
+// rare, C5 paths end by depth 3 -- go to this lane's slots of a global
+// overflow area laid out [term][lane] so a wave's stores coalesce.
+static constexpr int kLdsTerms = RT_LDS_TERMS;
+
+struct Terms {
+  float* lds;     // s_terms + lane
+  float* over;    // p.terms + 3 * global lane
+  size_t stride;  // floats between consecutive overflow terms of a lane
+};
+
+__device__ __forceinline__ void term_put(Terms& T, int k, col c) {
+  if (k < kLdsTerms) {
+    float* q = T.lds + k * 192;
+    q[0] = c.r;
+    q[64] = c.g;
+    q[128] = c.b;
+  } else {
+    float* q = T.over + (size_t)(k - kLdsTerms) * T.stride;
+    q[0] = c.r;
+    q[1] = c.g;
+    q[2] = c.b;
+  }
+}
+
+__device__ __forceinline__ col term_get(const Terms& T, int k) {
+  if (k < kLdsTerms) {
+    const float* q = T.lds + k * 192;
+    return col{q[0], q[64], q[128]};
+  }
+  const float* q = T.over + (size_t)(k - kLdsTerms) * T.stride;
+  return col{q[0], q[1], q[2]};
+}
+
 // One camera sample (cpu/raytracer.c:19-34) for every lane of the wave: the
-// recursion becomes a wave-uniform bounce loop; local terms are buffered and
-// folded deepest-first.  valid = the lane owns a pixel.
-template <int ACCEL, bool COUNT>
-__device__ __forceinline__ col trace_path(const KParams& p, bool valid, f3 o, f3 d, float coef, Stack& s,
-                          WaveCtx& w, WorkCount& wc, uint32_t tile) {
-  col terms[kMaxDepth];
+// recursion becomes a wave-uniform bounce loop.  valid = the lane owns a pixel.
+template <int ACCEL, bool COUNT, int POL>
+__device__ __forceinline__ col trace_path(const KParams& p, bool valid, f3 o, f3 d, float coef,
+                                          Stack& s, WaveCtx& w, WorkCount& wc, uint32_t tile,
+                                          Terms& T) {
   int depth = 0;
   bool alive = valid;
   for (;;) {
@@ -1323,12 +901,8 @@ __device__ __forceinline__ col trace_path(const KParams& p, bool valid, f3 o, f3
     b.prim = 0xffffffffu;
     b.obj = 0;
     b.u = b.v = 0.0f;
-#if RT_BEST_T
     b.t = 0.0f;
-#else
-    b.pt = o;
-#endif
-    closest_q<ACCEL, COUNT>(p, r, alive, depth, b, s, w, wc);
+    closest_q<ACCEL, COUNT, POL>(p, r, alive, depth, b, s, w, wc);
     if (ACCEL != RT_ACCEL_FLAT_D && depth == 0) cand_closest<COUNT>(p, r, alive, tile, b, wc);
     bool hit = alive && b.dist != __builtin_inff();
     f3 N = f3{0.0f, 0.0f, 0.0f};
@@ -1343,24 +917,16 @@ __device__ __forceinline__ col trace_path(const KParams& p, bool valid, f3 o, f3
     wc.zero_normal += (uint32_t)__popcll(__ballot(zero));
     hit = hit && !zero;
     const float* m = p.mat + RT_MAT_FLOATS_D * (hit ? b.obj : 0u);
-#if RT_BEST_T
-    // the winner's hit point, same operations as hit_dist (same bits)
-    f3 P = hit ? add(r.o, scale(r.nd, b.t * r.dlen)) : o;
-#else
-    f3 P = b.pt;
-#endif
-    col local = apply_light<ACCEL, COUNT>(p, hit, m, P, N, s, w, wc);
+    f3 P = hit ? hit_point(r, b.t) : o;  // the winner's hit point, same bits
+    col local = apply_light<ACCEL, COUNT, POL>(p, hit, m, P, N, s, w, wc);
     alive = hit;
-#ifdef RT_DBG_NO_BOUNCE  // timing breakdown only (wrong images)
-    alive = false;
-#endif
     bool deep = hit && depth == kMaxDepth;
     wc.overflow += (uint32_t)__popcll(__ballot(deep));
     if (hit) {
       if (deep) {
         alive = false;
       } else {
-        terms[depth++] = color_mul(local, coef);
+        term_put(T, depth++, color_mul(local, coef));
         d = bounce_dir(d, N);
         o = P;
         coef = m[10] * coef;
@@ -1368,53 +934,46 @@ __device__ __forceinline__ col trace_path(const KParams& p, bool valid, f3 o, f3
     }
   }
   col acc = init_color(0.0f, 0.0f, 0.0f);
-  for (int k = depth - 1; k >= 0; --k) acc = color_add(acc, terms[k]);
+  for (int k = depth - 1; k >= 0; --k) acc = color_add(acc, term_get(T, k));
   return acc;
 }
 
-template <int ACCEL, bool COUNT, int MINW>
-__global__ __launch_bounds__(64, MINW) void render_kernel(KParams p) {
+template <int ACCEL, bool COUNT, int POL>
+__global__ __launch_bounds__(64, RT_MIN_WAVES) void render_kernel(KParams p) {
   const int lane = threadIdx.x & 63;
   WorkCount wc = {};
-  __shared__ uint32_t s_idx[ACCEL == RT_ACCEL_FLAT_D ? 1 : kLdsStack * 64];
-  __shared__ float s_t[ACCEL == RT_ACCEL_FLAT_D ? 1 : kLdsStack * 64];
-  __shared__ uint32_t s_ws[ACCEL == RT_ACCEL_FLAT_D ? 1 : kWaveStack];
-  __shared__ float4 s_stk2[ACCEL == RT_ACCEL_FLAT_D ? 1 : 2 * kStack2];
+  // The per-lane stacks and the staged wave stack share one LDS area: a
+  // wave runs one walk at a time and every walk starts and ends with an
+  // empty stack (wave_sync() at both ends orders the accesses).
+  __shared__ float4 s_stack[ACCEL == RT_ACCEL_FLAT_D ? 1 : kStackArea];
   __shared__ float4 s_stage[ACCEL == RT_ACCEL_FLAT_D ? kStageFlat : kStageOct];
-  __shared__ uint64_t s_stkm[ACCEL == RT_ACCEL_FLAT_D ? 1 : kStack2];
+  __shared__ float s_terms[kLdsTerms * 3 * 64];
+  const size_t gl = (size_t)blockIdx.x * 64 + (size_t)lane;
   Stack stk;
-  stk.idx = s_idx;
-  stk.tt = s_t;
-  stk.spill = p.spill + ((size_t)blockIdx.x * 64 + (size_t)lane) * kSpillStack;
+  stk.idx = (uint32_t*)s_stack;
+  stk.tt = (float*)s_stack + kLdsStack * 64;
+  stk.spill = p.spill + gl * kSpillStack;
   stk.lane = lane;
   stk.sp = 0;
-  stk.occ = stk.occ2 = 0xffffffffu;
-  stk.slot = 0;
   WaveCtx w;
-  w.ws = s_ws;
-  w.stk2 = s_stk2;
-  w.stkm = s_stkm;
+  w.stk2 = s_stack;
+  w.stkm = (uint64_t*)(s_stack + 2 * kStack2);
   w.stage = s_stage;
   w.lane = lane;
-  // Tile scheduling: the rank's tiles are cut into RT_BANDS contiguous bands
-  // (image stripes); workgroup b starts on band b % RT_BANDS and moves on to
-  // the other bands when its own is drained.  Default one band: every wave
-  // pulls the next tile in scanline order (rt_kernels.h says why).
+  Terms T;
+  T.lds = s_terms + lane;
+  T.over = p.terms + 3 * gl;
+  T.stride = 3 * (size_t)gridDim.x * 64;
+  // Persistent waves pull the rank's tiles in scanline order from one atomic
+  // counter: all 8 XCDs then work on the same few tile rows, whose geometry
+  // stays in the Infinity Cache (measured, C5: 8 per-XCD bands ran 13 %
+  // slower).
   const uint32_t nt = (uint32_t)p.ntiles_local;
-  const uint32_t home = (uint32_t)blockIdx.x % RT_BANDS;
-  uint32_t probe = 0;
   for (;;) {
-    uint32_t band = (home + probe) % RT_BANDS;
-    uint32_t lo = (uint32_t)(((uint64_t)nt * band) / RT_BANDS);
-    uint32_t hi = (uint32_t)(((uint64_t)nt * (band + 1)) / RT_BANDS);
     uint32_t t = 0;
-    if (lane == 0) t = atomicAdd(p.tile_counter + band, 1u);
+    if (lane == 0) t = atomicAdd(p.tile_counter, 1u);
     t = uni(t);
-    if (t >= hi - lo) {
-      if (++probe == RT_BANDS) break;  // every band drained: the wave exits
-      continue;
-    }
-    t += lo;
+    if (t >= nt) break;  // every tile taken: the wave exits
     uint32_t g = t * (uint32_t)p.nranks + (uint32_t)p.rank;  // global tile index
     int ty = (int)(g / (uint32_t)p.tiles_x), tx = (int)(g % (uint32_t)p.tiles_x);
     int pr = ty * 8 + (lane >> 3), pc = tx * 8 + (lane & 7);
@@ -1432,7 +991,7 @@ __global__ __launch_bounds__(64, MINW) void render_kernel(KParams p) {
         float l = (float)j + 0.5f * (float)sl;
         f3 point = add(add(p.C, scale(p.u, k)), scale(p.v, l));
         f3 dir = normalize(sub(p.pos, point));
-        col sc = trace_path<ACCEL, COUNT>(p, valid, point, dir, 1.0f, stk, w, wc, t);
+        col sc = trace_path<ACCEL, COUNT, POL>(p, valid, point, dir, 1.0f, stk, w, wc, t, T);
         acc = color_add(acc, color_mul(sc, 0.25f));
       }
     }
@@ -1472,34 +1031,39 @@ __global__ __launch_bounds__(256) void assemble_kernel(const float* __restrict__
 }  // namespace rt
 
 // ---------------------------------------------------------------- launchers
-#ifndef RT_DEFAULT_MIN_WAVES
-#define RT_DEFAULT_MIN_WAVES 4
-#endif
-
-template <int ACCEL, bool COUNT>
-static void launch_render(const KParams* p, int min_waves, dim3 g, dim3 b, hipStream_t stream) {
-  switch (min_waves) {
-    case 2: hipLaunchKernelGGL((rt::render_kernel<ACCEL, COUNT, 2>), g, b, 0, stream, *p); break;
-    case 5: hipLaunchKernelGGL((rt::render_kernel<ACCEL, COUNT, 5>), g, b, 0, stream, *p); break;
-    case 3: hipLaunchKernelGGL((rt::render_kernel<ACCEL, COUNT, 3>), g, b, 0, stream, *p); break;
-    default: hipLaunchKernelGGL((rt::render_kernel<ACCEL, COUNT, 4>), g, b, 0, stream, *p); break;
-  }
-}
-
-extern "C" hipError_t rt_launch_render(const KParams* p, int accel, int count_work, int min_waves,
+// One instantiation per (accel, work counting, policy); the default policy's
+// kernel has no policy switch inside.  The work-counting pass and the test
+// policies are separate kernels, so they cannot slow the default one down.
+extern "C" hipError_t rt_launch_render(const KParams* p, int accel, int count_work, int policy,
                                        int grid, hipStream_t stream) {
   dim3 g(grid), b(64);
-  if (min_waves == 0) min_waves = RT_DEFAULT_MIN_WAVES;
   if (accel == RT_ACCEL_FLAT_D) {
     if (count_work)
-      launch_render<RT_ACCEL_FLAT_D, true>(p, min_waves, g, b, stream);
+      hipLaunchKernelGGL((rt::render_kernel<RT_ACCEL_FLAT_D, true, 0>), g, b, 0, stream, *p);
     else
-      launch_render<RT_ACCEL_FLAT_D, false>(p, min_waves, g, b, stream);
-  } else {
-    if (count_work)
-      launch_render<RT_ACCEL_OCTREE_D, true>(p, min_waves, g, b, stream);
-    else
-      launch_render<RT_ACCEL_OCTREE_D, false>(p, min_waves, g, b, stream);
+      hipLaunchKernelGGL((rt::render_kernel<RT_ACCEL_FLAT_D, false, 0>), g, b, 0, stream, *p);
+    return hipGetLastError();
+  }
+  switch (policy) {
+    case RT_POLICY_LANE:
+      hipLaunchKernelGGL((rt::render_kernel<RT_ACCEL_OCTREE_D, false, RT_POLICY_LANE>), g, b, 0,
+                         stream, *p);
+      break;
+    case RT_POLICY_STAGED:
+      hipLaunchKernelGGL((rt::render_kernel<RT_ACCEL_OCTREE_D, false, RT_POLICY_STAGED>), g, b, 0,
+                         stream, *p);
+      break;
+    case RT_POLICY_DIR_STAGED:
+      hipLaunchKernelGGL((rt::render_kernel<RT_ACCEL_OCTREE_D, false, RT_POLICY_DIR_STAGED>), g, b,
+                         0, stream, *p);
+      break;
+    default:
+      if (count_work)
+        hipLaunchKernelGGL((rt::render_kernel<RT_ACCEL_OCTREE_D, true, RT_POLICY_DEFAULT>), g, b, 0,
+                           stream, *p);
+      else
+        hipLaunchKernelGGL((rt::render_kernel<RT_ACCEL_OCTREE_D, false, RT_POLICY_DEFAULT>), g, b, 0,
+                           stream, *p);
   }
   return hipGetLastError();
 }

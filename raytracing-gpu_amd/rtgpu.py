@@ -138,6 +138,7 @@ _PROTOS = [
     ("rt_hip_set_count_work", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_set_cull_slack", C.c_int, [C.c_void_p, C.c_float]),
     ("rt_hip_set_exact_camera", C.c_int, [C.c_void_p, C.c_int]),
+    ("rt_hip_set_policy", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_set_camera_bound_scale", C.c_int, [C.c_void_p, C.c_double]),
     ("rt_cand_survey", C.c_int, [C.POINTER(SceneStruct), C.c_float, C.c_double, C.c_int, C.c_int,
                                  C.POINTER(C.c_ulonglong)]),
@@ -365,6 +366,11 @@ class Context:
 
     def set_exact_camera(self, on=True):
         _check(lib().rt_hip_set_exact_camera(self.h, 1 if on else 0), "exact_camera")
+
+    def set_policy(self, policy):
+        """Octree traversal policy (rt_hip_set_policy): 0 default, 1 per-lane,
+        2 staged packet, 3 default + staged directional shadows."""
+        _check(lib().rt_hip_set_policy(self.h, int(policy)), "policy")
 
     def set_camera_bound_scale(self, scale):
         _check(lib().rt_hip_set_camera_bound_scale(self.h, float(scale)), "bound_scale")

@@ -212,40 +212,40 @@ def test_synthetic_c5_exact_on_sampled_tiles(gpu):
     assert_bitexact(img[pix[:, 0], pix[:, 1]], vals, "C5 sample vs oracle")
 
 
-# Traversal policies of the octree walk (env RT_TRAV / RT_TRAV_SHADOW for
-# closest-hit / shadow queries, read per render; see csrc/rt_render.hip):
-# per-lane, packet, hybrid, staged packet, staged hybrid.  The defaults
-# (staged hybrid closest-hit, per-lane shadow) run in every other test.
-TRAV = [0, 1, 2, 3, 4]
+# Traversal policies of the octree walk (rt_hip_set_policy, one kernel each;
+# csrc/rt_render.hip): default (staged packet closest hit for coherent
+# queries, per-lane otherwise), all per-lane, all staged packet, default +
+# staged directional-light shadows.  The default runs in every other test.
+TRAV = [0, 1, 2, 3]
 TRAV_SCENES = ["cube", "car-on-road", "dark-night", "island_smooth", "spheres", "susans_smooth",
                "lighthouse", "point-light"]
 
 
 @pytest.mark.parametrize("trav", TRAV)
-def test_traversal_policies_bitexact(gpu, scene_dir, manifest, trav, monkeypatch):
+def test_traversal_policies_bitexact(gpu, scene_dir, manifest, trav):
     """Every traversal policy reproduces the reference goldens bit for bit."""
-    monkeypatch.setenv("RT_TRAV", str(trav))
-    monkeypatch.setenv("RT_TRAV_SHADOW", str(trav))  # the policy for shadow queries too
     for case in manifest:
         if case["scene"] not in TRAV_SCENES or case["width"] != 96:
             continue
         s = gpu.Scene.load_svati(os.path.join(scene_dir, case["scene"] + ".svati"))
         s.set_size(case["width"], case["height"])
-        img, st = gpu.Context(s, "octree").render_image(s.frame())
+        ctx = gpu.Context(s, "octree")
+        ctx.set_policy(trav)
+        img, st = ctx.render_image(s.frame())
         assert_bitexact(img, golden_image(case), f"{case_id(case)} trav {trav}")
         assert st["closest"] == case["closest"] and st["shadow"] == case["shadow"]
 
 
 @pytest.mark.parametrize("trav", TRAV)
-def test_traversal_policies_full_frame(gpu, scene_dir, trav, monkeypatch):
+def test_traversal_policies_full_frame(gpu, scene_dir, trav):
     """Whole 1080p frame of the densest reference scene: octree walk == brute force."""
     s = gpu.Scene.load_svati(os.path.join(scene_dir, "car-on-road.svati"))
     s.set_size(1920, 1080)
     f = s.frame()
     img_f, _ = gpu.Context(s, "flat").render_image(f)
-    monkeypatch.setenv("RT_TRAV", str(trav))
-    monkeypatch.setenv("RT_TRAV_SHADOW", str(trav))  # the policy for shadow queries too
-    img_o, _ = gpu.Context(s, "octree").render_image(f)
+    ctx = gpu.Context(s, "octree")
+    ctx.set_policy(trav)
+    img_o, _ = ctx.render_image(f)
     assert_bitexact(img_o, img_f, f"car-on-road 1080p trav {trav}")
 
 

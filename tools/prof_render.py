@@ -25,12 +25,14 @@ def main():
     ap.add_argument("--n", type=int, default=3)
     ap.add_argument("--exact", type=int, default=1)
     ap.add_argument("--scale", type=float, default=1.0)
+    ap.add_argument("--policy", type=int, default=0)
     a = ap.parse_args()
     s = rtgpu.Scene.synthetic(a.grid, a.grid, a.tris, seed=0x5EED, width=a.W, height=a.H)
     f = s.frame()
     ctx = rtgpu.Context(s, a.accel)
     ctx.set_exact_camera(bool(a.exact))
     ctx.set_camera_bound_scale(a.scale)
+    ctx.set_policy(a.policy)
     d = C.c_void_p()
     assert rtgpu.lib().rt_hip_malloc(0, rtgpu.tile_buffer_floats(a.W, a.H, 1) * 4, C.byref(d)) == 0
     for i in range(a.n):
