@@ -63,6 +63,12 @@ typedef struct rt_stats {
    * octree slack cannot guarantee, their tile-list entries (each tested by
    * the 64 pixels x 4 samples of the tile), and those every camera ray tests */
   unsigned long long cand_prims, cand_entries, cand_global;
+  /* per-lane work of the instrumented pass (rt_hip_set_count_work): node
+   * visits and triangle tests summed over the lanes that made them (a record
+   * tested by k lanes of a wave counts k times; node_visits / tri_tests count
+   * it once), for closest-hit and for shadow queries */
+  unsigned long long closest_node_lanes, closest_tri_lanes;
+  unsigned long long shadow_node_lanes, shadow_tri_lanes;
 } rt_stats;
 
 /* Sizes of the device-side scene image, for the roofline accounting. */
@@ -131,6 +137,12 @@ int rt_hip_stats(rt_hip_ctx *ctx, rt_stats *out);
  * culling").  Default RT_EPS_ULPS_DEFAULT (64).  Tuning knob: smaller is
  * faster and risks parity on grazing rays. */
 int rt_hip_set_cull_slack(rt_hip_ctx *ctx, float ulps);
+/* Phase timing: with enable, every rt_hip_render records HIP events on its
+ * stream before the camera candidate lists, before the render kernel and
+ * after it; rt_hip_last_times waits for the last one and returns the two
+ * spans in milliseconds (lists_ms = 0 without lists). */
+int rt_hip_set_timing(rt_hip_ctx *ctx, int enable);
+int rt_hip_last_times(rt_hip_ctx *ctx, float *lists_ms, float *render_ms);
 /* Instrumented build: also count node visits and triangle tests (slower). */
 int rt_hip_set_count_work(rt_hip_ctx *ctx, int enable);
 /* Exact camera rays (default 1): per-frame candidate lists of the triangles

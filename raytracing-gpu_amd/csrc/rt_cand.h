@@ -12,6 +12,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+namespace rtc {
+struct Footprint;
+}
+
 struct CandParams {
   const float4* tri;      // prim-order triangle records (3 float4 each)
   const float4* node;     // octree nodes (2 float4 each: box + words), may be NULL
@@ -32,29 +36,37 @@ struct CandParams {
   double c_dot, c_a;      // error-bound constants (tools/mt_bound.py C_DOT, C_A)
   double kmin, kmax, lmin, lmax_;  // sample coordinates of the frame
   int W, H, tiles_x, tiles_y, rank, nranks, ntiles_local;
-  uint32_t* visits;       // nprim + 1: tile entries of each prim (pass 1)
+  uint32_t* list;         // nprim: prims the float fast path cannot prove safe (pass 0)
+  rtc::Footprint* fp;     // nprim: footprint of list entry j (pass 1, read by passes 2 and big)
+  uint32_t* visits;       // nprim + 1: pass 0 flags, then tile entries of list entry j (pass 1)
   const uint32_t* off;    // nprim + 1: exclusive scan of visits
   uint32_t* keys;         // entries: local tile index (pass 2)
   uint32_t* vals;         // entries: prim
   uint32_t* global;       // nprim: prims whose footprint is unbounded
-  uint32_t* ctr;          // [1] global prims, [2] big footprints
-  uint32_t* big;          // nprim: prims with more than kBig entries
+  uint32_t* ctr;          // [1] global prims, [2] big footprints, [3] list length
+  uint32_t* big;          // nprim: list entries with more than kBig tile entries
   float* skip;            // nprim: depth-skip bound of each listed prim
 };
 
 // Host mirror for surveys (same classify/raster code): safe / footprint /
 // global triangle counts, tile entries of this rank, and a log2 histogram of
-// entries per footprint triangle.
-extern "C" void rt_cand_survey_host(const CandParams* p, const float* tri, const float* node,
-                                    const uint32_t* prim_leaf, int threads,
-                                    unsigned long long out[36]);
+// entries per footprint triangle.  Returns -1 when the per-row tile count of
+// the device count pass disagrees with the tiles the raster emits.
+extern "C" int rt_cand_survey_host(const CandParams* p, const float* tri, const float* node,
+                                   const uint32_t* prim_leaf, int threads,
+                                   unsigned long long out[36]);
 // prim_leaf[prim] = a leaf node holding a record of prim (scene build time)
 extern "C" hipError_t rt_cand_prim_leaf(const float4* node, uint32_t nnode, const float4* tri,
                                         uint32_t* prim_leaf, hipStream_t s);
 
-// pass 1 (per-prim tile counts) -> exclusive scan -> pass 2 ((tile, prim)
-// pairs at the prims' offsets) -> radix sort by tile -> per-tile offsets
+// pass 0 (float fast path flags) -> scan -> scatter (compact list of the
+// rest) -> pass 1 (their footprints and tile counts) -> exclusive scan ->
+// pass 2 ((tile, prim) pairs at the offsets) -> radix sort by tile ->
+// per-tile offsets
+extern "C" hipError_t rt_cand_quick(const CandParams* p, hipStream_t s);
+extern "C" hipError_t rt_cand_scatter(const CandParams* p, hipStream_t s);
 extern "C" hipError_t rt_cand_count(const CandParams* p, hipStream_t s);
+extern "C" size_t rt_cand_footprint_bytes(void);
 extern "C" hipError_t rt_cand_emit(const CandParams* p, hipStream_t s);
 extern "C" hipError_t rt_cand_big(const CandParams* p, uint32_t nbig, hipStream_t s);
 extern "C" hipError_t rt_cand_scan(const uint32_t* in, uint32_t* out, uint32_t n, void* temp,
@@ -62,5 +74,8 @@ extern "C" hipError_t rt_cand_scan(const uint32_t* in, uint32_t* out, uint32_t n
 extern "C" hipError_t rt_cand_sort(uint32_t* keys_in, uint32_t* keys_out, uint32_t* vals_in,
                                    uint32_t* vals_out, uint32_t n, int bits, void* temp,
                                    size_t* temp_bytes, hipStream_t s);
+// out[i] = skip[cand[i]]: the sorted lists' per-entry depth-skip bounds
+extern "C" hipError_t rt_cand_entry_skip(const uint32_t* cand, const float* skip, float* out,
+                                         uint32_t n, hipStream_t s);
 extern "C" hipError_t rt_cand_bounds(const uint32_t* keys, uint32_t n, uint32_t* start,
                                      uint32_t ntiles, hipStream_t s);

@@ -370,20 +370,23 @@ __host__ __device__ inline bool raster_rows(const CandParams& p, const Footprint
     const double lmn = fmin(fp.l[0], fmin(fp.l[1], fp.l[2])) - fp.dimg;
     const double lmx = fmax(fp.l[0], fmax(fp.l[1], fp.l[2])) + fp.dimg;
     if (!(lmx >= p.lmin && lmn <= p.lmax_)) return false;
-    r0 = (int)fmax(0.0, ceil(hh - lmx));
-    r1 = (int)fmin((double)(p.H - 1), floor(hh - lmn + 0.5));
+    // clamped in double before the conversion (a far-off footprint gives
+    // values beyond int range, whose conversion the host does not saturate)
+    r0 = (int)fmin(fmax(0.0, ceil(hh - lmx)), (double)p.H);
+    r1 = (int)fmax(fmin((double)(p.H - 1), floor(hh - lmn + 0.5)), -1.0);
   }
   return r0 <= r1;
 }
 
-// The footprint's tiles in tile row ty (rows clipped to [r0, r1]).
-template <class F>
-__host__ __device__ void raster_row(const CandParams& p, const Footprint& fp, int ty, int r0, int r1,
-                                    F emit) {
+// The footprint's tiles in tile row ty (rows clipped to [r0, r1]): tile
+// columns [a0, a1] and [b0, b1] (empty when a0 > a1; the second range only
+// counts where it leaves the first).
+__host__ __device__ inline void row_tiles(const CandParams& p, const Footprint& fp, int ty, int r0,
+                                          int r1, int& a0, int& a1, int& b0, int& b1) {
   const double hw_ = (double)(p.W / 2), hh = (double)(p.H / 2);
   auto cols = [&](double a, double b, int& c0, int& c1) {  // k in [a, b] -> columns
-    c0 = (int)fmax(0.0, ceil(hw_ - b));
-    c1 = (int)fmin((double)(p.W - 1), floor(hw_ - a + 0.5));
+    c0 = (int)fmin(fmax(0.0, ceil(hw_ - b)), (double)p.W);  // clamped before the conversion
+    c1 = (int)fmax(fmin((double)(p.W - 1), floor(hw_ - a + 0.5)), -1.0);
   };
   // k-range of a band |b0 + b1 k + b2 l| <= hw for some l in [la, lb]
   auto band = [&](double hw, double la, double lb, double& a, double& b) {
@@ -404,10 +407,6 @@ __host__ __device__ void raster_row(const CandParams& p, const Footprint& fp, in
       a = hi / fp.b1;
       b = lo / fp.b1;
     }
-  };
-  auto put = [&](int tx) {
-    const uint32_t g = (uint32_t)ty * (uint32_t)p.tiles_x + (uint32_t)tx;
-    if ((int)(g % (uint32_t)p.nranks) == p.rank) emit(g / (uint32_t)p.nranks);
   };
   const int ra = ty * 8 > r0 ? ty * 8 : r0, rb = ty * 8 + 7 < r1 ? ty * 8 + 7 : r1;
   const double la = hh - rb, lb = hh - ra + 0.5;  // l-range of the strip's samples
@@ -445,9 +444,46 @@ __host__ __device__ void raster_row(const CandParams& p, const Footprint& fp, in
     band(fp.hw0, la, lb, ba, bb);
     if (ba <= bb) cols(fmax(ba, p.kmin - 1.0), fmin(bb, p.kmax + 1.0), d0, d1);
   }
-  for (int tx = c0 >> 3; c0 <= c1 && tx <= (c1 >> 3); tx++) put(tx);
-  for (int tx = d0 >> 3; d0 <= d1 && tx <= (d1 >> 3); tx++)
-    if (!(c0 <= c1 && tx >= (c0 >> 3) && tx <= (c1 >> 3))) put(tx);
+  a0 = c0 <= c1 ? c0 >> 3 : 1;
+  a1 = c0 <= c1 ? c1 >> 3 : 0;
+  b0 = d0 <= d1 ? d0 >> 3 : 1;
+  b1 = d0 <= d1 ? d1 >> 3 : 0;
+}
+
+// The footprint's tiles of this rank in tile row ty, in column order.
+template <class F>
+__host__ __device__ void raster_row(const CandParams& p, const Footprint& fp, int ty, int r0, int r1,
+                                    F emit) {
+  int a0, a1, b0, b1;
+  row_tiles(p, fp, ty, r0, r1, a0, a1, b0, b1);
+  auto put = [&](int tx) {
+    const uint32_t g = (uint32_t)ty * (uint32_t)p.tiles_x + (uint32_t)tx;
+    if ((int)(g % (uint32_t)p.nranks) == p.rank) emit(g / (uint32_t)p.nranks);
+  };
+  for (int tx = a0; tx <= a1; tx++) put(tx);
+  for (int tx = b0; tx <= b1; tx++)
+    if (!(tx >= a0 && tx <= a1)) put(tx);
+}
+
+// Tiles g in [lo, hi] (global indices) with g % n == r.
+__host__ __device__ inline uint32_t rank_tiles(uint32_t lo, uint32_t hi, uint32_t n, uint32_t r) {
+  // tiles g = r + m n with g in [lo, hi]: m in [ceil((lo - r) / n), floor((hi - r) / n)]
+  const long long mlo = lo <= r ? 0 : ((long long)lo - r + n - 1) / n;
+  const long long mhi = hi < r ? -1 : ((long long)hi - r) / n;
+  return mhi >= mlo ? (uint32_t)(mhi - mlo + 1) : 0u;
+}
+
+// Number of tiles raster_row emits for row ty, without visiting them.
+__host__ __device__ inline uint32_t count_row(const CandParams& p, const Footprint& fp, int ty, int r0,
+                                              int r1) {
+  int a0, a1, b0, b1;
+  row_tiles(p, fp, ty, r0, r1, a0, a1, b0, b1);
+  const uint32_t base = (uint32_t)ty * (uint32_t)p.tiles_x, n = (uint32_t)p.nranks,
+                 r = (uint32_t)p.rank;
+  auto cnt = [&](int x0, int x1) { return x0 <= x1 ? rank_tiles(base + x0, base + x1, n, r) : 0u; };
+  uint32_t c = cnt(a0, a1) + cnt(b0, b1);
+  if (a0 <= a1 && b0 <= b1) c -= cnt(a0 > b0 ? a0 : b0, a1 < b1 ? a1 : b1);  // overlap counted once
+  return c;
 }
 
 // Tiles of this rank whose camera samples can be candidates for the
@@ -461,43 +497,71 @@ __host__ __device__ void raster(const CandParams& p, const Footprint& fp, F emit
   for (int ty = r0 >> 3; ty <= (r1 >> 3); ty++) raster_row(p, fp, ty, r0, r1, emit);
 }
 
+// The number of tiles raster() emits, one step per tile row.
+__host__ __device__ inline uint32_t raster_count(const CandParams& p, const Footprint& fp) {
+  int r0, r1;
+  if (!raster_rows(p, fp, r0, r1)) return 0;
+  uint32_t n = 0;
+  for (int ty = r0 >> 3; ty <= (r1 >> 3); ty++) n += count_row(p, fp, ty, r0, r1);
+  return n;
+}
+
 // footprints with more entries than this are emitted by a whole workgroup
 constexpr uint32_t kBig = 512;
 
-// Pass 1: classify (float fast path first), count each prim's tiles.
-__global__ __launch_bounds__(256) void count_kernel(CandParams p) {
+// Pass 0: the float fast path over every prim; flags the prims it cannot
+// prove safe (visits[prim] = 1), which an exclusive scan and scatter_kernel
+// turn into a compact list, so the f64 classification of pass 1 runs on full
+// waves instead of on the scattered third of the lanes of every wave.
+__global__ __launch_bounds__(256) void quick_kernel(CandParams p) {
   const uint32_t prim = blockIdx.x * blockDim.x + threadIdx.x;
   if (prim >= p.nprim) return;
+  p.visits[prim] = quick_safe(p, (const float*)(p.tri + 3 * (size_t)prim)) ? 0u : 1u;
+}
+
+__global__ __launch_bounds__(256) void scatter_kernel(CandParams p) {
+  const uint32_t prim = blockIdx.x * blockDim.x + threadIdx.x;
+  if (prim > p.nprim) return;
+  if (prim == p.nprim) {
+    p.ctr[3] = p.off[prim];  // list length
+    return;
+  }
+  if (p.visits[prim]) p.list[p.off[prim]] = prim;
+}
+
+// Pass 1: classify the listed prims, keep each one's footprint and count its
+// tiles (visits[j] for list entry j; visits is zero beyond the list).
+__global__ __launch_bounds__(256) void count_kernel(CandParams p) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= p.ctr[3]) return;
+  const uint32_t prim = p.list[j];
   const float* rec = (const float*)(p.tri + 3 * (size_t)prim);
   uint32_t visits = 0;
-  if (!quick_safe(p, rec)) {
-    Footprint fp;
-    const float* lb = p.prim_leaf ? (const float*)(p.node + 2 * (size_t)p.prim_leaf[prim]) : nullptr;
-    const int c = classify(p, rec, lb, fp);
-    if (c == GLOBAL) {
-      p.global[atomicAdd(p.ctr + 1, 1u)] = prim;
-      p.skip[prim] = -1e30f;
-    } else if (c == FOOTPRINT) {
-      raster(p, fp, [&](uint32_t) { visits++; });
-      p.skip[prim] = fp.skip;
-      if (visits > kBig) p.big[atomicAdd(p.ctr + 2, 1u)] = prim;
-    }
+  Footprint fp;
+  const float* lb = p.prim_leaf ? (const float*)(p.node + 2 * (size_t)p.prim_leaf[prim]) : nullptr;
+  const int c = classify(p, rec, lb, fp);
+  if (c == GLOBAL) {
+    p.global[atomicAdd(p.ctr + 1, 1u)] = prim;
+    p.skip[prim] = -1e30f;
+  } else if (c == FOOTPRINT) {
+    visits = raster_count(p, fp);
+    p.skip[prim] = fp.skip;
+    if (visits) p.fp[j] = fp;
+    if (visits > kBig) p.big[atomicAdd(p.ctr + 2, 1u)] = j;
   }
-  p.visits[prim] = visits;
+  p.visits[j] = visits;
 }
 
 // Pass 2 (after the scan of visits): the listed prims write their (tile,
 // prim) pairs at their offsets.
 __global__ __launch_bounds__(256) void emit_kernel(CandParams p) {
-  const uint32_t prim = blockIdx.x * blockDim.x + threadIdx.x;
-  if (prim >= p.nprim) return;
-  uint32_t o = p.off[prim];
-  const uint32_t n = p.off[prim + 1] - o;
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= p.ctr[3]) return;
+  uint32_t o = p.off[j];
+  const uint32_t n = p.off[j + 1] - o;
   if (n == 0 || n > kBig) return;  // big footprints: big_kernel
-  Footprint fp;
-  const float* lb = p.prim_leaf ? (const float*)(p.node + 2 * (size_t)p.prim_leaf[prim]) : nullptr;
-  if (classify(p, (const float*)(p.tri + 3 * (size_t)prim), lb, fp) != FOOTPRINT)
-    return;  // same answer as pass 1
+  const uint32_t prim = p.list[j];
+  const Footprint fp = p.fp[j];
   raster(p, fp, [&](uint32_t t) {
     p.keys[o] = t;
     p.vals[o] = prim;
@@ -508,16 +572,14 @@ __global__ __launch_bounds__(256) void emit_kernel(CandParams p) {
 // One workgroup per big footprint: its tile rows are spread over the
 // threads, a block scan places each thread's entries.
 __global__ __launch_bounds__(256) void big_kernel(CandParams p) {
-  const uint32_t prim = p.big[blockIdx.x];
-  Footprint fp;
-  const float* lb = p.prim_leaf ? (const float*)(p.node + 2 * (size_t)p.prim_leaf[prim]) : nullptr;
-  const bool ok = classify(p, (const float*)(p.tri + 3 * (size_t)prim), lb, fp) == FOOTPRINT;
+  const uint32_t j = p.big[blockIdx.x], prim = p.list[j];
+  const Footprint fp = p.fp[j];
   int r0 = 0, r1 = -1;
-  const bool rows = ok && raster_rows(p, fp, r0, r1);
+  const bool rows = raster_rows(p, fp, r0, r1);
   const int ty0 = r0 >> 3, ty1 = r1 >> 3, tid = threadIdx.x;
   uint32_t cnt = 0;
   if (rows)
-    for (int ty = ty0 + tid; ty <= ty1; ty += 256) raster_row(p, fp, ty, r0, r1, [&](uint32_t) { cnt++; });
+    for (int ty = ty0 + tid; ty <= ty1; ty += 256) cnt += count_row(p, fp, ty, r0, r1);
   __shared__ uint32_t sh[256];
   sh[tid] = cnt;
   __syncthreads();
@@ -527,7 +589,7 @@ __global__ __launch_bounds__(256) void big_kernel(CandParams p) {
     sh[tid] += y;
     __syncthreads();
   }
-  uint32_t o = p.off[prim] + sh[tid] - cnt;
+  uint32_t o = p.off[j] + sh[tid] - cnt;
   if (rows)
     for (int ty = ty0 + tid; ty <= ty1; ty += 256)
       raster_row(p, fp, ty, r0, r1, [&](uint32_t t) {
@@ -563,6 +625,14 @@ __global__ __launch_bounds__(256) void bounds_kernel(const uint32_t* keys, uint3
   start[t] = t == ntiles ? n : lo;
 }
 
+// per list entry: the depth-skip bound of its prim (coalesced for the render
+// kernel, which would otherwise gather it right after loading the entry)
+__global__ __launch_bounds__(256) void entry_skip_kernel(const uint32_t* cand, const float* skip,
+                                                         float* out, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = skip[cand[i]];
+}
+
 }  // namespace rtc
 
 #include <thread>
@@ -576,16 +646,17 @@ extern "C" hipError_t rt_cand_prim_leaf(const float4* node, uint32_t nnode, cons
   return hipGetLastError();
 }
 
-extern "C" void rt_cand_survey_host(const CandParams* p, const float* tri, const float* node,
-                                    const uint32_t* prim_leaf, int threads,
-                                    unsigned long long out[36]) {
+extern "C" int rt_cand_survey_host(const CandParams* p, const float* tri, const float* node,
+                                   const uint32_t* prim_leaf, int threads,
+                                   unsigned long long out[36]) {
   // out: [0] safe, [1] footprint, [2] global, [3] entries, [4 + k] prims
   // with 2^k <= entries < 2^(k+1), [20 + k] their entries (k < 16)
   if (threads < 1) threads = 1;
   std::vector<unsigned long long> part(36 * (size_t)threads, 0);
+  std::vector<unsigned long long> bad((size_t)threads, 0);
   std::vector<std::thread> th;
   for (int t = 0; t < threads; t++)
-    th.emplace_back([=, &part]() {
+    th.emplace_back([=, &part, &bad]() {
       unsigned long long* o = &part[36 * (size_t)t];
       for (uint32_t i = (uint32_t)t; i < p->nprim; i += (uint32_t)threads) {
         rtc::Footprint fp;
@@ -595,6 +666,22 @@ extern "C" void rt_cand_survey_host(const CandParams* p, const float* tri, const
         if (c == rtc::FOOTPRINT) {
           unsigned long long v = 0;
           rtc::raster(*p, fp, [&](uint32_t) { v++; });
+          if (v != rtc::raster_count(*p, fp)) {
+            bad[t]++;  // the device count pass must agree
+#ifdef RT_SURVEY_DEBUG
+            int r0, r1;
+            rtc::raster_rows(*p, fp, r0, r1);
+            for (int ty = r0 >> 3; ty <= (r1 >> 3); ty++) {
+              unsigned long long vr = 0;
+              rtc::raster_row(*p, fp, ty, r0, r1, [&](uint32_t) { vr++; });
+              int a0, a1, b0, b1;
+              rtc::row_tiles(*p, fp, ty, r0, r1, a0, a1, b0, b1);
+              if (vr != rtc::count_row(*p, fp, ty, r0, r1))
+                fprintf(stderr, "prim %u ty %d iter %llu count %u a %d..%d b %d..%d\n", i, ty, vr,
+                        rtc::count_row(*p, fp, ty, r0, r1), a0, a1, b0, b1);
+            }
+#endif
+          }
           o[3] += v;
           int k = 0;
           while (k < 15 && (2ull << k) <= v) k++;
@@ -610,10 +697,27 @@ extern "C" void rt_cand_survey_host(const CandParams* p, const float* tri, const
     out[k] = 0;
     for (int t = 0; t < threads; t++) out[k] += part[36 * (size_t)t + k];
   }
+  unsigned long long nbad = 0;
+  for (int t = 0; t < threads; t++) nbad += bad[t];
+  return nbad ? -1 : 0;
+}
+
+extern "C" size_t rt_cand_footprint_bytes(void) { return sizeof(rtc::Footprint); }
+
+extern "C" hipError_t rt_cand_quick(const CandParams* p, hipStream_t s) {
+  if (p->nprim == 0) return hipSuccess;
+  hipLaunchKernelGGL(rtc::quick_kernel, dim3((p->nprim + 255) / 256), dim3(256), 0, s, *p);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t rt_cand_scatter(const CandParams* p, hipStream_t s) {
+  hipLaunchKernelGGL(rtc::scatter_kernel, dim3((p->nprim + 1 + 255) / 256), dim3(256), 0, s, *p);
+  return hipGetLastError();
 }
 
 extern "C" hipError_t rt_cand_count(const CandParams* p, hipStream_t s) {
   if (p->nprim == 0) return hipSuccess;
+  // sized for the worst case; threads beyond the list's length exit at once
   hipLaunchKernelGGL(rtc::count_kernel, dim3((p->nprim + 255) / 256), dim3(256), 0, s, *p);
   return hipGetLastError();
 }
@@ -641,6 +745,14 @@ extern "C" hipError_t rt_cand_sort(uint32_t* keys_in, uint32_t* keys_out, uint32
                                    size_t* temp_bytes, hipStream_t s) {
   return rocprim::radix_sort_pairs(temp, *temp_bytes, keys_in, keys_out, vals_in, vals_out,
                                    (size_t)n, 0, bits, s);
+}
+
+extern "C" hipError_t rt_cand_entry_skip(const uint32_t* cand, const float* skip, float* out,
+                                         uint32_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(rtc::entry_skip_kernel, dim3((n + 255) / 256), dim3(256), 0, s, cand, skip,
+                     out, n);
+  return hipGetLastError();
 }
 
 extern "C" hipError_t rt_cand_bounds(const uint32_t* keys, uint32_t n, uint32_t* start,

@@ -61,6 +61,8 @@ struct rt_hip_ctx {
   double bound_scale = 1.0;  // 1 = the proven float-MT error bound (tools/mt_bound.py)
   float4* d_tri_prim = nullptr;  // prim-order records (== d_tri for FLAT)
   uint32_t nprim = 0;
+  uint32_t* d_cand_list = nullptr;    // nprim
+  void* d_cand_fp = nullptr;          // nprim footprints (rt_cand_footprint_bytes each)
   uint32_t* d_cand_visits = nullptr;  // nprim + 1
   uint32_t* d_cand_off = nullptr;     // nprim + 1
   uint32_t* d_cand_start = nullptr;   // ntiles + 1
@@ -78,6 +80,11 @@ struct rt_hip_ctx {
   size_t scan_tmp_bytes = 0;
   uint32_t* h_cand = nullptr;  // pinned: total entries, risky, global, visits
   unsigned long long cand_prims = 0, cand_entries = 0, cand_global = 0;
+  // phase timing (rt_hip_set_timing): events before the candidate lists,
+  // before the render kernel and after it, on the render's stream
+  int timing = 0;
+  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  int ev_valid = 0;
 };
 
 static int cand_params(const rt_frame* f, const float scene_c[3], float scene_r, float eps_ulps,
@@ -129,6 +136,8 @@ extern "C" void rt_hip_destroy(rt_hip_ctx* c) {
   (void)hipFree(c->d_spill);
   (void)hipFree(c->d_terms);
   if (c->d_tri_prim != c->d_tri) (void)hipFree(c->d_tri_prim);
+  (void)hipFree(c->d_cand_list);
+  (void)hipFree(c->d_cand_fp);
   (void)hipFree(c->d_cand_visits);
   (void)hipFree(c->d_cand_off);
   (void)hipFree(c->d_cand_start);
@@ -143,6 +152,8 @@ extern "C" void rt_hip_destroy(rt_hip_ctx* c) {
   (void)hipFree(c->d_cand);
   (void)hipFree(c->d_scan_tmp);
   if (c->h_cand) (void)hipHostFree(c->h_cand);
+  for (hipEvent_t e : c->ev)
+    if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -361,12 +372,33 @@ extern "C" int rt_cand_survey(const rt_scene* scene, float eps_ulps, double boun
   }
   if (!rc) {
     cp.nprim = (uint32_t)fs.ntri;
-    rt_cand_survey_host(&cp, fs.tri, use_leaves ? ft.node : nullptr,
-                        use_leaves ? pl.data() : nullptr, threads, out);
+    if (rt_cand_survey_host(&cp, fs.tri, use_leaves ? ft.node : nullptr,
+                            use_leaves ? pl.data() : nullptr, threads, out))
+      rc = rt_set_error(RT_EINVAL, "candidate survey: per-row tile count != rasterised tiles");
   }
   if (use_leaves) rt_flat_free(&ft);
   rt_flat_free(&fs);
   return rc;
+}
+
+extern "C" int rt_hip_set_timing(rt_hip_ctx* c, int enable) {
+  if (!c) return rt_set_error(RT_EINVAL, "null context");
+  HIP_TRY(hipSetDevice(c->device));
+  for (hipEvent_t& e : c->ev)
+    if (!e) HIP_TRY(hipEventCreate(&e));
+  c->timing = enable ? 1 : 0;
+  c->ev_valid = 0;
+  return RT_OK;
+}
+
+extern "C" int rt_hip_last_times(rt_hip_ctx* c, float* lists_ms, float* render_ms) {
+  if (!c || !lists_ms || !render_ms) return rt_set_error(RT_EINVAL, "null argument");
+  if (!c->ev_valid) return rt_set_error(RT_EINVAL, "no timed render (rt_hip_set_timing)");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipEventSynchronize(c->ev[2]));
+  HIP_TRY(hipEventElapsedTime(lists_ms, c->ev[0], c->ev[1]));
+  HIP_TRY(hipEventElapsedTime(render_ms, c->ev[1], c->ev[2]));
+  return RT_OK;
 }
 
 extern "C" int rt_hip_set_count_work(rt_hip_ctx* c, int enable) {
@@ -509,6 +541,8 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
   cp.node = c->d_node;
   cp.prim_leaf = c->d_prim_leaf;
   if (!c->d_cand_global) {
+    HIP_TRY(hipMalloc((void**)&c->d_cand_list, (np + 1) * sizeof(uint32_t)));
+    HIP_TRY(hipMalloc(&c->d_cand_fp, (np + 1) * rt_cand_footprint_bytes()));
     HIP_TRY(hipMalloc((void**)&c->d_cand_visits, (np + 1) * sizeof(uint32_t)));
     HIP_TRY(hipMalloc((void**)&c->d_cand_off, (np + 1) * sizeof(uint32_t)));
     HIP_TRY(hipMalloc((void**)&c->d_cand_global, (np + 1) * sizeof(uint32_t)));
@@ -523,6 +557,8 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
     if (rc) return rc;
     c->cand_tiles_cap = cap;
   }
+  cp.list = c->d_cand_list;
+  cp.fp = (rtc::Footprint*)c->d_cand_fp;
   cp.visits = c->d_cand_visits;
   cp.off = c->d_cand_off;
   cp.global = c->d_cand_global;
@@ -531,11 +567,18 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
   cp.skip = c->d_cand_skip;
   HIP_TRY(hipMemsetAsync(c->d_cand_visits + np, 0, sizeof(uint32_t), s));
   HIP_TRY(hipMemsetAsync(c->d_cand_ctr, 0, 4 * sizeof(uint32_t), s));
-  HIP_TRY(rt_cand_count(&cp, s));
   size_t tb = 0;
   HIP_TRY(rt_cand_scan(c->d_cand_visits, c->d_cand_off, (uint32_t)np, nullptr, &tb, s));
   rc = ensure_tmp(c, tb);
   if (rc) return rc;
+  // pass 0: flags -> compact list of the prims the float fast path leaves
+  HIP_TRY(rt_cand_quick(&cp, s));
+  tb = c->scan_tmp_bytes;
+  HIP_TRY(rt_cand_scan(c->d_cand_visits, c->d_cand_off, (uint32_t)np, c->d_scan_tmp, &tb, s));
+  HIP_TRY(rt_cand_scatter(&cp, s));
+  HIP_TRY(hipMemsetAsync(c->d_cand_visits, 0, (np + 1) * sizeof(uint32_t), s));
+  // pass 1: footprints and tile counts of the listed prims
+  HIP_TRY(rt_cand_count(&cp, s));
   tb = c->scan_tmp_bytes;
   HIP_TRY(rt_cand_scan(c->d_cand_visits, c->d_cand_off, (uint32_t)np, c->d_scan_tmp, &tb, s));
   HIP_TRY(hipMemcpyAsync(c->h_cand, c->d_cand_off + np, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
@@ -547,12 +590,14 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
       (void)hipFree(*b);
       *b = nullptr;
     }
+
     size_t cap = 0;
     rc = grow_dev(&c->d_cand_keys, &cap, total + 1);
     if (rc) return rc;
     c->cand_cap = cap;
     for (uint32_t** b : {&c->d_cand_vals, &c->d_cand_keys2, &c->d_cand})
       HIP_TRY(hipMalloc((void**)b, c->cand_cap * sizeof(uint32_t)));
+
   }
   cp.keys = c->d_cand_keys;
   cp.vals = c->d_cand_vals;
@@ -570,12 +615,15 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
     HIP_TRY(rt_cand_sort(c->d_cand_keys, c->d_cand_keys2, c->d_cand_vals, c->d_cand, total, bits,
                          c->d_scan_tmp, &tb, s));
   HIP_TRY(rt_cand_bounds(c->d_cand_keys2, total, c->d_cand_start, (uint32_t)nt, s));
+  // the sorted keys are spent: their buffer takes the per-entry skip bounds
+  float* entry_skip = (float*)c->d_cand_keys2;
+  HIP_TRY(rt_cand_entry_skip(c->d_cand, c->d_cand_skip, entry_skip, total, s));
   kp->cand_start = c->d_cand_start;
   kp->cand = c->d_cand;
   kp->cand_global = c->d_cand_global;
   kp->n_cand_global = nglobal;
   kp->tri_prim = c->d_tri_prim;
-  kp->cand_skip = c->d_cand_skip;
+  kp->cand_skip = entry_skip;
   c->cand_entries = total;
   c->cand_global = nglobal;
   c->cand_prims = 0;  // not counted separately (entries and globals are)
@@ -623,6 +671,8 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
   p.eps_rel = c->eps_ulps * 5.9604645e-8f;
   p.terms = c->d_terms;
   c->cand_prims = c->cand_entries = c->cand_global = 0;
+  c->ev_valid = 0;
+  if (c->timing) HIP_TRY(hipEventRecord(c->ev[0], s));
   if (c->accel == RT_ACCEL_OCTREE && c->d_node && c->exact_camera) {
     int rc = cand_prepare(c, f, &p, s);
     if (rc) return rc;
@@ -631,11 +681,17 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
     // empty scene: nothing to traverse, the FLAT kernel with 0 records is exact
     HIP_TRY(hipMemsetAsync(c->d_counter, 0, 64, s));
     HIP_TRY(hipMemsetAsync(c->d_stats, 0, RT_NSTATS * sizeof(unsigned long long), s));
+    if (c->timing) HIP_TRY(hipEventRecord(c->ev[1], s));
     HIP_TRY(rt_launch_render(&p, RT_ACCEL_FLAT_D, c->count_work, c->policy, c->grid, s));
   } else {
     HIP_TRY(hipMemsetAsync(c->d_counter, 0, 64, s));
     HIP_TRY(hipMemsetAsync(c->d_stats, 0, RT_NSTATS * sizeof(unsigned long long), s));
+    if (c->timing) HIP_TRY(hipEventRecord(c->ev[1], s));
     HIP_TRY(rt_launch_render(&p, c->accel, c->count_work, c->policy, c->grid, s));
+  }
+  if (c->timing) {
+    HIP_TRY(hipEventRecord(c->ev[2], s));
+    c->ev_valid = 1;
   }
   c->last_stream = s;
   return RT_OK;
@@ -658,6 +714,10 @@ extern "C" int rt_hip_stats(rt_hip_ctx* c, rt_stats* out) {
   out->depth_overflow = h[5];
   out->zero_normal = h[6];
   out->hits = h[7];
+  out->closest_node_lanes = h[8];
+  out->closest_tri_lanes = h[9];
+  out->shadow_node_lanes = h[10];
+  out->shadow_tri_lanes = h[11];
   out->cand_prims = c->cand_prims;
   out->cand_entries = c->cand_entries;
   out->cand_global = c->cand_global;
@@ -830,6 +890,10 @@ extern "C" int rt_raytrace_multi(const char* input, const char* output, int ngpu
     sum.cand_prims += st.cand_prims;
     sum.cand_entries += st.cand_entries;
     sum.cand_global += st.cand_global;
+    sum.closest_node_lanes += st.closest_node_lanes;
+    sum.closest_tri_lanes += st.closest_tri_lanes;
+    sum.shadow_node_lanes += st.shadow_node_lanes;
+    sum.shadow_tri_lanes += st.shadow_tri_lanes;
   }
   t1 = std::chrono::steady_clock::now();
   if (rc) goto out;

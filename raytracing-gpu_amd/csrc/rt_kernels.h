@@ -12,7 +12,7 @@
 #define RT_MAT_FLOATS_D 12
 #define RT_LIGHT_FLOATS_D 8
 #define RT_MAX_DEPTH 32
-#define RT_NSTATS 8
+#define RT_NSTATS 12
 // per-lane global overflow area of the traversal stack (entries beyond LDS)
 #define RT_SPILL_STACK 112
 // reflection terms of a path kept in LDS (deeper ones: KParams::terms)
@@ -30,6 +30,9 @@
 // widened to 64-bit by the final atomics)
 struct WorkCount {
   uint32_t closest, shadow, pixels, nodes, tris, overflow, zero_normal, hits;
+  // per-lane node visits / triangle tests of closest-hit and shadow queries
+  // (COUNT pass): a record tested by k lanes counts k times
+  uint32_t cl_nodes, cl_tris, sh_nodes, sh_tris;
 };
 
 struct KParams {
@@ -57,7 +60,7 @@ struct KParams {
   const uint32_t* cand_global;  // prims every camera ray tests
   uint32_t n_cand_global;
   const float4* tri_prim;       // prim-order triangle records
-  const float* cand_skip;       // per prim: lower bound of new_dist - |pos - o| (depth skip)
+  const float* cand_skip;       // per cand entry: lower bound of new_dist - |pos - o| (depth skip)
 };
 
 // policy = RT_POLICY_* (octree only)

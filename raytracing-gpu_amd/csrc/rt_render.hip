@@ -171,6 +171,7 @@ struct Stack {
 // WorkCount after the walk (absorb).
 struct LaneCount {
   uint32_t nodes, tris, overflow;
+  uint32_t lnodes, ltris;  // this lane's own visits / tests (COUNT pass)
 };
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
@@ -199,10 +200,18 @@ __device__ __forceinline__ uint32_t lanes_distinct(uint32_t key) {
 }
 
 template <bool COUNT>
-__device__ __forceinline__ void absorb(WorkCount& wc, const LaneCount& lc) {
+__device__ __forceinline__ void absorb(WorkCount& wc, const LaneCount& lc, bool shadow) {
   if (COUNT) {
     wc.nodes += wave_sum(lc.nodes);
     wc.tris += wave_sum(lc.tris);
+    const uint32_t ln = wave_sum(lc.lnodes), lt = wave_sum(lc.ltris);
+    if (shadow) {
+      wc.sh_nodes += ln;
+      wc.sh_tris += lt;
+    } else {
+      wc.cl_nodes += ln;
+      wc.cl_tris += lt;
+    }
   }
   wc.overflow += wave_sum(lc.overflow);
 }
@@ -316,7 +325,10 @@ __device__ __forceinline__ bool leaf_lane(const float4* __restrict__ tri, uint32
       n1 = q[3 * (k + 1) + 1];
       n2 = q[3 * (k + 1) + 2];
     }
-    if (COUNT) wc.tris += lanes_distinct(first + k);
+    if (COUNT) {
+      wc.tris += lanes_distinct(first + k);
+      wc.ltris++;
+    }
     if (ANY) {
       if (any_hit_rec(r, q0, q1, q2)) return true;
     } else {
@@ -345,7 +357,10 @@ __device__ void oct_closest(const KParams& p, const Ray& r, Best& b, Stack& s, L
     if (b.dist != __builtin_inff() && rt_prune(tn, r.dlen, b.dist, r.eps)) continue;
     float4 lo = node[2 * ni], hi = node[2 * ni + 1];
     uint32_t first = __float_as_uint(lo.w), info = __float_as_uint(hi.w);
-    if (COUNT) wc.nodes += lanes_distinct(ni);
+    if (COUNT) {
+      wc.nodes += lanes_distinct(ni);
+      wc.lnodes++;
+    }
     if (info & RT_NODE_LEAF)
       leaf_lane<false, COUNT>(p.tri, first, RT_LEAF_COUNT(info), r, b, wc);
     else
@@ -373,6 +388,7 @@ __device__ bool oct_any(const KParams& p, const Ray& r, Stack& s, LaneCount& wc)
     float info_bits;
     pop(s, first, info_bits);
     uint32_t info = __float_as_uint(info_bits);
+    if (COUNT) wc.lnodes++;
     if (info & RT_NODE_LEAF) {
       if (leaf_lane<true, COUNT>(p.tri, first, RT_LEAF_COUNT(info), r, unused, wc)) {
         s.sp = 0;
@@ -505,7 +521,10 @@ __device__ void flat_closest_w(const KParams& p, const Ray& r, bool act, Best& b
       if (act) consider(r, q0, q1, q2, b);
     }
   }
-  if (COUNT) wc.tris += n;
+  if (COUNT) {
+    wc.tris += n;
+    wc.cl_tris += n * (uint32_t)__popcll(__ballot(act));
+  }
 }
 
 template <bool COUNT>
@@ -519,7 +538,10 @@ __device__ bool flat_any_w(const KParams& p, const Ray& r, bool act, WaveCtx& w,
     fetch_commit(f, w);
     uint32_t nb = base + kFlatRecs;
     if (nb < n) f = fetch_issue(p.tri + 3 * (size_t)nb, 3 * (int)chunk<kFlatRecs>(n, nb), w.lane);
-    if (COUNT) wc.tris += m;
+    if (COUNT) {
+      wc.tris += m;
+      wc.sh_tris += m * (uint32_t)__popcll(__ballot(alive));
+    }
     float4 n0 = w.stage[0], n1 = w.stage[1], n2 = w.stage[2];
     for (uint32_t k = 0; k < m; k++) {
       float4 q0 = n0, q1 = n1, q2 = n2;
@@ -611,7 +633,10 @@ __device__ void staged_closest(const KParams& p, const Ray& r, bool act, Best& b
       want = !(tn * r.dlen > limit);
     }
     if (__ballot(want) == 0) continue;
-    if (COUNT) wc.nodes++;
+    if (COUNT) {
+      wc.nodes++;
+      wc.cl_nodes += (uint32_t)__popcll(__ballot(want));
+    }
     fetch_commit(f, w);
     if (leaf) {
       for (uint32_t base = 0; base < cnt; base += kOctRecs) {
@@ -623,7 +648,10 @@ __device__ void staged_closest(const KParams& p, const Ray& r, bool act, Best& b
         }
       }
       limit = rt_prune_limit(b.dist, r.eps);
-      if (COUNT) wc.tris += cnt;
+      if (COUNT) {
+        wc.tris += cnt;
+        wc.cl_tris += cnt * (uint32_t)__popcll(__ballot(want));
+      }
     } else {
       stage_push_children<false>(r, inv, dm, info, want, limit, sp, w, wc);
     }
@@ -654,7 +682,10 @@ __device__ bool staged_any(const KParams& p, const Ray& r, bool act, WaveCtx& w,
     // pushed and still search want it now (no re-test)
     bool want = alive && ((lm >> w.lane) & 1) != 0;
     if (__ballot(want) == 0) continue;
-    if (COUNT) wc.nodes++;
+    if (COUNT) {
+      wc.nodes++;
+      wc.sh_nodes += (uint32_t)__popcll(__ballot(want));
+    }
     if (info & RT_NODE_LEAF) {
       uint32_t cnt = RT_LEAF_COUNT(info);
       for (uint32_t base = 0; base < cnt && __ballot(want) != 0; base += kOctRecs) {
@@ -662,6 +693,7 @@ __device__ bool staged_any(const KParams& p, const Ray& r, bool act, WaveCtx& w,
         stage_load(tri + 3 * (size_t)(first + base), 3 * (int)m, w);
         if (COUNT) wc.tris += m;
         for (uint32_t k = 0; k < m; k++) {
+          if (COUNT) wc.sh_tris += (uint32_t)__popcll(__ballot(want));
           float4 q0 = w.stage[3 * k], q1 = w.stage[3 * k + 1], q2 = w.stage[3 * k + 2];
           if (want && any_hit_rec(r, q0, q1, q2)) {
             hit = true;
@@ -703,9 +735,9 @@ __device__ __forceinline__ void closest_q(const KParams& p, const Ray& r, bool a
   if (staged) {
     staged_closest<COUNT>(p, r, act, b, w, wc);
   } else {
-    LaneCount lc = {0, 0, 0};
+    LaneCount lc = {0, 0, 0, 0, 0};
     if (act) oct_closest<COUNT>(p, r, b, s, lc);
-    absorb<COUNT>(wc, lc);
+    absorb<COUNT>(wc, lc, false);
   }
 }
 
@@ -721,9 +753,9 @@ __device__ __forceinline__ bool shadow_q(const KParams& p, f3 o, f3 d, uint32_t 
   bool staged = POL == RT_POLICY_STAGED ||
                 (POL == RT_POLICY_DIR_STAGED && type == 1 && __popcll(am) >= kPacketMin);
   if (staged) return staged_any<COUNT>(p, r, act, w, wc);
-  LaneCount lc = {0, 0, 0};
+  LaneCount lc = {0, 0, 0, 0, 0};
   bool hit = act && oct_any<COUNT>(p, r, s, lc);
-  absorb<COUNT>(wc, lc);
+  absorb<COUNT>(wc, lc, true);
   return hit;
 }
 
@@ -797,15 +829,18 @@ __device__ col apply_light(const KParams& p, bool hit, const float* m, f3 P, f3 
 // Camera rays: the triangles of this tile's candidate list (csrc/rt_cand.hip)
 // and of the global list, tested with the reference's exact arithmetic after
 // the walk -- the ones whose float Moller-Trumbore error region reaches
-// beyond the walk's culling slack.  Wave-uniform loop, scalar record loads.
+// beyond the walk's culling slack.
 template <bool COUNT>
 __device__ __forceinline__ void cand_closest(const KParams& p, const Ray& r, bool act, uint32_t tile,
-                                             Best& b, WorkCount& wc) {
+                                             Best& b, WaveCtx& w, WorkCount& wc) {
   if (!p.cand_start || __ballot(act) == 0) return;
-  // Depth skip: a candidate's float new_dist is at least |pos - o| +
-  // cand_skip[prim] (csrc/rt_cand.hip), so one whose bound exceeds every
+  // Depth skip: a candidate's float new_dist is at least |pos - o| + its
+  // entry's cand_skip (csrc/rt_cand.hip), so one whose bound exceeds every
   // lane's best - |pos - o| (plus the float error of that difference)
-  // cannot win here -- one scalar compare instead of a test.
+  // cannot win here -- one compare instead of a test.  (A per-lane test of
+  // the footprint's image-space band, measured: the bands of the long
+  // footprints are 6-34 pixels wide, so nearly every listed tile has lanes
+  // inside; it removed 1 % of the tests and cost 2.7 ms on C5.)
   float bl = -__builtin_inff();
   if (act)
     bl = b.dist == __builtin_inff() ? __builtin_inff()
@@ -814,33 +849,52 @@ __device__ __forceinline__ void cand_closest(const KParams& p, const Ray& r, boo
   for (int off = 32; off > 0; off >>= 1) bl = fmaxf(bl, __shfl_xor(bl, off));
   const float bmax = __uint_as_float(uni(__float_as_uint(bl)));
   const uint32_t s = uni(p.cand_start[tile]), e = uni(p.cand_start[tile + 1]);
-  const int lane = __lane_id();
+  const int lane = w.lane;
   uint32_t tested = 0;
-  // 64 entries per round trip: each lane loads one entry and its skip bound,
-  // the wave then tests the survivors one after another
-  for (uint32_t base = s; base < e; base += 64) {
+  // kOctRecs entries per round: each lane loads one entry and its skip
+  // bound, the survivors' records are gathered in parallel (one memory round
+  // trip) into the LDS stage, compacted, then tested one after another as
+  // LDS broadcasts
+  for (uint32_t base = s; base < e; base += kOctRecs) {
     uint32_t prim = 0;
     bool keep = false;
-    if (base + lane < e) {
+    if (lane < kOctRecs && base + lane < e) {
       prim = p.cand[base + lane];
-      keep = !(p.cand_skip[prim] > bmax);
+      keep = !(p.cand_skip[base + lane] > bmax);
     }
-    uint64_t m = __ballot(keep);
-    while (m) {
-      const int j = __ffsll((unsigned long long)m) - 1;
-      m &= m - 1;
-      const float4* q = p.tri_prim + 3 * (size_t)uni(__shfl(prim, j));
-      float4 q0 = ldu(q, 0), q1 = ldu(q, 1), q2 = ldu(q, 2);
+    const uint64_t m = __ballot(keep);
+    if (m == 0) continue;
+    const uint32_t n = (uint32_t)__popcll(m);
+    const uint32_t slot = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    float4 g0, g1, g2;
+    if (keep) {
+      const float4* q = p.tri_prim + 3 * (size_t)prim;
+      g0 = q[0];
+      g1 = q[1];
+      g2 = q[2];
+    }
+    wave_sync();  // after the previous readers of stage
+    if (keep) {
+      w.stage[3 * slot] = g0;
+      w.stage[3 * slot + 1] = g1;
+      w.stage[3 * slot + 2] = g2;
+    }
+    wave_sync();
+    for (uint32_t k = 0; k < n; k++) {
+      float4 q0 = w.stage[3 * k], q1 = w.stage[3 * k + 1], q2 = w.stage[3 * k + 2];
       if (act) consider(r, q0, q1, q2, b);
-      tested++;
     }
+    tested += n;
   }
   for (uint32_t k = 0; k < p.n_cand_global; k++) {
     const float4* q = p.tri_prim + 3 * (size_t)uni(p.cand_global[k]);
     float4 q0 = ldu(q, 0), q1 = ldu(q, 1), q2 = ldu(q, 2);
     if (act) consider(r, q0, q1, q2, b);
   }
-  if (COUNT) wc.tris += tested + p.n_cand_global;
+  if (COUNT) {
+    wc.tris += tested + p.n_cand_global;
+    wc.cl_tris += (tested + p.n_cand_global) * (uint32_t)__popcll(__ballot(act));
+  }
 }
 
 // Reflection terms of one path, folded deepest-first at the end
@@ -903,7 +957,7 @@ __device__ __forceinline__ col trace_path(const KParams& p, bool valid, f3 o, f3
     b.u = b.v = 0.0f;
     b.t = 0.0f;
     closest_q<ACCEL, COUNT, POL>(p, r, alive, depth, b, s, w, wc);
-    if (ACCEL != RT_ACCEL_FLAT_D && depth == 0) cand_closest<COUNT>(p, r, alive, tile, b, wc);
+    if (ACCEL != RT_ACCEL_FLAT_D && depth == 0) cand_closest<COUNT>(p, r, alive, tile, b, w, wc);
     bool hit = alive && b.dist != __builtin_inff();
     f3 N = f3{0.0f, 0.0f, 0.0f};
     wc.hits += (uint32_t)__popcll(__ballot(hit));
@@ -1002,10 +1056,11 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES) void render_kernel(KParams p) {
     out[2] = acc.b;
   }
   // the counters are wave totals already: one atomic per counter per wave
-  uint32_t v[8] = {wc.closest, wc.shadow,   wc.pixels,      wc.nodes,
-                   wc.tris,    wc.overflow, wc.zero_normal, wc.hits};
+  uint32_t v[RT_NSTATS] = {wc.closest, wc.shadow,   wc.pixels,      wc.nodes,
+                           wc.tris,    wc.overflow, wc.zero_normal, wc.hits,
+                           wc.cl_nodes, wc.cl_tris, wc.sh_nodes,   wc.sh_tris};
 #pragma unroll
-  for (int k = 0; k < 8; k++)
+  for (int k = 0; k < RT_NSTATS; k++)
     if (lane == 0 && v[k]) atomicAdd(p.stats + k, (unsigned long long)v[k]);
 }
 

@@ -87,7 +87,9 @@ class Stats(C.Structure):
                 ("depth_overflow", C.c_ulonglong), ("zero_normal", C.c_ulonglong),
                 ("pixels", C.c_ulonglong), ("hits", C.c_ulonglong),
                 ("cand_prims", C.c_ulonglong), ("cand_entries", C.c_ulonglong),
-                ("cand_global", C.c_ulonglong)]
+                ("cand_global", C.c_ulonglong),
+                ("closest_node_lanes", C.c_ulonglong), ("closest_tri_lanes", C.c_ulonglong),
+                ("shadow_node_lanes", C.c_ulonglong), ("shadow_tri_lanes", C.c_ulonglong)]
 
     def as_dict(self):
         return {k: int(getattr(self, k)) for k, _ in self._fields_}
@@ -139,6 +141,8 @@ _PROTOS = [
     ("rt_hip_set_cull_slack", C.c_int, [C.c_void_p, C.c_float]),
     ("rt_hip_set_exact_camera", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_set_policy", C.c_int, [C.c_void_p, C.c_int]),
+    ("rt_hip_set_timing", C.c_int, [C.c_void_p, C.c_int]),
+    ("rt_hip_last_times", C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     ("rt_hip_set_camera_bound_scale", C.c_int, [C.c_void_p, C.c_double]),
     ("rt_cand_survey", C.c_int, [C.POINTER(SceneStruct), C.c_float, C.c_double, C.c_int, C.c_int,
                                  C.POINTER(C.c_ulonglong)]),
@@ -366,6 +370,17 @@ class Context:
 
     def set_exact_camera(self, on=True):
         _check(lib().rt_hip_set_exact_camera(self.h, 1 if on else 0), "exact_camera")
+
+    def set_timing(self, on=True):
+        """HIP events around the candidate lists and the render kernel of
+        every render (rt_hip_set_timing); read them with last_times()."""
+        _check(lib().rt_hip_set_timing(self.h, 1 if on else 0), "timing")
+
+    def last_times(self):
+        """(lists_ms, render_kernel_ms) of the last timed render."""
+        a, b = C.c_float(), C.c_float()
+        _check(lib().rt_hip_last_times(self.h, C.byref(a), C.byref(b)), "last_times")
+        return a.value, b.value
 
     def set_policy(self, policy):
         """Octree traversal policy (rt_hip_set_policy): 0 default, 1 per-lane,

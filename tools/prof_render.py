@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--exact", type=int, default=1)
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--policy", type=int, default=0)
+    ap.add_argument("--count", action="store_true", help="instrumented pass: print the work counters")
     a = ap.parse_args()
     s = rtgpu.Scene.synthetic(a.grid, a.grid, a.tris, seed=0x5EED, width=a.W, height=a.H)
     f = s.frame()
@@ -33,6 +34,8 @@ def main():
     ctx.set_exact_camera(bool(a.exact))
     ctx.set_camera_bound_scale(a.scale)
     ctx.set_policy(a.policy)
+    if a.count:
+        ctx.set_count_work(True)
     d = C.c_void_p()
     assert rtgpu.lib().rt_hip_malloc(0, rtgpu.tile_buffer_floats(a.W, a.H, 1) * 4, C.byref(d)) == 0
     for i in range(a.n):
@@ -41,6 +44,9 @@ def main():
         st = ctx.stats()
         print(f"render {i}: {(time.perf_counter() - t) * 1e3:.2f} ms, cand {st['cand_prims']} prims "
               f"{st['cand_entries']} entries", flush=True)
+    if a.count:
+        import json
+        print(json.dumps(st), flush=True)
 
 
 if __name__ == "__main__":
