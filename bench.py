@@ -1,12 +1,14 @@
 #!/usr/bin/env python3
 """bench.py -- Mrays/s (closest-hit + shadow queries) of the MI355X render path.
 
-A "step" renders one whole frame of the workload: every rank renders its
-8x8 tiles (tile t -> rank t % N) through the C ABI of lib/librtgpu.so on
-torch's current stream, rank tile buffers are gathered to rank 0 with one
-RCCL gather (torch.distributed "nccl" backend = RCCL over xGMI), and rank 0
-assembles the PPM-order float image.  Scene image and octree are built and
-uploaded before timing (inputs resident in HBM).
+A "step" renders one whole frame of the workload: every rank builds the
+frame's camera-ray candidate lists and renders its 8x8 tiles (tile t -> rank
+t % N) through the C ABI of lib/librtgpu.so on torch's current stream, rank
+tile buffers are gathered to rank 0 with one RCCL gather (torch.distributed
+"nccl" backend = RCCL over xGMI), and rank 0 assembles the PPM-order float
+image.  Scene image and octree are built and uploaded before timing (inputs
+resident in HBM).  The render kernel's own duration is measured with HIP
+events on its stream (rt_hip_set_timing), every timed step.
 
 Default workload = config C5 (BASELINE.json): the deterministic synthetic
 10M-triangle sphere field at 3840x2160, octree traversal.
@@ -46,8 +48,9 @@ N_XCD = 8
 
 WORKLOADS = {
     "c5": dict(kind="synthetic", accel="octree_gpu", W=3840, H=2160,
-               desc="C5 synthetic 10M-triangle sphere field (32x32 UV spheres x 9776 tris + ground, "
-                    "seed 0x5EED), 3840x2160, device-built octree"),
+               desc="C5 synthetic 10M-triangle sphere field (32x32 UV spheres of 53 stacks x 94 "
+                    "slices = 9776 tris + ground quad, seed 0x5EED, BASELINE.md), 3840x2160, "
+                    "device-built octree, exact camera rays (per-frame candidate lists)"),
     "c4": dict(kind="svati", scene="car-on-road", accel="octree", W=3840, H=2160,
                desc="C4 car-on-road.svati at 3840x2160, octree"),
     "c3": dict(kind="svati", scene="island_smooth", accel="octree", W=1920, H=1080,
@@ -65,7 +68,7 @@ def log(*a):
 
 def load_scene(wl, tmpdir):
     if wl["kind"] == "synthetic":
-        return rtgpu.Scene.synthetic(32, 32, 9766, seed=0x5EED, width=wl["W"], height=wl["H"])
+        return rtgpu.Scene.synthetic(32, 32, 9776, seed=0x5EED, width=wl["W"], height=wl["H"])
     src = os.path.join(REPO, "tests", "golden", "scenes", wl["scene"] + ".svati.gz")
     path = os.path.join(tmpdir, wl["scene"] + ".svati")
     with gzip.open(src, "rb") as i, open(path, "wb") as o:
@@ -75,41 +78,87 @@ def load_scene(wl, tmpdir):
     return s
 
 
-def cpu_baseline(scene, W, H, seconds, threads, gpu_img):
-    """The oracle (plain-C restatement of cpu/rt, brute force like the
-    reference) on a bounded deterministic pixel sample of the same frame."""
+def _oracle():
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as orc
     orc.lib()
-    rng = np.random.default_rng(1234)
-    order = rng.permutation(W * H)
-    done = 0
-    closest = shadow = 0
-    mism = 0
-    batch = threads
+    return orc
+
+
+def _sample_loop(orc, scene, W, H, pixels, seconds, threads, gpu_img, out):
+    """Render pixels (deterministic order) with the oracle until `seconds`
+    pass; accumulates queries, pixels and mismatches vs the GPU image."""
     t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds and done < len(order):
-        idx = order[done:done + batch]
-        pix = np.stack([idx // W, idx % W], axis=1).astype(np.int32)
+    done = 0
+    batch = max(1, threads)
+    while time.perf_counter() - t0 < seconds and done < len(pixels):
+        pix = pixels[done:done + batch]
         vals, cnt = orc.render(scene.ptr, W, H, pixels=pix, threads=threads)
-        closest += cnt["closest"]
-        shadow += cnt["shadow"]
+        out["closest"] += cnt["closest"]
+        out["shadow"] += cnt["shadow"]
         if gpu_img is not None:
             g = gpu_img[pix[:, 0], pix[:, 1]]
-            mism += int((g.view(np.uint32) != vals.view(np.uint32)).any(axis=1).sum())
-        done += len(idx)
-        el = time.perf_counter() - t0
-        if el < seconds / 4:
+            out["mism"] += int((g.view(np.uint32) != vals.view(np.uint32)).any(axis=1).sum())
+        done += len(pix)
+        if time.perf_counter() - t0 < seconds / 4:
             batch *= 2
-    el = time.perf_counter() - t0
+    out["pixels"] += done
+
+
+def cpu_baseline(scene, W, H, seconds, threads, gpu_img):
+    """The oracle (plain-C restatement of cpu/rt, brute force like the
+    reference) on bounded deterministic pixel samples of the same frame, in
+    the reference's own mode (SURVEY.md §8(d) "Mode A": 4 threads, one image
+    quadrant each, cpu/raytracer.c:92-127) and on all the cores this process
+    may use ("Mode B").  Returns the Mode B line with Mode A beside it."""
+    import threading
+    orc = _oracle()
+    rng = np.random.default_rng(1234)
+
+    def pix_of(idx):
+        return np.stack([idx // W, idx % W], axis=1).astype(np.int32)
+
+    # Mode A: quadrant q = (row half, column half) of cpu/raytracer.c:99-114,
+    # each thread its own quadrant's pixels in a deterministic random order
+    quads = []
+    for rh in (0, 1):
+        for ch in (0, 1):
+            rows = np.arange(rh * (H // 2), H // 2 + rh * (H - H // 2))
+            cols = np.arange(ch * (W // 2), W // 2 + ch * (W - W // 2))
+            idx = (rows[:, None] * W + cols[None, :]).ravel()
+            quads.append(pix_of(rng.permutation(idx)))
+    res_a = [dict(closest=0, shadow=0, pixels=0, mism=0) for _ in quads]
+    t0 = time.perf_counter()
+    th = [threading.Thread(target=_sample_loop,
+                           args=(orc, scene, W, H, q, seconds / 2, 1, gpu_img, r))
+          for q, r in zip(quads, res_a)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    el_a = time.perf_counter() - t0
+    qa = sum(r["closest"] + r["shadow"] for r in res_a)
+    # Mode B: every core of this process's share, one shared pixel sample
+    res_b = dict(closest=0, shadow=0, pixels=0, mism=0)
+    t0 = time.perf_counter()
+    _sample_loop(orc, scene, W, H, pix_of(rng.permutation(W * H)), seconds / 2, threads, gpu_img,
+                 res_b)
+    el_b = time.perf_counter() - t0
+    qb = res_b["closest"] + res_b["shadow"]
+    mism = res_b["mism"] + sum(r["mism"] for r in res_a)
     return {
-        "value": (closest + shadow) / el / 1e6,
+        "value": qb / el_b / 1e6,
         "unit": "Mrays/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{done} pixels ({closest} closest + {shadow} shadow queries) of the same "
-                  f"{W}x{H} frame, deterministic random order, {el:.1f} s, oracle/rt_oracle.c "
-                  f"(brute force like cpu/rt, -O2, {threads} threads)",
+        "sample": f"Mode B: {res_b['pixels']} pixels ({res_b['closest']} closest + {res_b['shadow']} "
+                  f"shadow queries) of the same {W}x{H} frame, deterministic random order, "
+                  f"{el_b:.1f} s on {threads} threads; oracle/rt_oracle.c (brute force like cpu/rt, "
+                  f"-O2)",
+        "host_cpus": os.cpu_count(),
+        "mode_a": {"value": qa / el_a / 1e6, "unit": "Mrays/s", "cores": 4,
+                   "sample": f"{sum(r['pixels'] for r in res_a)} pixels, {el_a:.1f} s, 4 threads, "
+                             f"one image quadrant each (cpu/raytracer.c:92-127)"},
         "sample_pixels_bitexact_vs_gpu": (mism == 0) if gpu_img is not None else None,
     }
 
@@ -128,8 +177,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", default="c5", choices=sorted(WORKLOADS))
     ap.add_argument("--accel", default=None, choices=["flat", "octree", "octree_gpu"])
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=20.0,
+                    help="CPU baseline budget (split between Mode A and Mode B)")
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="Mode B threads (default: this process's CPU share -- the box's "
+                         "OMP_NUM_THREADS -- capped by os.cpu_count())")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cull-slack", type=float, default=None,
                     help="octree culling slack override (tuning; default = library default)")
@@ -179,15 +231,8 @@ def main():
     work = ctx.stats()
     ctx.set_count_work(False)
 
-    k_start = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    k_end = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-
-    def step(i=None):
-        if i is not None:
-            k_start[i].record(stream)
+    def step():
         ctx.render(frame, rank, world, tiles.data_ptr(), sh)
-        if i is not None:
-            k_end[i].record(stream)
         if world > 1:
             dist.gather(tiles, list(gathered.view(world, per)) if rank == 0 else None, dst=0)
             if rank == 0:
@@ -202,26 +247,37 @@ def main():
     assert st["depth_overflow"] == 0
     counts = torch.tensor([st["closest"], st["shadow"], st["hits"], st["pixels"],
                            work["node_visits"], work["tri_tests"], work["hits"],
-                           work["closest"] + work["shadow"]], dtype=torch.float64, device=dev)
+                           work["closest"] + work["shadow"],
+                           work["closest_node_lanes"], work["closest_tri_lanes"],
+                           work["shadow_node_lanes"], work["shadow_tri_lanes"],
+                           work["closest"], work["shadow"], st["cand_entries"]],
+                          dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(counts)
-    closest, shadow, hits, pixels, nodes, tris, whits, wq = [float(x) for x in counts.tolist()]
+    (closest, shadow, hits, pixels, nodes, tris, whits, wq, cl_nodes, cl_tris, sh_nodes, sh_tris,
+     wcl, wsh, cand_entries) = [float(x) for x in counts.tolist()]
 
+    # HIP events around the candidate lists and the render kernel of every
+    # timed step, on the stream they run on (rt_hip_set_timing)
+    ctx.set_timing(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i)
+    for _ in range(args.steps):
+        step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in zip(k_start, k_end)) / args.steps
-    tt = torch.tensor([el, kern_ms], dtype=torch.float64, device=dev)
+    ft = ctx.frame_times(min(args.steps, 1024))
+    ctx.set_timing(False)
+    lists_ms = sum(a for a, _ in ft) / len(ft)
+    kern_ms = sum(b for _, b in ft) / len(ft)
+    tt = torch.tensor([el, kern_ms, lists_ms], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    el, kern_ms = tt.tolist()
+    el, kern_ms, lists_ms = tt.tolist()
 
     queries = closest + shadow
     value = queries * args.steps / el / 1e6
@@ -230,20 +286,29 @@ def main():
                  pixels * PIXEL_BYTES)
     per_launch = alg_bytes / world
     achieved = per_launch / (kern_ms * 1e-3) / 1e9
-    traffic = None
+    traffic = traffic_hi = None
+    traffic_src = None
     if world == 1 and args.traffic_json is None and args.cull_slack is None:
         # default run: the newest committed rocprofv3 PMC pass of this
-        # workload (profiles/r*_<workload>/, tools/gpu_profile.sh), named in
-        # roofline.traffic_source; a PMC pass cannot run inside the bench
+        # workload (profiles/r*_<workload>/, tools/gpu_profile.sh); a PMC
+        # pass cannot run inside the bench, so the line says where it came from
         args.traffic_json = latest_profile(args.workload, "traffic.json")
         if args.valu_json is None:
             args.valu_json = latest_profile(args.workload, "pmc_valu.json")
     if args.traffic_json and os.path.exists(args.traffic_json):
         with open(args.traffic_json) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
+            tj = json.load(f)
+        # FETCH_SIZE is exact for scattered 64 B requests and half the bytes
+        # of wide coalesced reads (MI355X_MICROARCH.md "HBM"); the kernel
+        # mixes both, so the raw count is a lower bound and x2 an upper one
+        if "fetch_size_kib_raw" in tj:
+            wb = tj.get("write_bytes_per_launch", 0.0)
+            traffic = tj["fetch_size_kib_raw"] * 1024 + wb
+            traffic_hi = tj["fetch_size_kib_raw"] * 2048 + wb
+        traffic_src = os.path.relpath(args.traffic_json, REPO)
     valu = None
     if args.valu_json and os.path.exists(args.valu_json):
-        # the resource this kernel actually saturates (DESIGN.md §5): VALU
+        # the resource this kernel actually saturates (DESIGN.md §4): VALU
         # issue.  SQ_* cycle counters count quad-cycles; GRBM_GUI_ACTIVE sums
         # the 8 XCDs' busy clocks (MI355X_MICROARCH.md, DVFS give-back).
         with open(args.valu_json) as f:
@@ -256,13 +321,21 @@ def main():
             "clock_ghz": round(pm["GRBM_GUI_ACTIVE"] / N_XCD / (kern_ms * 1e-3) / 1e9, 3),
             "source": os.path.relpath(args.valu_json, REPO),
         }
+        if "SQ_WAVE_CYCLES" in pm:
+            # resident waves per SIMD, averaged over the kernel's duration
+            valu["waves_per_simd"] = round(pm["SQ_WAVE_CYCLES"] / (N_SIMD * quad), 3)
+        if "SQ_WAVES" in pm:
+            valu["waves_launched"] = pm["SQ_WAVES"]
 
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu:
             img = rgb.view(H, W, 3).cpu().numpy()
-            log(f"[rank 0] cpu baseline: {args.cpu_seconds:.0f}s sample on {args.cpu_threads} threads")
-            cpu = cpu_baseline(scene, W, H, args.cpu_seconds, args.cpu_threads, img)
+            thr = args.cpu_threads or min(os.cpu_count() or 1,
+                                          int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or 16)
+            log(f"[rank 0] cpu baseline: {args.cpu_seconds:.0f}s of samples (Mode A 4 threads, "
+                f"Mode B {thr} threads)")
+            cpu = cpu_baseline(scene, W, H, args.cpu_seconds, thr, img)
         out = {
             "metric": "Mrays/sec (primary+shadow) at 3840x2160",
             "value": round(value, 3),
@@ -288,20 +361,39 @@ def main():
                                       "closest_hits": int(hits), "pixels": int(pixels)},
             },
             "roofline": {
+                # priced against HBM; what the kernel
+                # actually saturates is VALU issue (valu.busy_frac)
                 "bound": "hbm",
+                "limiter": ("valu" if valu and valu["busy_frac"] > achieved / HBM_PEAK_GBS
+                            else None),
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
                 "traffic": traffic,
-                "traffic_source": (os.path.relpath(args.traffic_json, REPO)
+                "traffic_upper": traffic_hi,
+                "traffic_source": (f"committed profile {traffic_src} (not measured in this run)"
                                    if traffic is not None else None),
                 "kernel": "render_kernel<FLAT>" if wl["accel"] == "flat" else "render_kernel<OCTREE>",
                 "kernel_ms": round(kern_ms, 3),
+                "candidate_lists_ms": round(lists_ms, 3),
                 "algorithmic_bytes_per_launch": int(per_launch),
                 "per_query_bytes": round(alg_bytes / wq, 1) if wq else None,
+                # wave-distinct record fetches (a record several lanes load with
+                # one instruction counts once) per query ...
                 "node_fetches_per_query": round(nodes / wq, 3) if wq else None,
                 "tri_fetches_per_query": round(tris / wq, 3) if wq else None,
+                # ... and the per-lane work behind them (SURVEY.md §8(d) N_node, N_tri)
+                "per_lane": {
+                    "closest_nodes_per_query": round(cl_nodes / wcl, 3) if wcl else None,
+                    "closest_tris_per_query": round(cl_tris / wcl, 3) if wcl else None,
+                    "shadow_nodes_per_query": round(sh_nodes / wsh, 3) if wsh else None,
+                    "shadow_tris_per_query": round(sh_tris / wsh, 3) if wsh else None,
+                    "bytes_per_launch": int((wq * RAY_BYTES + (cl_nodes + sh_nodes) * NODE_BYTES +
+                                             (cl_tris + sh_tris) * TRI_BYTES +
+                                             whits * NORMAL_BYTES + pixels * PIXEL_BYTES) / world),
+                },
+                "candidate_entries": int(cand_entries),
             },
             "valu": valu,
             "cpu_baseline": cpu,

@@ -139,10 +139,11 @@ int rt_hip_stats(rt_hip_ctx *ctx, rt_stats *out);
 int rt_hip_set_cull_slack(rt_hip_ctx *ctx, float ulps);
 /* Phase timing: with enable, every rt_hip_render records HIP events on its
  * stream before the camera candidate lists, before the render kernel and
- * after it; rt_hip_last_times waits for the last one and returns the two
- * spans in milliseconds (lists_ms = 0 without lists). */
+ * after it (a ring of the last 1024 frames; enabling clears it).
+ * rt_hip_frame_times waits for the last n timed frames and returns their two
+ * spans in milliseconds, oldest first (lists_ms ~0 without lists). */
 int rt_hip_set_timing(rt_hip_ctx *ctx, int enable);
-int rt_hip_last_times(rt_hip_ctx *ctx, float *lists_ms, float *render_ms);
+int rt_hip_frame_times(rt_hip_ctx *ctx, int n, float *lists_ms, float *render_ms);
 /* Instrumented build: also count node visits and triangle tests (slower). */
 int rt_hip_set_count_work(rt_hip_ctx *ctx, int enable);
 /* Exact camera rays (default 1): per-frame candidate lists of the triangles

@@ -345,6 +345,7 @@ struct job {
   float *out;
   vec3 u, v, C;
   atomic_size_t next;
+  size_t chunk;  /* pixels per grab: small batches must still spread over every thread */
   pthread_mutex_t lock;
   struct or_counts total;
 };
@@ -356,10 +357,10 @@ static void *worker(void *arg)
   const int W = jb->scene->camera.width;
   for (;;)
   {
-    size_t start = atomic_fetch_add(&jb->next, 16);
+    size_t start = atomic_fetch_add(&jb->next, jb->chunk);
     if (start >= jb->npix)
       break;
-    size_t stop = start + 16 < jb->npix ? start + 16 : jb->npix;
+    size_t stop = start + jb->chunk < jb->npix ? start + jb->chunk : jb->npix;
     for (size_t p = start; p < stop; p++)
     {
       int row, col;
@@ -404,6 +405,11 @@ int oracle_render(const struct or_scene *scene, const int *pixels, size_t npix, 
   jb.npix = npix;
   jb.out = out;
   atomic_init(&jb.next, 0);
+  jb.chunk = npix / ((size_t)nthreads * 4);
+  if (jb.chunk < 1)
+    jb.chunk = 1;
+  if (jb.chunk > 16)
+    jb.chunk = 16;
   pthread_mutex_init(&jb.lock, NULL);
   oracle_camera_frame(scene, &jb.u, &jb.v, &jb.C);
   pthread_t *tid = calloc((size_t)nthreads, sizeof *tid);

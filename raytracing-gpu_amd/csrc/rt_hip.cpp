@@ -35,6 +35,8 @@ extern "C" {
                           __LINE__);                                                     \
   } while (0)
 
+#define RT_TIMED_FRAMES 1024
+
 struct rt_hip_ctx {
   int device = 0;
   int accel = RT_ACCEL_FLAT;
@@ -80,11 +82,12 @@ struct rt_hip_ctx {
   size_t scan_tmp_bytes = 0;
   uint32_t* h_cand = nullptr;  // pinned: total entries, risky, global, visits
   unsigned long long cand_prims = 0, cand_entries = 0, cand_global = 0;
-  // phase timing (rt_hip_set_timing): events before the candidate lists,
-  // before the render kernel and after it, on the render's stream
+  // phase timing (rt_hip_set_timing): per frame, events before the
+  // candidate lists, before the render kernel and after it, on the render's
+  // stream; a ring of the last RT_TIMED_FRAMES frames
   int timing = 0;
-  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
-  int ev_valid = 0;
+  hipEvent_t ev[RT_TIMED_FRAMES][3] = {};
+  unsigned long long frames = 0;  // timed frames recorded
 };
 
 static int cand_params(const rt_frame* f, const float scene_c[3], float scene_r, float eps_ulps,
@@ -152,8 +155,9 @@ extern "C" void rt_hip_destroy(rt_hip_ctx* c) {
   (void)hipFree(c->d_cand);
   (void)hipFree(c->d_scan_tmp);
   if (c->h_cand) (void)hipHostFree(c->h_cand);
-  for (hipEvent_t e : c->ev)
-    if (e) (void)hipEventDestroy(e);
+  for (auto& f : c->ev)
+    for (hipEvent_t e : f)
+      if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -384,20 +388,26 @@ extern "C" int rt_cand_survey(const rt_scene* scene, float eps_ulps, double boun
 extern "C" int rt_hip_set_timing(rt_hip_ctx* c, int enable) {
   if (!c) return rt_set_error(RT_EINVAL, "null context");
   HIP_TRY(hipSetDevice(c->device));
-  for (hipEvent_t& e : c->ev)
-    if (!e) HIP_TRY(hipEventCreate(&e));
+  for (auto& f : c->ev)
+    for (hipEvent_t& e : f)
+      if (!e) HIP_TRY(hipEventCreate(&e));
   c->timing = enable ? 1 : 0;
-  c->ev_valid = 0;
+  c->frames = 0;
   return RT_OK;
 }
 
-extern "C" int rt_hip_last_times(rt_hip_ctx* c, float* lists_ms, float* render_ms) {
+extern "C" int rt_hip_frame_times(rt_hip_ctx* c, int n, float* lists_ms, float* render_ms) {
   if (!c || !lists_ms || !render_ms) return rt_set_error(RT_EINVAL, "null argument");
-  if (!c->ev_valid) return rt_set_error(RT_EINVAL, "no timed render (rt_hip_set_timing)");
+  if (n <= 0 || n > RT_TIMED_FRAMES || (unsigned long long)n > c->frames)
+    return rt_set_error(RT_EINVAL, "%d timed frames asked, %llu recorded (ring of %d)", n,
+                        c->frames, RT_TIMED_FRAMES);
   HIP_TRY(hipSetDevice(c->device));
-  HIP_TRY(hipEventSynchronize(c->ev[2]));
-  HIP_TRY(hipEventElapsedTime(lists_ms, c->ev[0], c->ev[1]));
-  HIP_TRY(hipEventElapsedTime(render_ms, c->ev[1], c->ev[2]));
+  for (int i = 0; i < n; i++) {
+    hipEvent_t* e = c->ev[(c->frames - (unsigned long long)n + (unsigned long long)i) % RT_TIMED_FRAMES];
+    HIP_TRY(hipEventSynchronize(e[2]));
+    HIP_TRY(hipEventElapsedTime(lists_ms + i, e[0], e[1]));
+    HIP_TRY(hipEventElapsedTime(render_ms + i, e[1], e[2]));
+  }
   return RT_OK;
 }
 
@@ -671,8 +681,8 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
   p.eps_rel = c->eps_ulps * 5.9604645e-8f;
   p.terms = c->d_terms;
   c->cand_prims = c->cand_entries = c->cand_global = 0;
-  c->ev_valid = 0;
-  if (c->timing) HIP_TRY(hipEventRecord(c->ev[0], s));
+  hipEvent_t* ev = c->ev[c->frames % RT_TIMED_FRAMES];
+  if (c->timing) HIP_TRY(hipEventRecord(ev[0], s));
   if (c->accel == RT_ACCEL_OCTREE && c->d_node && c->exact_camera) {
     int rc = cand_prepare(c, f, &p, s);
     if (rc) return rc;
@@ -681,17 +691,17 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
     // empty scene: nothing to traverse, the FLAT kernel with 0 records is exact
     HIP_TRY(hipMemsetAsync(c->d_counter, 0, 64, s));
     HIP_TRY(hipMemsetAsync(c->d_stats, 0, RT_NSTATS * sizeof(unsigned long long), s));
-    if (c->timing) HIP_TRY(hipEventRecord(c->ev[1], s));
+    if (c->timing) HIP_TRY(hipEventRecord(ev[1], s));
     HIP_TRY(rt_launch_render(&p, RT_ACCEL_FLAT_D, c->count_work, c->policy, c->grid, s));
   } else {
     HIP_TRY(hipMemsetAsync(c->d_counter, 0, 64, s));
     HIP_TRY(hipMemsetAsync(c->d_stats, 0, RT_NSTATS * sizeof(unsigned long long), s));
-    if (c->timing) HIP_TRY(hipEventRecord(c->ev[1], s));
+    if (c->timing) HIP_TRY(hipEventRecord(ev[1], s));
     HIP_TRY(rt_launch_render(&p, c->accel, c->count_work, c->policy, c->grid, s));
   }
   if (c->timing) {
-    HIP_TRY(hipEventRecord(c->ev[2], s));
-    c->ev_valid = 1;
+    HIP_TRY(hipEventRecord(ev[2], s));
+    c->frames++;
   }
   c->last_stream = s;
   return RT_OK;

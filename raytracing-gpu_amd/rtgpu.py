@@ -142,7 +142,8 @@ _PROTOS = [
     ("rt_hip_set_exact_camera", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_set_policy", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_set_timing", C.c_int, [C.c_void_p, C.c_int]),
-    ("rt_hip_last_times", C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
+    ("rt_hip_frame_times", C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_float),
+                                     C.POINTER(C.c_float)]),
     ("rt_hip_set_camera_bound_scale", C.c_int, [C.c_void_p, C.c_double]),
     ("rt_cand_survey", C.c_int, [C.POINTER(SceneStruct), C.c_float, C.c_double, C.c_int, C.c_int,
                                  C.POINTER(C.c_ulonglong)]),
@@ -373,14 +374,14 @@ class Context:
 
     def set_timing(self, on=True):
         """HIP events around the candidate lists and the render kernel of
-        every render (rt_hip_set_timing); read them with last_times()."""
+        every render (rt_hip_set_timing); read them with frame_times()."""
         _check(lib().rt_hip_set_timing(self.h, 1 if on else 0), "timing")
 
-    def last_times(self):
-        """(lists_ms, render_kernel_ms) of the last timed render."""
-        a, b = C.c_float(), C.c_float()
-        _check(lib().rt_hip_last_times(self.h, C.byref(a), C.byref(b)), "last_times")
-        return a.value, b.value
+    def frame_times(self, n=1):
+        """[(lists_ms, render_kernel_ms)] of the last n timed renders, oldest first."""
+        a, b = (C.c_float * n)(), (C.c_float * n)()
+        _check(lib().rt_hip_frame_times(self.h, n, a, b), "frame_times")
+        return list(zip(a, b))
 
     def set_policy(self, policy):
         """Octree traversal policy (rt_hip_set_policy): 0 default, 1 per-lane,

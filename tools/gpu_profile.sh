@@ -10,7 +10,7 @@ set -euo pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 WL=${WL:-c5}
-TAG=${TAG:-r01_$WL}
+TAG=${TAG:-r02_$WL}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 B="bench.py --workload $WL"
@@ -26,7 +26,7 @@ timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o write --outp
 python3 tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" -o "$OUT/traffic.json"
 echo "== pmc VALU"
 bash tools/pmc_pass.sh "$OUT/pmc_valu" \
-    "SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU SQ_WAVE_CYCLES GRBM_GUI_ACTIVE" \
+    "SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAVES GRBM_GUI_ACTIVE" \
     --workload $WL
 echo "== bench $WL"
 timeout -k 10 ${BENCH_TIMEOUT:-400} python3 $B --steps ${STEPS:-5} --warmup 1 \

@@ -8,10 +8,11 @@
     python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write -o profiles/x.json
 
 FETCH_SIZE / WRITE_SIZE are in KiB (rocprofv3 derived counters).  On gfx950
-FETCH_SIZE reports half the bytes of wide (16 B/lane) reads
-(MI355X_MICROARCH.md "HBM"), so it is doubled here; WRITE_SIZE is exact for
-16 B/lane stores and used as is.  The render kernel reads its node and
-triangle records as per-lane float4 loads, i.e. that 16 B/lane shape.
+FETCH_SIZE reports half the bytes of wide coalesced (16 B/lane) streaming
+reads (MI355X_MICROARCH.md "HBM") and is uncalibrated for other shapes.  The
+render kernel mixes coalesced staged fetches with scattered per-lane float4
+loads, so the raw count (x1) is reported as the lower bound and x2 as the
+upper one; WRITE_SIZE is used as is.
 Only dispatches of the uninstrumented render kernel (render_kernel<A, false>)
 are averaged.
 """
@@ -58,9 +59,11 @@ def main():
     fetch_kib = sum(f.values()) / len(f)
     out = {"kernel": a.kernel, "dispatches": len(f),
            "fetch_size_kib_raw": fetch_kib,
-           "fetch_bytes_per_launch": fetch_kib * 1024 * 2,
-           "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count of 16 B/lane reads)"}
-    total = out["fetch_bytes_per_launch"]
+           "fetch_bytes_per_launch_lo": fetch_kib * 1024,
+           "fetch_bytes_per_launch_hi": fetch_kib * 1024 * 2,
+           "correction": "FETCH_SIZE KiB x1024 (lower bound) .. x2048 (upper bound: gfx950 "
+                         "half-count of wide coalesced reads)"}
+    total = out["fetch_bytes_per_launch_lo"]
     if a.write_dir:
         w = per_dispatch(a.write_dir, "WRITE_SIZE", a.kernel)
         if w:
@@ -69,6 +72,7 @@ def main():
             out["write_bytes_per_launch"] = wk * 1024
             total += wk * 1024
     out["hbm_bytes_per_launch"] = total
+    out["hbm_bytes_per_launch_hi"] = total + out["fetch_bytes_per_launch_lo"]
     os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
     with open(a.out, "w") as fh:
         json.dump(out, fh, indent=1)
