@@ -156,7 +156,7 @@ __device__ __forceinline__ bool any_hit_rec(const Ray& r, const float4& q0, cons
 // Per-lane traversal stack: the first kLdsStack entries live in LDS, laid
 // out [entry][lane] so every lane hits its own bank; deeper entries spill to
 // a per-lane area in global memory (rare: typical depth is < 16).
-static constexpr int kLdsStack = 6;
+static constexpr int kLdsStack = 9;  // fills the 10 KB/workgroup LDS budget of 16 workgroups per CU
 static constexpr int kSpillStack = RT_SPILL_STACK;
 
 struct Stack {
@@ -275,7 +275,8 @@ __device__ __forceinline__ uint32_t mask_xor(uint32_t m, uint32_t dm) {
 // pipelined: child k+1's box is in flight while child k is tested.
 // CLOSEST pushes (node, entry t) and prunes by best; any-hit pushes the
 // child's own (first, info) words from its box record, so a pop needs no
-// node fetch -- one dependent load per step instead of two.
+// node fetch -- one dependent load per step instead of two.  (The per-lane
+// any-hit walk uses push_children_any: measured on C5, 16.18 vs 16.33 ms.)
 template <bool CLOSEST, bool COUNT>
 __device__ __forceinline__ void push_children(const float4* __restrict__ node, const Ray& r, f3 inv,
                                               uint32_t dm, uint32_t first, uint32_t info,
@@ -308,6 +309,34 @@ __device__ __forceinline__ void push_children(const float4* __restrict__ node, c
       push(s, __float_as_uint(clo.w), chi.w, wc);
     }
     if (!more) break;
+  }
+}
+
+// Any-hit interior node: the children's boxes in storage order (increasing
+// octant), reversed when the ray's direction octant is mostly negative, so
+// the walk still tends to pop the nearer children first; no per-child
+// octant arithmetic (any-hit needs no exact front-to-back order).  Child
+// k+1's box is in flight while child k is tested.
+template <bool COUNT>
+__device__ __forceinline__ void push_children_any(const float4* __restrict__ node, const Ray& r,
+                                                  f3 inv, uint32_t dm, uint32_t first,
+                                                  uint32_t info, Stack& s, LaneCount& wc) {
+  const int cnt = (int)RT_NODE_COUNT(info);
+  const bool up = __popc(dm) >= 2;  // storage order = far-to-near for dm = 7
+  int k = up ? 0 : cnt - 1;
+  const int step = up ? 1 : -1;
+  uint32_t ci = first + (uint32_t)k;
+  float4 nlo = node[2 * ci], nhi = node[2 * ci + 1];
+  if (COUNT) wc.nodes += lanes_distinct(ci);
+  for (int n = 0; n < cnt; n++) {
+    float4 clo = nlo, chi = nhi;
+    if (n + 1 < cnt) {
+      ci += (uint32_t)step;
+      nlo = node[2 * ci];
+      nhi = node[2 * ci + 1];
+      if (COUNT) wc.nodes += lanes_distinct(ci);
+    }
+    if (box_enter(r, inv, clo, chi) != __builtin_inff()) push(s, __float_as_uint(clo.w), chi.w, wc);
   }
 }
 
@@ -396,7 +425,7 @@ __device__ bool oct_any(const KParams& p, const Ray& r, Stack& s, LaneCount& wc)
         return true;
       }
     } else {
-      push_children<false, COUNT>(node, r, inv, dm, first, info, 0.0f, s, wc);
+      push_children_any<COUNT>(node, r, inv, dm, first, info, s, wc);
     }
   }
   wave_sync();
@@ -1002,6 +1031,7 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES) void render_kernel(KParams p) {
   __shared__ float4 s_stack[ACCEL == RT_ACCEL_FLAT_D ? 1 : kStackArea];
   __shared__ float4 s_stage[ACCEL == RT_ACCEL_FLAT_D ? kStageFlat : kStageOct];
   __shared__ float s_terms[kLdsTerms * 3 * 64];
+  __shared__ float s_acc[3 * 64];  // the pixel's sample sum (cpu/raytracer.c:60-68)
   const size_t gl = (size_t)blockIdx.x * 64 + (size_t)lane;
   Stack stk;
   stk.idx = (uint32_t*)s_stack;
@@ -1028,27 +1058,38 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES) void render_kernel(KParams p) {
     if (lane == 0) t = atomicAdd(p.tile_counter, 1u);
     t = uni(t);
     if (t >= nt) break;  // every tile taken: the wave exits
-    uint32_t g = t * (uint32_t)p.nranks + (uint32_t)p.rank;  // global tile index
-    int ty = (int)(g / (uint32_t)p.tiles_x), tx = (int)(g % (uint32_t)p.tiles_x);
-    int pr = ty * 8 + (lane >> 3), pc = tx * 8 + (lane & 7);
-    // PPM (row, col) -> framebuffer slot (j, i) of cpu/raytracer.c:71,128-134
-    int ii = p.W - pc, jj = p.H - pr;
-    bool valid = pr < p.H && pc < p.W && ii >= 1 && ii <= 2 * (p.W / 2) && jj >= 1 &&
-                 jj <= 2 * (p.H / 2);
-    int i = ii - p.W / 2, j = jj - p.H / 2;
-    col acc = init_color(0.0f, 0.0f, 0.0f);
-    wc.pixels += (uint32_t)__popcll(__ballot(valid));
-    // for (float k = i; k < i + 1; k += 0.5) for (float l = j; ...)  (cpu/raytracer.c:55-58)
-    for (int sk = 0; sk < 2; sk++) {
-      float k = (float)i + 0.5f * (float)sk;
-      for (int sl = 0; sl < 2; sl++) {
-        float l = (float)j + 0.5f * (float)sl;
-        f3 point = add(add(p.C, scale(p.u, k)), scale(p.v, l));
-        f3 dir = normalize(sub(p.pos, point));
-        col sc = trace_path<ACCEL, COUNT, POL>(p, valid, point, dir, 1.0f, stk, w, wc, t, T);
-        acc = color_add(acc, color_mul(sc, 0.25f));
-      }
+    // Pixel state is recomputed per sample from (t, lane) and the pixel's
+    // accumulator lives in LDS, so nothing but the lane id stays live across
+    // a path (in registers, the walks' pressure spilled them to scratch: 72 B
+    // per lane per tile of HBM writes)
+    bool valid = false;
+    for (int smp = 0; smp < 4; smp++) {
+      // an opaque copy of the lane id: keeps the compiler from hoisting the
+      // pixel arithmetic out of the sample loop (and spilling it)
+      int ln = lane;
+      __asm__ volatile("" : "+v"(ln));
+      const uint32_t g = t * (uint32_t)p.nranks + (uint32_t)p.rank;  // global tile index
+      const int ty = (int)(g / (uint32_t)p.tiles_x), tx = (int)(g % (uint32_t)p.tiles_x);
+      const int pr = ty * 8 + (ln >> 3), pc = tx * 8 + (ln & 7);
+      // PPM (row, col) -> framebuffer slot (j, i) of cpu/raytracer.c:71,128-134
+      const int ii = p.W - pc, jj = p.H - pr;
+      valid = pr < p.H && pc < p.W && ii >= 1 && ii <= 2 * (p.W / 2) && jj >= 1 &&
+              jj <= 2 * (p.H / 2);
+      const int i = ii - p.W / 2, j = jj - p.H / 2;
+      if (smp == 0) wc.pixels += (uint32_t)__popcll(__ballot(valid));
+      // for (float k = i; k < i + 1; k += 0.5) for (float l = j; ...)  (cpu/raytracer.c:55-58)
+      const float k = (float)i + 0.5f * (float)(smp >> 1);
+      const float l = (float)j + 0.5f * (float)(smp & 1);
+      f3 point = add(add(p.C, scale(p.u, k)), scale(p.v, l));
+      f3 dir = normalize(sub(p.pos, point));
+      col sc = trace_path<ACCEL, COUNT, POL>(p, valid, point, dir, 1.0f, stk, w, wc, t, T);
+      col a = smp == 0 ? init_color(0.0f, 0.0f, 0.0f) : col{s_acc[lane], s_acc[64 + lane], s_acc[128 + lane]};
+      a = color_add(a, color_mul(sc, 0.25f));
+      s_acc[lane] = a.r;
+      s_acc[64 + lane] = a.g;
+      s_acc[128 + lane] = a.b;
     }
+    col acc = col{s_acc[lane], s_acc[64 + lane], s_acc[128 + lane]};
     if (!valid) acc = col{0.0f, 0.0f, 0.0f};
     float* out = p.out + ((size_t)t * 64 + (size_t)lane) * 3;
     out[0] = acc.r;
