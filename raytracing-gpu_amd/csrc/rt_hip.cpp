@@ -12,6 +12,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <string>
+#include <thread>
 #include <vector>
 
 #include "rt_build.h"
@@ -816,6 +818,26 @@ extern "C" int rt_raytrace(const char* input, const char* output) {
     }                                                                                  \
   } while (0)
 
+// fn(g) for every GPU g on its own host thread (device setup and the render
+// calls -- whose candidate lists wait on their device once -- proceed on all
+// GPUs at once); the first failure's message is re-raised on this thread
+// (the detail message is per thread, rt_error.c).
+template <class F>
+static int per_gpu(int ngpus, F fn) {
+  std::vector<int> rcs(ngpus, RT_OK);
+  std::vector<std::string> msgs(ngpus);
+  std::vector<std::thread> th;
+  for (int g = 0; g < ngpus; g++)
+    th.emplace_back([&, g]() {
+      rcs[g] = fn(g);
+      if (rcs[g]) msgs[g] = rt_last_error();
+    });
+  for (auto& t : th) t.join();
+  for (int g = 0; g < ngpus; g++)
+    if (rcs[g]) return rt_set_error(rcs[g], "GPU %d: %s", g, msgs[g].c_str());
+  return RT_OK;
+}
+
 extern "C" int rt_raytrace_multi(const char* input, const char* output, int ngpus, int accel,
                                  rt_stats* stats, double* render_ms) {
   if (!input || !output || ngpus < 1 || ngpus > 64) return rt_set_error(RT_EINVAL, "bad argument");
@@ -852,10 +874,14 @@ extern "C" int rt_raytrace_multi(const char* input, const char* output, int ngpu
   size_t npx = (size_t)f.width * f.height;
   std::chrono::steady_clock::time_point t0, t1;
   rt_stats sum{};
-  for (int g = 0; !rc && g < ngpus; g++) {
-    rc = rt_hip_create(g, scene, accel, &ctx[g]);
-    if (!rc) rc = rt_hip_malloc(g, tile_floats * sizeof(float), (void**)&d_tiles[g]);
-  }
+  bool in_group = false;
+  // every GPU builds its own scene image and octree at once
+  if (!rc)
+    rc = per_gpu(ngpus, [&](int g) {
+      int r = rt_hip_create(g, scene, accel, &ctx[g]);
+      if (!r) r = rt_hip_malloc(g, tile_floats * sizeof(float), (void**)&d_tiles[g]);
+      return r;
+    });
   if (!rc) rc = rt_hip_malloc(0, tile_floats * ngpus * sizeof(float), (void**)&d_gather);
   if (!rc) rc = rt_hip_malloc(0, npx * 3 * sizeof(float), (void**)&d_rgb);
   if (rc) goto out;
@@ -869,16 +895,18 @@ extern "C" int rt_raytrace_multi(const char* input, const char* output, int ngpu
     (void)hipDeviceSynchronize();
   }
   t0 = std::chrono::steady_clock::now();
-  for (int g = 0; !rc && g < ngpus; g++) rc = rt_hip_render(ctx[g], &f, g, ngpus, d_tiles[g], nullptr);
+  rc = per_gpu(ngpus, [&](int g) { return rt_hip_render(ctx[g], &f, g, ngpus, d_tiles[g], nullptr); });
   if (rc) goto out;
   if (ngpus > 1) {
     // one gather of every rank's tile buffer to device 0 over xGMI
     NCCL_TRY(ncclGroupStart());
+    in_group = true;
     for (int g = 0; g < ngpus; g++) {
       (void)hipSetDevice(g);
       NCCL_TRY(ncclGather(d_tiles[g], g == 0 ? d_gather : nullptr, tile_floats, ncclFloat, 0,
                           comms[g], ctx[g]->stream));
     }
+    in_group = false;
     NCCL_TRY(ncclGroupEnd());
     rc = rt_hip_assemble(ctx[0], &f, d_gather, ngpus, d_rgb, nullptr);
   } else {
@@ -913,6 +941,7 @@ extern "C" int rt_raytrace_multi(const char* input, const char* output, int ngpu
   if (stats) *stats = sum;
   if (render_ms) *render_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
 out:
+  if (in_group) (void)ncclGroupEnd();  // close the group a failed enqueue left open
   for (int g = 0; g < ngpus; g++) {
     if (comms[g]) ncclCommDestroy(comms[g]);
     if (d_tiles[g]) rt_hip_free(d_tiles[g]);

@@ -57,6 +57,24 @@ static void *scan_chunk(void *arg)
   scan_task *t = arg;
   rt_lex cur = *t->lx;
   const char *p = t->s;
+  /* a table entry per line at most: sized once from the chunk's newlines,
+   * so the scan never reallocates (first-touch page faults then happen on
+   * this thread, in parallel with the others) */
+  size_t lines = 1;
+  for (const char *q = p; q < t->e; q++)
+  {
+    q = memchr(q, '\n', (size_t)(t->e - q));
+    if (!q)
+      break;
+    lines++;
+  }
+  t->cap = lines;
+  t->v = malloc(t->cap * sizeof *t->v);
+  if (!t->v)
+  {
+    t->oom = 1;
+    return NULL;
+  }
   while (p < t->e)
   {
     const char *q = p;
@@ -71,18 +89,6 @@ static void *scan_chunk(void *arg)
       if (!rt_lex_float(&cur, &l.x) && !rt_lex_float(&cur, &l.y) && !rt_lex_float(&cur, &l.z) &&
           cur.p - q < (ptrdiff_t)UINT32_MAX)
       {
-        if (t->n == t->cap)
-        {
-          size_t nc = t->cap ? 2 * t->cap : 4096;
-          rt_vline *na = realloc(t->v, nc * sizeof *na);
-          if (!na)
-          {
-            t->oom = 1;
-            return NULL;
-          }
-          t->v = na;
-          t->cap = nc;
-        }
         l.off = (size_t)(q - t->lx->buf);
         l.len = (uint32_t)(cur.p - q);
         t->v[t->n++] = l;
@@ -132,33 +138,29 @@ int rt_prescan_build(const rt_lex *lx, rt_prescan *ps)
       pthread_join(tid[i], NULL);
     else
       scan_chunk(&task[i]);
-  size_t total = 0;
   int oom = 0;
   for (int i = 0; i < nt; i++)
-  {
-    total += task[i].n;
     oom |= task[i].oom;
-  }
-  rt_vline *all = oom ? NULL : malloc((total ? total : 1) * sizeof *all);
-  if (all)
+  if (oom)
   {
-    size_t k = 0;
+    /* out of memory for the tables: fall back to the serial scanner */
     for (int i = 0; i < nt; i++)
-    {
-      memcpy(all + k, task[i].v, task[i].n * sizeof *all);
-      k += task[i].n;
-    }
-    ps->v = all;
-    ps->n = total;
+      free(task[i].v);
+    return RT_OK;
   }
+  /* the threads' tables, in file order, are the segments (no merge copy) */
   for (int i = 0; i < nt; i++)
-    free(task[i].v);
-  /* out of memory for the table: fall back to the serial scanner */
+  {
+    ps->seg_v[i] = task[i].v;
+    ps->seg_n[i] = task[i].n;
+  }
+  ps->nseg = nt;
   return RT_OK;
 }
 
 void rt_prescan_free(rt_prescan *ps)
 {
-  free(ps->v);
+  for (int i = 0; i < ps->nseg; i++)
+    free(ps->seg_v[i]);
   memset(ps, 0, sizeof *ps);
 }

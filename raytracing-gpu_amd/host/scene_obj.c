@@ -21,6 +21,7 @@
 #include <string.h>
 
 #include "rt_internal.h"
+#include "rt_par_write.h"
 #include "rt_lex.h"
 
 void rt_object_defaults(rt_object *o);
@@ -347,37 +348,64 @@ int rt_scene_load_obj(const char *path, rt_scene **out)
   return RT_OK;
 }
 
+typedef struct {
+  const rt_scene *s;
+  const size_t *base; /* first vertex index (1-based) of each object */
+} obj_ctx;
+
+/* unit 0 of an object: its `o` line and #rt material block; then 3t `v`
+ * lines, 3t `vn` lines and t `f` lines (t triangles) */
+static size_t obj_unit(const void *ctx_, size_t oi, size_t j, char *p)
+{
+  const obj_ctx *ctx = ctx_;
+  const rt_object *o = &ctx->s->objects[oi];
+  const size_t nv = 3 * (size_t)o->triangle_count;
+  if (j == 0)
+    return (size_t)snprintf(p, RT_UNIT_MAX,
+                            "o object%zu\n#rt Ka %.9g %.9g %.9g\n#rt Kd %.9g %.9g %.9g\n"
+                            "#rt Ks %.9g %.9g %.9g\n#rt Ns %.9g\n#rt Ni %.9g\n#rt Nr %.9g\n"
+                            "#rt d %.9g\n",
+                            oi, (double)o->ka.x, (double)o->ka.y, (double)o->ka.z, (double)o->kd.x,
+                            (double)o->kd.y, (double)o->kd.z, (double)o->ks.x, (double)o->ks.y,
+                            (double)o->ks.z, (double)o->ns, (double)o->ni, (double)o->nr,
+                            (double)o->d);
+  j--;
+  if (j < 2 * nv)
+  {
+    const int normal = j >= nv;
+    const size_t m = normal ? j - nv : j;
+    const rt_vec3 v = normal ? o->triangles[m / 3].normal[m % 3] : o->triangles[m / 3].vertex[m % 3];
+    return (size_t)snprintf(p, RT_UNIT_MAX, "%s %.9g %.9g %.9g\n", normal ? "vn" : "v",
+                            (double)v.x, (double)v.y, (double)v.z);
+  }
+  const size_t a = ctx->base[oi] + 3 * (j - 2 * nv);
+  return (size_t)snprintf(p, RT_UNIT_MAX, "f %zu//%zu %zu//%zu %zu//%zu\n", a, a, a + 1, a + 1,
+                          a + 2, a + 2);
+}
+
 int rt_scene_write_obj(const rt_scene *s, const char *path)
 {
   FILE *f = fopen(path, "w");
   if (!f)
     return rt_set_error(RT_EIO, "%s: %s", path, strerror(errno));
-  size_t base = 1;
+  size_t *units = malloc((2 * s->object_count + 1) * sizeof *units);
+  if (!units)
+  {
+    fclose(f);
+    return rt_set_error(RT_ENOMEM, "writer");
+  }
+  size_t *base = units + s->object_count;
+  size_t b = 1;
   for (size_t i = 0; i < s->object_count; i++)
   {
-    const rt_object *o = &s->objects[i];
-    fprintf(f, "o object%zu\n", i);
-    fprintf(f, "#rt Ka %.9g %.9g %.9g\n#rt Kd %.9g %.9g %.9g\n#rt Ks %.9g %.9g %.9g\n",
-            (double)o->ka.x, (double)o->ka.y, (double)o->ka.z, (double)o->kd.x, (double)o->kd.y,
-            (double)o->kd.z, (double)o->ks.x, (double)o->ks.y, (double)o->ks.z);
-    fprintf(f, "#rt Ns %.9g\n#rt Ni %.9g\n#rt Nr %.9g\n#rt d %.9g\n", (double)o->ns, (double)o->ni,
-            (double)o->nr, (double)o->d);
-    for (unsigned t = 0; t < o->triangle_count; t++)
-      for (int k = 0; k < 3; k++)
-        fprintf(f, "v %.9g %.9g %.9g\n", (double)o->triangles[t].vertex[k].x,
-                (double)o->triangles[t].vertex[k].y, (double)o->triangles[t].vertex[k].z);
-    for (unsigned t = 0; t < o->triangle_count; t++)
-      for (int k = 0; k < 3; k++)
-        fprintf(f, "vn %.9g %.9g %.9g\n", (double)o->triangles[t].normal[k].x,
-                (double)o->triangles[t].normal[k].y, (double)o->triangles[t].normal[k].z);
-    for (unsigned t = 0; t < o->triangle_count; t++)
-    {
-      size_t a = base + 3 * (size_t)t;
-      fprintf(f, "f %zu//%zu %zu//%zu %zu//%zu\n", a, a, a + 1, a + 1, a + 2, a + 2);
-    }
-    base += 3 * (size_t)o->triangle_count;
+    units[i] = 1 + 7 * (size_t)s->objects[i].triangle_count;
+    base[i] = b;
+    b += 3 * (size_t)s->objects[i].triangle_count;
   }
-  if (fclose(f) != 0)
-    return rt_set_error(RT_EIO, "%s: write failed", path);
-  return RT_OK;
+  obj_ctx ctx = { s, base };
+  int rc = rt_par_write(f, &ctx, s->object_count, units, obj_unit);
+  free(units);
+  if (fclose(f) != 0 && !rc)
+    rc = rt_set_error(RT_EIO, "%s: write failed", path);
+  return rc;
 }

@@ -24,6 +24,7 @@
 
 #include "rt_internal.h"
 #include "rt_lex.h"
+#include "rt_par_write.h"
 
 int rt_lex_open(const char *path, rt_lex *lx)
 {
@@ -340,9 +341,26 @@ void rt_scene_free(rt_scene *s)
 
 /* ---- writer ---- */
 
-static void put_vec(FILE *f, const char *key, rt_vec3 v)
+/* unit 0 of an object: its header block; units 1..nv its `v` lines, then nv
+ * `vn` lines.  The parser pops from the end: line m holds corner nv-1-m. */
+static size_t svati_unit(const void *ctx, size_t oi, size_t j, char *p)
 {
-  fprintf(f, "%s %.9g %.9g %.9g\n", key, (double)v.x, (double)v.y, (double)v.z);
+  const rt_object *o = &((const rt_scene *)ctx)->objects[oi];
+  size_t nv = 3 * (size_t)o->triangle_count;
+  if (j == 0)
+    return (size_t)snprintf(p, RT_UNIT_MAX,
+                            "\nobject %zu\nNs %.9g\nNi %.9g\nNr %.9g\nd %.9g\n"
+                            "Ka %.9g %.9g %.9g\nKd %.9g %.9g %.9g\nKs %.9g %.9g %.9g\n",
+                            nv, (double)o->ns, (double)o->ni, (double)o->nr, (double)o->d,
+                            (double)o->ka.x, (double)o->ka.y, (double)o->ka.z, (double)o->kd.x,
+                            (double)o->kd.y, (double)o->kd.z, (double)o->ks.x, (double)o->ks.y,
+                            (double)o->ks.z);
+  const int normal = j > nv;
+  size_t idx = nv - 1 - (normal ? j - 1 - nv : j - 1);
+  const rt_vec3 v = normal ? o->triangles[idx / 3].normal[idx % 3]
+                           : o->triangles[idx / 3].vertex[idx % 3];
+  return (size_t)snprintf(p, RT_UNIT_MAX, "%s %.9g %.9g %.9g\n", normal ? "vn" : "v", (double)v.x,
+                          (double)v.y, (double)v.z);
 }
 
 int rt_scene_write_svati(const rt_scene *s, const char *path)
@@ -365,29 +383,17 @@ int rt_scene_write_svati(const rt_scene *s, const char *path)
               (double)l->r, (double)l->g, (double)l->b, (double)l->v.x, (double)l->v.y,
               (double)l->v.z);
   }
-  for (size_t i = 0; i < s->object_count; i++)
+  size_t *units = malloc((s->object_count + 1) * sizeof *units);
+  if (!units)
   {
-    const rt_object *o = &s->objects[i];
-    size_t nv = 3 * (size_t)o->triangle_count;
-    fprintf(f, "\nobject %zu\n", nv);
-    fprintf(f, "Ns %.9g\nNi %.9g\nNr %.9g\nd %.9g\n", (double)o->ns, (double)o->ni, (double)o->nr,
-            (double)o->d);
-    put_vec(f, "Ka", o->ka);
-    put_vec(f, "Kd", o->kd);
-    put_vec(f, "Ks", o->ks);
-    /* the parser pops from the end: line m holds corner N-1-m */
-    for (size_t m = 0; m < nv; m++)
-    {
-      size_t idx = nv - 1 - m;
-      put_vec(f, "v", o->triangles[idx / 3].vertex[idx % 3]);
-    }
-    for (size_t m = 0; m < nv; m++)
-    {
-      size_t idx = nv - 1 - m;
-      put_vec(f, "vn", o->triangles[idx / 3].normal[idx % 3]);
-    }
+    fclose(f);
+    return rt_set_error(RT_ENOMEM, "writer");
   }
-  if (fclose(f) != 0)
-    return rt_set_error(RT_EIO, "%s: write failed", path);
-  return RT_OK;
+  for (size_t i = 0; i < s->object_count; i++)
+    units[i] = 1 + 6 * (size_t)s->objects[i].triangle_count;
+  int rc = rt_par_write(f, s, s->object_count, units, svati_unit);
+  free(units);
+  if (fclose(f) != 0 && !rc)
+    rc = rt_set_error(RT_EIO, "%s: write failed", path);
+  return rc;
 }

@@ -70,6 +70,30 @@ def test_cli_ppm_md5(gpu, scene_dir, tmp_path, manifest):
     assert p.returncode == 1 and "usage:" in p.stderr
 
 
+def _with_camera_size(src, dst, width, height):
+    """Copy of a .svati scene with its camera line's resolution replaced."""
+    lines = open(src).read().split("\n")
+    for i, ln in enumerate(lines):
+        f = ln.split()
+        if f and f[0] == "camera":
+            lines[i] = " ".join(["camera", str(width), str(height)] + f[3:])
+    dst.write_text("\n".join(lines))
+
+
+def test_raytrace_multi_one_gpu_md5(gpu, scene_dir, tmp_path, manifest):
+    """The drop-in entry rt_raytrace_multi (file in, P3 file out, its own
+    device setup, gather and assemble) with ngpus=1 writes the reference's
+    exact bytes for every golden case (rt_raytrace is its ngpus=1 form)."""
+    for case in manifest:
+        sv = tmp_path / f"{case['scene']}_{case['width']}.svati"
+        _with_camera_size(os.path.join(scene_dir, case["scene"] + ".svati"), sv, case["width"],
+                          case["height"])
+        out = tmp_path / "o.ppm"
+        st, _ = gpu.raytrace(str(sv), str(out), gpus=1)
+        assert hashlib.md5(out.read_bytes()).hexdigest() == case["ppm_md5"], case_id(case)
+        assert st["closest"] == case["closest"] and st["shadow"] == case["shadow"], case_id(case)
+
+
 @pytest.mark.parametrize("nranks", [2, 3, 8])
 def test_tile_partition_gather_assemble(gpu, scene_dir, nranks, manifest):
     """Rank-sharded renders + rank-major gather + assemble == the single image."""

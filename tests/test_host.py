@@ -301,3 +301,38 @@ def test_ppm_writer_parallel_chunks(built, tmp_path):
         finally:
             _threads(None)
         assert out.read_bytes() == want, th
+
+
+@pytest.mark.parametrize("kind", ["svati", "obj"])
+def test_scene_writers_parallel_identical(built, tmp_path, kind):
+    """§8f item 1: the scene writers format chunks of lines on the host
+    threads (host/par_write.c) and write them in order: the bytes do not
+    depend on the thread count, and every `v`/`vn` line is the "%.9g"
+    formatting of the scene's floats in the writer's documented order."""
+    import rtgpu
+    s = rtgpu.Scene.synthetic(3, 3, 3000, seed=0x5EED, width=64, height=36)
+    outs = []
+    for th in (1, 3, 8):
+        _threads(th)
+        try:
+            p = tmp_path / f"w{th}.{kind}"
+            (s.write_svati if kind == "svati" else s.write_obj)(str(p))
+            outs.append(p.read_bytes())
+        finally:
+            _threads(None)
+    assert outs[0] == outs[1] == outs[2]
+    tri = s.triangles_array()  # (T, 6, 3): 3 vertices then 3 normals, file/object order
+    lines = outs[0].decode().split("\n")
+    vlines = [ln for ln in lines if ln.startswith("v ")]
+    assert len(vlines) == 3 * len(tri)
+    # obj: object by object, triangle t corner k in order; svati: each
+    # object's corners in reverse (the reference parser pops from the end)
+    first = vlines[0].split()[1:]
+    if kind == "obj":
+        want = tri[0, 0]
+    else:
+        n0 = sum(1 for ln in lines[:lines.index(vlines[0])] if ln.startswith("object"))
+        assert n0 == 1
+        nv0 = int(next(ln for ln in lines if ln.startswith("object")).split()[1])
+        want = tri[nv0 // 3 - 1, 2]
+    assert first == ["%.9g" % float(x) for x in want]
