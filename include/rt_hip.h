@@ -145,6 +145,10 @@ int rt_hip_set_cull_slack(rt_hip_ctx *ctx, float ulps);
 int rt_hip_set_timing(rt_hip_ctx *ctx, int enable);
 int rt_hip_frame_times(rt_hip_ctx *ctx, int n, float *lists_ms, float *render_ms);
 /* Instrumented build: also count node visits and triangle tests (slower). */
+/* Shader clocks of every work item -- (tile t, sample s) at index 4t + s,
+ * rank-local tile order -- of the last instrumented render (n <= 4 x tiles
+ * of the rank): the load-balance picture of a frame. */
+int rt_hip_tile_cycles(rt_hip_ctx *ctx, unsigned long long *out, size_t n);
 int rt_hip_set_count_work(rt_hip_ctx *ctx, int enable);
 /* Exact camera rays (default 1): per-frame candidate lists of the triangles
  * whose float Moller-Trumbore error region the octree slack does not cover

@@ -60,6 +60,10 @@ struct rt_hip_ctx {
   float eps_ulps = RT_EPS_ULPS_DEFAULT;
   int policy = RT_POLICY_DEFAULT;  // traversal policy (tests / A/B only: rt_hip_set_policy)
   float* d_terms = nullptr;        // deep reflection terms (KParams::terms)
+  unsigned long long* d_tile_cycles = nullptr;  // COUNT pass: per-item clocks
+  float* d_samples = nullptr;                   // per-item sample colours (KParams::samples)
+  size_t samples_cap = 0;                       // tiles
+  size_t tile_cycles_cap = 0, tile_cycles_n = 0;
   // exact camera rays (csrc/rt_cand.hip)
   int exact_camera = 1;
   double bound_scale = 1.0;  // 1 = the proven float-MT error bound (tools/mt_bound.py)
@@ -140,6 +144,8 @@ extern "C" void rt_hip_destroy(rt_hip_ctx* c) {
   (void)hipFree(c->d_stats);
   (void)hipFree(c->d_spill);
   (void)hipFree(c->d_terms);
+  (void)hipFree(c->d_tile_cycles);
+  (void)hipFree(c->d_samples);
   if (c->d_tri_prim != c->d_tri) (void)hipFree(c->d_tri_prim);
   (void)hipFree(c->d_cand_list);
   (void)hipFree(c->d_cand_fp);
@@ -203,7 +209,7 @@ extern "C" int rt_hip_create(int device, const rt_scene* scene, int accel, rt_hi
   if (!rc) rc = upload(&c->d_mat, fs.mat, bytes_mat);
   if (!rc) rc = upload(&c->d_light, fs.light, bytes_light);
   if (!rc && fs.nnode) rc = upload(&c->d_node, fs.node, bytes_node);
-  if (!rc) rc = upload(&c->d_counter, nullptr, 64);
+  if (!rc) rc = upload(&c->d_counter, nullptr, 8 * 128);  // 8 item-stream counters (rt_render.hip)
   if (!rc) rc = upload(&c->d_stats, nullptr, RT_NSTATS * sizeof(unsigned long long));
   if (!rc && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
     rc = rt_set_error(RT_EHIP, "hipStreamCreate");
@@ -410,6 +416,18 @@ extern "C" int rt_hip_frame_times(rt_hip_ctx* c, int n, float* lists_ms, float* 
     HIP_TRY(hipEventElapsedTime(lists_ms + i, e[0], e[1]));
     HIP_TRY(hipEventElapsedTime(render_ms + i, e[1], e[2]));
   }
+  return RT_OK;
+}
+
+extern "C" int rt_hip_tile_cycles(rt_hip_ctx* c, unsigned long long* out, size_t n) {
+  if (!c || !out) return rt_set_error(RT_EINVAL, "null argument");
+  if (!c->d_tile_cycles || n > c->tile_cycles_n)
+    return rt_set_error(RT_EINVAL, "%zu tile clocks asked, %zu recorded (rt_hip_set_count_work)", n,
+                        c->tile_cycles_n);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = c->last_stream ? c->last_stream : c->stream;
+  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(hipMemcpy(out, c->d_tile_cycles, n * sizeof *out, hipMemcpyDeviceToHost));
   return RT_OK;
 }
 
@@ -682,6 +700,26 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
   // (DESIGN.md "Conservative culling")
   p.eps_rel = c->eps_ulps * 5.9604645e-8f;
   p.terms = c->d_terms;
+  if ((size_t)p.ntiles_local > c->samples_cap) {
+    (void)hipFree(c->d_samples);
+    c->d_samples = nullptr;
+    c->samples_cap = 0;
+    HIP_TRY(hipMalloc((void**)&c->d_samples, (size_t)p.ntiles_local * 4 * 192 * sizeof(float)));
+    c->samples_cap = (size_t)p.ntiles_local;
+  }
+  p.samples = c->d_samples;
+  if (c->count_work) {  // per-item clocks of the instrumented pass (rt_hip_tile_cycles)
+    const size_t items = 4 * (size_t)p.ntiles_local;
+    if (items > c->tile_cycles_cap) {
+      (void)hipFree(c->d_tile_cycles);
+      c->d_tile_cycles = nullptr;
+      c->tile_cycles_cap = 0;
+      HIP_TRY(hipMalloc((void**)&c->d_tile_cycles, items * sizeof(unsigned long long)));
+      c->tile_cycles_cap = items;
+    }
+    c->tile_cycles_n = items;
+    p.tile_cycles = c->d_tile_cycles;
+  }
   c->cand_prims = c->cand_entries = c->cand_global = 0;
   hipEvent_t* ev = c->ev[c->frames % RT_TIMED_FRAMES];
   if (c->timing) HIP_TRY(hipEventRecord(ev[0], s));
@@ -691,12 +729,12 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
   }
   if (c->accel == RT_ACCEL_OCTREE && !c->d_node) {
     // empty scene: nothing to traverse, the FLAT kernel with 0 records is exact
-    HIP_TRY(hipMemsetAsync(c->d_counter, 0, 64, s));
+    HIP_TRY(hipMemsetAsync(c->d_counter, 0, 8 * 128, s));  // 8 item streams, 128 B apart
     HIP_TRY(hipMemsetAsync(c->d_stats, 0, RT_NSTATS * sizeof(unsigned long long), s));
     if (c->timing) HIP_TRY(hipEventRecord(ev[1], s));
     HIP_TRY(rt_launch_render(&p, RT_ACCEL_FLAT_D, c->count_work, c->policy, c->grid, s));
   } else {
-    HIP_TRY(hipMemsetAsync(c->d_counter, 0, 64, s));
+    HIP_TRY(hipMemsetAsync(c->d_counter, 0, 8 * 128, s));  // 8 item streams, 128 B apart
     HIP_TRY(hipMemsetAsync(c->d_stats, 0, RT_NSTATS * sizeof(unsigned long long), s));
     if (c->timing) HIP_TRY(hipEventRecord(ev[1], s));
     HIP_TRY(rt_launch_render(&p, c->accel, c->count_work, c->policy, c->grid, s));

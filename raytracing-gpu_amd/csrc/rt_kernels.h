@@ -45,14 +45,16 @@ struct KParams {
   rt::f3 u, v, C, pos;  // camera frame (cpu/raytracer.c:82-86)
   int W, H;
   int tiles_x, ntiles_total, rank, nranks, ntiles_local;
-  float* out;                   // rank's tile buffer
-  uint32_t* tile_counter;       // zeroed before launch (one counter)
+  float* out;                   // rank's tile buffer (written by combine_kernel)
+  float* samples;               // ntiles_local x 4 samples x 3 channels x 64 lanes: sample colours
+  uint32_t* tile_counter;       // 8 item-stream counters, 32 words apart; zeroed before launch
   unsigned long long* stats;    // RT_NSTATS counters, zeroed before launch
   uint2* spill;                 // grid*64 lanes x RT_SPILL_STACK stack entries
   rt::f3 scene_c;               // scene box centre
   float scene_cmag;             // max-norm of scene_c
   float scene_r;                // scene box half-extent (max-norm)
   float eps_rel;                // culling slack, rt_cull.h rt_cull_eps()
+  unsigned long long* tile_cycles;  // COUNT pass: shader clocks of each work item (tile, sample) (NULL: none)
   float* terms;                 // (RT_MAX_DEPTH - RT_LDS_TERMS) x grid*64 lanes x 3: deep reflection terms
   // camera-ray candidate lists (csrc/rt_cand.hip); cand_start == NULL: none
   const uint32_t* cand_start;   // ntiles_local + 1 offsets into cand

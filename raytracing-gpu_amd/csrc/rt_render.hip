@@ -156,7 +156,7 @@ __device__ __forceinline__ bool any_hit_rec(const Ray& r, const float4& q0, cons
 // Per-lane traversal stack: the first kLdsStack entries live in LDS, laid
 // out [entry][lane] so every lane hits its own bank; deeper entries spill to
 // a per-lane area in global memory (rare: typical depth is < 16).
-static constexpr int kLdsStack = 9;  // fills the 10 KB/workgroup LDS budget of 16 workgroups per CU
+static constexpr int kLdsStack = 10;  // fills the 10 KB/workgroup LDS budget of 16 workgroups per CU
 static constexpr int kSpillStack = RT_SPILL_STACK;
 
 struct Stack {
@@ -1031,7 +1031,6 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES) void render_kernel(KParams p) {
   __shared__ float4 s_stack[ACCEL == RT_ACCEL_FLAT_D ? 1 : kStackArea];
   __shared__ float4 s_stage[ACCEL == RT_ACCEL_FLAT_D ? kStageFlat : kStageOct];
   __shared__ float s_terms[kLdsTerms * 3 * 64];
-  __shared__ float s_acc[3 * 64];  // the pixel's sample sum (cpu/raytracer.c:60-68)
   const size_t gl = (size_t)blockIdx.x * 64 + (size_t)lane;
   Stack stk;
   stk.idx = (uint32_t*)s_stack;
@@ -1052,49 +1051,55 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES) void render_kernel(KParams p) {
   // counter: all 8 XCDs then work on the same few tile rows, whose geometry
   // stays in the Infinity Cache (measured, C5: 8 per-XCD bands ran 13 %
   // slower).
+  // Work item = (tile t, sample s): the four samples of a tile run on four
+  // waves, so a tile of long mirror paths (C2: the worst tile cost 7.7x a
+  // balanced schedule's whole frame, tools/tile_cost.py) is no longer one
+  // wave's serial critical path.  Items come in 8 streams, stream x = the
+  // tiles t = x (mod 8) in scanline order, 4 items each: workgroup b (on XCD
+  // b mod 8, the dispatcher's round robin) pulls from stream b mod 8, so a
+  // tile's samples share one XCD's L2, all XCDs work on the same few tile
+  // rows (their geometry stays in the Infinity Cache), and the item counters'
+  // atomic traffic is split 8 ways; a drained stream's waves move on to the
+  // next.  Each item writes its sample colour; combine_kernel sums a pixel's
+  // four in the reference's order.
   const uint32_t nt = (uint32_t)p.ntiles_local;
+  const uint32_t home = (uint32_t)blockIdx.x & 7u;
+  uint32_t probe = 0;
   for (;;) {
-    uint32_t t = 0;
-    if (lane == 0) t = atomicAdd(p.tile_counter, 1u);
-    t = uni(t);
-    if (t >= nt) break;  // every tile taken: the wave exits
-    // Pixel state is recomputed per sample from (t, lane) and the pixel's
-    // accumulator lives in LDS, so nothing but the lane id stays live across
-    // a path (in registers, the walks' pressure spilled them to scratch: 72 B
-    // per lane per tile of HBM writes)
-    bool valid = false;
-    for (int smp = 0; smp < 4; smp++) {
-      // an opaque copy of the lane id: keeps the compiler from hoisting the
-      // pixel arithmetic out of the sample loop (and spilling it)
-      int ln = lane;
-      __asm__ volatile("" : "+v"(ln));
-      const uint32_t g = t * (uint32_t)p.nranks + (uint32_t)p.rank;  // global tile index
-      const int ty = (int)(g / (uint32_t)p.tiles_x), tx = (int)(g % (uint32_t)p.tiles_x);
-      const int pr = ty * 8 + (ln >> 3), pc = tx * 8 + (ln & 7);
-      // PPM (row, col) -> framebuffer slot (j, i) of cpu/raytracer.c:71,128-134
-      const int ii = p.W - pc, jj = p.H - pr;
-      valid = pr < p.H && pc < p.W && ii >= 1 && ii <= 2 * (p.W / 2) && jj >= 1 &&
-              jj <= 2 * (p.H / 2);
-      const int i = ii - p.W / 2, j = jj - p.H / 2;
-      if (smp == 0) wc.pixels += (uint32_t)__popcll(__ballot(valid));
-      // for (float k = i; k < i + 1; k += 0.5) for (float l = j; ...)  (cpu/raytracer.c:55-58)
-      const float k = (float)i + 0.5f * (float)(smp >> 1);
-      const float l = (float)j + 0.5f * (float)(smp & 1);
-      f3 point = add(add(p.C, scale(p.u, k)), scale(p.v, l));
-      f3 dir = normalize(sub(p.pos, point));
-      col sc = trace_path<ACCEL, COUNT, POL>(p, valid, point, dir, 1.0f, stk, w, wc, t, T);
-      col a = smp == 0 ? init_color(0.0f, 0.0f, 0.0f) : col{s_acc[lane], s_acc[64 + lane], s_acc[128 + lane]};
-      a = color_add(a, color_mul(sc, 0.25f));
-      s_acc[lane] = a.r;
-      s_acc[64 + lane] = a.g;
-      s_acc[128 + lane] = a.b;
+    const uint32_t x = (home + probe) & 7u;
+    const uint32_t nx = nt > x ? (nt - x + 7u) / 8u : 0u;  // tiles of stream x
+    uint32_t q = 0;
+    if (lane == 0) q = atomicAdd(p.tile_counter + 32u * x, 1u);
+    q = uni(q);
+    if (q >= 4u * nx) {
+      if (++probe == 8u) break;  // every stream drained: the wave exits
+      continue;
     }
-    col acc = col{s_acc[lane], s_acc[64 + lane], s_acc[128 + lane]};
-    if (!valid) acc = col{0.0f, 0.0f, 0.0f};
-    float* out = p.out + ((size_t)t * 64 + (size_t)lane) * 3;
-    out[0] = acc.r;
-    out[1] = acc.g;
-    out[2] = acc.b;
+    const uint32_t u = 4u * (8u * (q >> 2) + x) + (q & 3u);  // item index 4t + s
+    const unsigned long long c0 = COUNT ? __builtin_readcyclecounter() : 0ull;
+    const uint32_t t = u >> 2;
+    const int smp = (int)(u & 3u);
+    const uint32_t g = t * (uint32_t)p.nranks + (uint32_t)p.rank;  // global tile index
+    const int ty = (int)(g / (uint32_t)p.tiles_x), tx = (int)(g % (uint32_t)p.tiles_x);
+    const int pr = ty * 8 + (lane >> 3), pc = tx * 8 + (lane & 7);
+    // PPM (row, col) -> framebuffer slot (j, i) of cpu/raytracer.c:71,128-134
+    const int ii = p.W - pc, jj = p.H - pr;
+    const bool valid = pr < p.H && pc < p.W && ii >= 1 && ii <= 2 * (p.W / 2) && jj >= 1 &&
+                       jj <= 2 * (p.H / 2);
+    const int i = ii - p.W / 2, j = jj - p.H / 2;
+    if (smp == 0) wc.pixels += (uint32_t)__popcll(__ballot(valid));
+    // for (float k = i; k < i + 1; k += 0.5) for (float l = j; ...)  (cpu/raytracer.c:55-58)
+    const float k = (float)i + 0.5f * (float)(smp >> 1);
+    const float l = (float)j + 0.5f * (float)(smp & 1);
+    f3 point = add(add(p.C, scale(p.u, k)), scale(p.v, l));
+    f3 dir = normalize(sub(p.pos, point));
+    col sc = trace_path<ACCEL, COUNT, POL>(p, valid, point, dir, 1.0f, stk, w, wc, t, T);
+    // this item's sample colour, [item][channel][lane] (coalesced)
+    float* so = p.samples + (size_t)u * 192 + lane;
+    so[0] = sc.r;
+    so[64] = sc.g;
+    so[128] = sc.b;
+    if (COUNT && p.tile_cycles && lane == 0) p.tile_cycles[u] = __builtin_readcyclecounter() - c0;
   }
   // the counters are wave totals already: one atomic per counter per wave
   uint32_t v[RT_NSTATS] = {wc.closest, wc.shadow,   wc.pixels,      wc.nodes,
@@ -1103,6 +1108,35 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES) void render_kernel(KParams p) {
 #pragma unroll
   for (int k = 0; k < RT_NSTATS; k++)
     if (lane == 0 && v[k]) atomicAdd(p.stats + k, (unsigned long long)v[k]);
+}
+
+// A pixel's four sample colours (render_kernel items 4t..4t+3) summed in the
+// reference's order: acc = color_add(acc, color_mul(s, 0.25)) for the samples
+// (i,j), (i,j+.5), (i+.5,j), (i+.5,j+.5) (cpu/raytracer.c:55-68); pixels
+// outside the framebuffer's even-sized area are 0.  One thread per pixel.
+__global__ __launch_bounds__(256) void combine_kernel(const float* __restrict__ samples,
+                                                      float* __restrict__ out, uint32_t ntiles,
+                                                      int W, int H, int tiles_x, int rank,
+                                                      int nranks) {
+  const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= ntiles * 64u) return;
+  const uint32_t t = idx >> 6, lane = idx & 63u;
+  const uint32_t g = t * (uint32_t)nranks + (uint32_t)rank;
+  const int ty = (int)(g / (uint32_t)tiles_x), tx = (int)(g % (uint32_t)tiles_x);
+  const int pr = ty * 8 + (int)(lane >> 3), pc = tx * 8 + (int)(lane & 7);
+  const int ii = W - pc, jj = H - pr;
+  const bool valid = pr < H && pc < W && ii >= 1 && ii <= 2 * (W / 2) && jj >= 1 &&
+                     jj <= 2 * (H / 2);
+  col acc = init_color(0.0f, 0.0f, 0.0f);
+  for (int smp = 0; smp < 4; smp++) {
+    const float* si = samples + ((size_t)t * 4 + (size_t)smp) * 192 + lane;
+    acc = color_add(acc, color_mul(col{si[0], si[64], si[128]}, 0.25f));
+  }
+  if (!valid) acc = col{0.0f, 0.0f, 0.0f};
+  float* o = out + (size_t)idx * 3;
+  o[0] = acc.r;
+  o[1] = acc.g;
+  o[2] = acc.b;
 }
 
 // tiles of all ranks (rank-major, as gathered) -> PPM-order image
@@ -1130,6 +1164,14 @@ __global__ __launch_bounds__(256) void assemble_kernel(const float* __restrict__
 // One instantiation per (accel, work counting, policy); the default policy's
 // kernel has no policy switch inside.  The work-counting pass and the test
 // policies are separate kernels, so they cannot slow the default one down.
+static hipError_t launch_combine(const KParams* p, hipStream_t stream) {
+  const uint32_t n = (uint32_t)p->ntiles_local * 64u;
+  if (n == 0) return hipGetLastError();
+  hipLaunchKernelGGL(rt::combine_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, p->samples,
+                     p->out, (uint32_t)p->ntiles_local, p->W, p->H, p->tiles_x, p->rank, p->nranks);
+  return hipGetLastError();
+}
+
 extern "C" hipError_t rt_launch_render(const KParams* p, int accel, int count_work, int policy,
                                        int grid, hipStream_t stream) {
   dim3 g(grid), b(64);
@@ -1138,7 +1180,8 @@ extern "C" hipError_t rt_launch_render(const KParams* p, int accel, int count_wo
       hipLaunchKernelGGL((rt::render_kernel<RT_ACCEL_FLAT_D, true, 0>), g, b, 0, stream, *p);
     else
       hipLaunchKernelGGL((rt::render_kernel<RT_ACCEL_FLAT_D, false, 0>), g, b, 0, stream, *p);
-    return hipGetLastError();
+    hipError_t e = hipGetLastError();
+    return e != hipSuccess ? e : launch_combine(p, stream);
   }
   switch (policy) {
     case RT_POLICY_LANE:
@@ -1161,7 +1204,8 @@ extern "C" hipError_t rt_launch_render(const KParams* p, int accel, int count_wo
         hipLaunchKernelGGL((rt::render_kernel<RT_ACCEL_OCTREE_D, false, RT_POLICY_DEFAULT>), g, b, 0,
                            stream, *p);
   }
-  return hipGetLastError();
+  hipError_t e = hipGetLastError();
+  return e != hipSuccess ? e : launch_combine(p, stream);
 }
 
 extern "C" hipError_t rt_launch_assemble(const float* tiles, float* rgb, int W, int H, int tiles_x,

@@ -141,6 +141,7 @@ _PROTOS = [
     ("rt_hip_set_cull_slack", C.c_int, [C.c_void_p, C.c_float]),
     ("rt_hip_set_exact_camera", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_set_policy", C.c_int, [C.c_void_p, C.c_int]),
+    ("rt_hip_tile_cycles", C.c_int, [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_size_t]),
     ("rt_hip_set_timing", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_frame_times", C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_float),
                                      C.POINTER(C.c_float)]),
@@ -382,6 +383,13 @@ class Context:
         a, b = (C.c_float * n)(), (C.c_float * n)()
         _check(lib().rt_hip_frame_times(self.h, n, a, b), "frame_times")
         return list(zip(a, b))
+
+    def tile_cycles(self, n):
+        """Per-tile shader clocks of the last instrumented render (numpy uint64)."""
+        out = np.zeros(n, dtype=np.uint64)
+        _check(lib().rt_hip_tile_cycles(self.h, out.ctypes.data_as(C.POINTER(C.c_ulonglong)), n),
+               "tile_cycles")
+        return out
 
     def set_policy(self, policy):
         """Octree traversal policy (rt_hip_set_policy): 0 default, 1 per-lane,

@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Per-tile cost distribution of one frame (instrumented render kernel,
+rt_hip_tile_cycles): how unevenly the 8x8 tiles cost, and the tail a
+persistent-wave schedule can not hide.
+
+    python tools/tile_cost.py --scene spheres --W 1920 --H 1080 [--accel octree]
+    python tools/tile_cost.py --synthetic 32 --W 3840 --H 2160
+"""
+import argparse
+import gzip
+import json
+import os
+import sys
+import tempfile
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "raytracing-gpu_amd"))
+import rtgpu  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scene", default=None)
+    ap.add_argument("--synthetic", type=int, default=0)
+    ap.add_argument("--W", type=int, default=1920)
+    ap.add_argument("--H", type=int, default=1080)
+    ap.add_argument("--accel", default="octree")
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    if a.synthetic:
+        s = rtgpu.Scene.synthetic(a.synthetic, a.synthetic, 9776, seed=0x5EED, width=a.W, height=a.H)
+    else:
+        src = os.path.join(REPO, "tests", "golden", "scenes", a.scene + ".svati.gz")
+        with tempfile.TemporaryDirectory() as td:
+            p = os.path.join(td, "s.svati")
+            with gzip.open(src, "rb") as i, open(p, "wb") as o:
+                o.write(i.read())
+            s = rtgpu.Scene.load_svati(p)
+        s.set_size(a.W, a.H)
+    ctx = rtgpu.Context(s, a.accel)
+    ctx.set_count_work(True)
+    f = s.frame()
+    img, st = ctx.render_image(f)
+    tx, ty = (a.W + 7) // 8, (a.H + 7) // 8
+    items = ctx.tile_cycles(4 * tx * ty).astype(np.float64)  # item 4t + s = (tile t, sample s)
+    c = items.reshape(-1, 4).sum(axis=1)
+    order = np.argsort(-c)
+    tot = c.sum()
+    res = {
+        "tiles": int(len(c)), "total_clocks": tot, "mean": c.mean(), "max": c.max(),
+        "p50": float(np.percentile(c, 50)), "p99": float(np.percentile(c, 99)),
+        "max_over_mean": c.max() / c.mean(),
+        "top1pct_share": float(c[order[: max(1, len(c) // 100)]].sum() / tot),
+        # a persistent schedule of 4096 waves cannot finish before its most
+        # expensive work item (one sample of a tile), nor before total / 4096
+        "max_item": items.max(),
+        "bound_tail_over_balanced": items.max() / (tot / 4096.0),
+        "worst_tiles_rc": [[int(i // tx), int(i % tx)] for i in order[:10]],
+        "stats": st,
+    }
+    print(json.dumps(res, default=float))
+    if a.out:
+        with open(a.out, "w") as fh:
+            json.dump(res, fh, default=float, indent=1)
+
+
+if __name__ == "__main__":
+    main()
