@@ -29,7 +29,9 @@ enum {
   RT_EHIP = -5,      /* HIP runtime error (device alloc, launch, copy)   */
   RT_ENODEV = -6,    /* no usable gfx950 device                          */
   RT_EDEPTH = -7,    /* a path exceeded the reflection-depth buffer      */
-  RT_ERCCL = -8      /* RCCL collective failed                           */
+  RT_ERCCL = -8,     /* RCCL collective failed                           */
+  RT_EZERONORMAL = -9 /* a closest hit had an exactly zero interpolated normal:
+                       * cpu/hit.c:79 skips that object, which is not reproduced */
 };
 
 const char *rt_strerror(int code);

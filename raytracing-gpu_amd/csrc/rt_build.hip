@@ -15,11 +15,11 @@
 //              that cell -- so its references sit deep in the tree instead of
 //              inflating every ancestor box (the reference's own rule leaves
 //              42-51 % of triangles near the root).
-//   2. scan    hipcub exclusive sum of the counts -> reference offsets.
+//   2. scan    rocPRIM exclusive scan of the counts -> reference offsets.
 //   3. emit    63-bit Morton key (21 levels x 3 bits, octant bit a = upper
 //              half of axis a, as rt_cull.h), triangle id and clipped box per
 //              reference.
-//   4. sort    hipcub radix sort of (key, reference) pairs, stable.
+//   4. sort    rocPRIM radix sort of (key, reference) pairs, stable.
 //   5. split   breadth-first, one thread per pending node: a node whose
 //              range holds <= leaf_cap references (or is at level 21) is a
 //              leaf, otherwise levels where the whole range shares one octant
@@ -35,7 +35,8 @@
 // some Lc cell it is referenced in, inside that reference's clipped box,
 // inside every ancestor's box.  Deterministic: stable sort, scans, no atomics.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
+#include <cstring>  // before rocPRIM (its texture-cache iterator uses memset)
+#include <rocprim/rocprim.hpp>
 
 #include <cfloat>
 #include <cmath>
@@ -382,9 +383,9 @@ extern "C" hipError_t rt_device_build_octree(const float4* d_rec, uint32_t ntri,
   BTRY(hipMemsetAsync(cnt + ntri, 0, 4, s));
   hipLaunchKernelGGL(k_count, dim3(blocks(ntri)), dim3(256), 0, s, p, cnt);
   BTRY(hipGetLastError());
-  BTRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt, off, ntri + 1, s));
+  BTRY(rocprim::exclusive_scan(nullptr, tmp_bytes, cnt, off, 0u, (size_t)(ntri + 1), rocprim::plus<uint32_t>(), s));
   BTRY(hipMalloc(&tmp, tmp_bytes));
-  BTRY(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cnt, off, ntri + 1, s));
+  BTRY(rocprim::exclusive_scan(tmp, tmp_bytes, cnt, off, 0u, (size_t)(ntri + 1), rocprim::plus<uint32_t>(), s));
   BTRY(hipMemcpyAsync(&nref, off + ntri, 4, hipMemcpyDeviceToHost, s));
   BTRY(hipStreamSynchronize(s));
   BTRY(hipFree(tmp));
@@ -400,11 +401,9 @@ extern "C" hipError_t rt_device_build_octree(const float4* d_rec, uint32_t ntri,
   hipLaunchKernelGGL(k_emit, dim3(blocks(ntri)), dim3(256), 0, s, p, off, key, ref, ref_prim, ref_box);
   BTRY(hipGetLastError());
   tmp_bytes = 0;
-  BTRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, key, key2, ref, ref2, nref, 0,
-                                          3 * kLevels, s));
+  BTRY(rocprim::radix_sort_pairs(nullptr, tmp_bytes, key, key2, ref, ref2, (size_t)nref, 0u, 3u * kLevels, s));
   BTRY(hipMalloc(&tmp, tmp_bytes));
-  BTRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, key, key2, ref, ref2, nref, 0,
-                                          3 * kLevels, s));
+  BTRY(rocprim::radix_sort_pairs(tmp, tmp_bytes, key, key2, ref, ref2, (size_t)nref, 0u, 3u * kLevels, s));
   BTRY(hipFree(tmp));
   tmp = nullptr;
   BTRY(hipFree(cnt));
@@ -427,7 +426,7 @@ extern "C" hipError_t rt_device_build_octree(const float4* d_rec, uint32_t ntri,
     BTRY(hipMemcpyAsync(pa, &root, sizeof root, hipMemcpyHostToDevice, s));
     uint32_t np = 1;
     tmp_bytes = 0;
-    BTRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, nch, coff, nref + 2, s));
+    BTRY(rocprim::exclusive_scan(nullptr, tmp_bytes, nch, coff, 0u, (size_t)(nref + 2), rocprim::plus<uint32_t>(), s));
     BTRY(hipMalloc(&tmp, tmp_bytes));
     while (np > 0) {
       hipLaunchKernelGGL(k_split, dim3(blocks(np)), dim3(256), 0, s, pa, np, key2, leaf_cap, split,
@@ -435,7 +434,7 @@ extern "C" hipError_t rt_device_build_octree(const float4* d_rec, uint32_t ntri,
       BTRY(hipGetLastError());
       BTRY(hipMemsetAsync(nch + np, 0, 4, s));
       size_t tb = tmp_bytes;
-      BTRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, nch, coff, np + 1, s));
+      BTRY(rocprim::exclusive_scan(tmp, tb, nch, coff, 0u, (size_t)(np + 1), rocprim::plus<uint32_t>(), s));
       uint32_t nnext = 0;
       BTRY(hipMemcpyAsync(&nnext, coff + np, 4, hipMemcpyDeviceToHost, s));
       hipLaunchKernelGGL(k_link, dim3(blocks(np)), dim3(256), 0, s, pa, np, split, lvl, nch, coff,

@@ -774,6 +774,12 @@ extern "C" int rt_hip_stats(rt_hip_ctx* c, rt_stats* out) {
   if (out->depth_overflow)
     return rt_set_error(RT_EDEPTH, "%llu paths overflowed the depth/stack buffers",
                         out->depth_overflow);
+  // never silent: the image may differ from cpu/rt's there
+  if (out->zero_normal)
+    return rt_set_error(RT_EZERONORMAL,
+                        "%llu closest hits had an exactly zero interpolated normal (cpu/hit.c:79 "
+                        "would skip those objects)",
+                        out->zero_normal);
   return RT_OK;
 }
 

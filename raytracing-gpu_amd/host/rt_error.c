@@ -19,6 +19,7 @@ const char *rt_strerror(int code)
   case RT_ENODEV: return "no usable gfx950 device";
   case RT_EDEPTH: return "reflection depth buffer overflow";
   case RT_ERCCL: return "RCCL error";
+  case RT_EZERONORMAL: return "zero interpolated normal (cpu/hit.c:79 not reproduced)";
   default: return "unknown error";
   }
 }

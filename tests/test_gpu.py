@@ -302,3 +302,17 @@ def test_exact_camera_rank_split(gpu):
         t, st = _tiles_of_rank(ctx, f, rank, 3)
         ref = gpu.tiles_from_image_numpy(img_f, rank, 3)
         assert_bitexact(t, ref[: len(t)], f"rank {rank}/3")
+
+
+def test_zero_normal_is_an_error(gpu, tmp_path):
+    """cpu/hit.c:79 skips an object whose closest hit has an exactly zero
+    interpolated normal; that rule is not reproduced, so a render that meets
+    it must fail loudly (RT_EZERONORMAL from rt_hip_stats), never write a
+    silently different image."""
+    sv = tmp_path / "zn.svati"
+    sv.write_text("camera 32 32 0 0 -5 1 0 0 0 -1 0 60\na_light 1 1 1\n\nobject 3\nKa 1 1 1\n"
+                  "v -2 -2 0\nv 2 -2 0\nv 0 2 0\nvn 0 0 0\nvn 0 0 0\nvn 0 0 0\n")
+    s = gpu.Scene.load_svati(str(sv))
+    with pytest.raises(gpu.RtError) as e:
+        gpu.Context(s, "flat").render_image(s.frame())
+    assert e.value.code == -9
