@@ -185,6 +185,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cull-slack", type=float, default=None,
                     help="octree culling slack override (tuning; default = library default)")
+    ap.add_argument("--camera-slack", type=float, default=None,
+                    help="camera-ray culling slack override (tuning; default = library default)")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary (tools/pmc_traffic.py) to report as roofline.traffic")
     ap.add_argument("--valu-json", default=None,
@@ -210,6 +212,8 @@ def main():
     ctx = rtgpu.Context(scene, wl["accel"], device=local)
     if args.cull_slack is not None:
         ctx.set_cull_slack(args.cull_slack)
+    if args.camera_slack is not None:
+        ctx.set_camera_slack(args.camera_slack)
     info = ctx.info()
     log(f"[rank {rank}] scene {ntri} triangles, accel {wl['accel']}: {info['tri_refs']} records, "
         f"{info['nodes']} nodes, build {info['build_seconds']:.1f}s, setup {time.perf_counter()-t:.1f}s")
@@ -280,6 +284,11 @@ def main():
     el, kern_ms, lists_ms = tt.tolist()
 
     queries = closest + shadow
+    cyc = [float(work[k]) for k in ("cycles_camera", "cycles_cand", "cycles_secondary",
+                                    "cycles_shadow")]
+    phase_share = ({k: round(v / sum(cyc), 4) for k, v in
+                    zip(("camera_walk", "camera_candidates", "secondary_walks", "shadow_queries"), cyc)}
+                   if sum(cyc) > 0 else None)
     value = queries * args.steps / el / 1e6
     # algorithmic bytes of one render launch (per rank, averaged over ranks)
     alg_bytes = (wq * RAY_BYTES + nodes * NODE_BYTES + tris * TRI_BYTES + whits * NORMAL_BYTES +
@@ -288,7 +297,8 @@ def main():
     achieved = per_launch / (kern_ms * 1e-3) / 1e9
     traffic = traffic_hi = None
     traffic_src = None
-    if world == 1 and args.traffic_json is None and args.cull_slack is None:
+    if world == 1 and args.traffic_json is None and args.cull_slack is None and \
+            args.camera_slack is None:
         # default run: the newest committed rocprofv3 PMC pass of this
         # workload (profiles/r*_<workload>/, tools/gpu_profile.sh); a PMC
         # pass cannot run inside the bench, so the line says where it came from
@@ -394,6 +404,8 @@ def main():
                                              whits * NORMAL_BYTES + pixels * PIXEL_BYTES) / world),
                 },
                 "candidate_entries": int(cand_entries),
+                # instrumented pass: share of the waves' clocks per phase
+                "phase_share": phase_share,
             },
             "valu": valu,
             "cpu_baseline": cpu,

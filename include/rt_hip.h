@@ -69,6 +69,10 @@ typedef struct rt_stats {
    * it once), for closest-hit and for shadow queries */
   unsigned long long closest_node_lanes, closest_tri_lanes;
   unsigned long long shadow_node_lanes, shadow_tri_lanes;
+  /* instrumented pass: shader clocks the waves spent in the camera-ray walk,
+   * the camera candidate tests, the secondary closest-hit walks and the
+   * shadow queries (summed over waves) */
+  unsigned long long cycles_camera, cycles_cand, cycles_secondary, cycles_shadow;
 } rt_stats;
 
 /* Sizes of the device-side scene image, for the roofline accounting. */
@@ -137,6 +141,11 @@ int rt_hip_stats(rt_hip_ctx *ctx, rt_stats *out);
  * culling").  Default RT_EPS_ULPS_DEFAULT (64).  Tuning knob: smaller is
  * faster and risks parity on grazing rays. */
 int rt_hip_set_cull_slack(rt_hip_ctx *ctx, float ulps);
+/* The same slack for camera rays only (bounce depth 0; rt_hip_set_cull_slack
+ * sets both).  A wider camera slack costs a few more node visits and lets
+ * the walk find triangles the per-frame candidate lists would otherwise have
+ * to carry; exactness holds for every value. */
+int rt_hip_set_camera_slack(rt_hip_ctx *ctx, float ulps);
 /* Phase timing: with enable, every rt_hip_render records HIP events on its
  * stream before the camera candidate lists, before the render kernel and
  * after it (a ring of the last 1024 frames; enabling clears it).

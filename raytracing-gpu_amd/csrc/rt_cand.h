@@ -44,7 +44,7 @@ struct CandParams {
   uint32_t* vals;         // entries: prim
   uint32_t* global;       // nprim: prims whose footprint is unbounded
   uint32_t* ctr;          // [1] global prims, [2] big footprints, [3] list length
-  uint32_t* big;          // nprim: list entries with more than kBig tile entries
+  uint32_t* big;          // nprim: list entries with big footprints (rt_cand.hip kSmallRows)
   float* skip;            // nprim: depth-skip bound of each listed prim
 };
 
@@ -67,6 +67,8 @@ extern "C" hipError_t rt_cand_quick(const CandParams* p, hipStream_t s);
 extern "C" hipError_t rt_cand_scatter(const CandParams* p, hipStream_t s);
 extern "C" hipError_t rt_cand_count(const CandParams* p, hipStream_t s);
 extern "C" size_t rt_cand_footprint_bytes(void);
+// pass 1b: tile counts of the big footprints (one wave each)
+extern "C" hipError_t rt_cand_big_count(const CandParams* p, hipStream_t s);
 extern "C" hipError_t rt_cand_emit(const CandParams* p, hipStream_t s);
 extern "C" hipError_t rt_cand_big(const CandParams* p, uint32_t nbig, hipStream_t s);
 extern "C" hipError_t rt_cand_scan(const uint32_t* in, uint32_t* out, uint32_t n, void* temp,

@@ -506,8 +506,16 @@ __host__ __device__ inline uint32_t raster_count(const CandParams& p, const Foot
   return n;
 }
 
-// footprints with more entries than this are emitted by a whole workgroup
-constexpr uint32_t kBig = 512;
+// A footprint is "big" -- counted and emitted by one wave, its tile rows
+// spread over the lanes -- when it spans more than kSmallRows tile rows or
+// has more than kSmallEntries entries; the others are counted and emitted by
+// one thread each.  (A thread per footprint of hundreds of entries stalled
+// its whole wave: count 2.6 ms, emit 1.4 ms on C5 before the split.)
+constexpr int kSmallRows = 2;
+constexpr uint32_t kSmallEntries = 32;
+// persistent waves of the big-footprint passes (they loop over the big list,
+// whose length only the device knows before the scan)
+constexpr int kBigWaves = 4096;
 
 // Pass 0: the float fast path over every prim; flags the prims it cannot
 // prove safe (visits[prim] = 1), which an exclusive scan and scatter_kernel
@@ -529,8 +537,19 @@ __global__ __launch_bounds__(256) void scatter_kernel(CandParams p) {
   if (p.visits[prim]) p.list[p.off[prim]] = prim;
 }
 
-// Pass 1: classify the listed prims, keep each one's footprint and count its
-// tiles (visits[j] for list entry j; visits is zero beyond the list).
+// small footprint: few tile rows, counted here row by row; false: big
+__host__ __device__ inline bool small_count(const CandParams& p, const Footprint& fp, uint32_t& n) {
+  int r0, r1;
+  n = 0;
+  if (!raster_rows(p, fp, r0, r1)) return true;
+  if ((r1 >> 3) - (r0 >> 3) + 1 > kSmallRows) return false;
+  for (int ty = r0 >> 3; ty <= (r1 >> 3); ty++) n += count_row(p, fp, ty, r0, r1);
+  return n <= kSmallEntries;
+}
+
+// Pass 1: classify the listed prims, keep each one's footprint and count the
+// tiles of the small ones (visits[j] for list entry j; visits is zero beyond
+// the list); big ones are queued for big_count_kernel.
 __global__ __launch_bounds__(256) void count_kernel(CandParams p) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= p.ctr[3]) return;
@@ -544,24 +563,61 @@ __global__ __launch_bounds__(256) void count_kernel(CandParams p) {
     p.global[atomicAdd(p.ctr + 1, 1u)] = prim;
     p.skip[prim] = -1e30f;
   } else if (c == FOOTPRINT) {
-    visits = raster_count(p, fp);
     p.skip[prim] = fp.skip;
-    if (visits) p.fp[j] = fp;
-    if (visits > kBig) p.big[atomicAdd(p.ctr + 2, 1u)] = j;
+    if (small_count(p, fp, visits)) {
+      if (visits) p.fp[j] = fp;
+    } else {
+      p.fp[j] = fp;
+      p.big[atomicAdd(p.ctr + 2, 1u)] = j;
+      visits = 0;  // big_count_kernel
+    }
   }
   p.visits[j] = visits;
 }
 
-// Pass 2 (after the scan of visits): the listed prims write their (tile,
-// prim) pairs at their offsets.
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+  return x;
+}
+
+// exclusive prefix sum over the 64 lanes of a wave
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, int lane) {
+  uint32_t inc = x;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  return inc - x;
+}
+
+// Pass 1b: one wave per big footprint, its tile rows over the lanes.
+__global__ __launch_bounds__(64) void big_count_kernel(CandParams p) {
+  const int lane = threadIdx.x;
+  const uint32_t nbig = p.ctr[2];
+  for (uint32_t b = blockIdx.x; b < nbig; b += gridDim.x) {
+    const uint32_t j = p.big[b];
+    const Footprint fp = p.fp[j];
+    int r0, r1;
+    uint32_t cnt = 0;
+    if (raster_rows(p, fp, r0, r1))
+      for (int ty = (r0 >> 3) + lane; ty <= (r1 >> 3); ty += 64) cnt += count_row(p, fp, ty, r0, r1);
+    cnt = wave_sum(cnt);
+    if (lane == 0) p.visits[j] = cnt;
+  }
+}
+
+// Pass 2 (after the scan of visits): the small footprints write their
+// (tile, prim) pairs at their offsets.
 __global__ __launch_bounds__(256) void emit_kernel(CandParams p) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= p.ctr[3]) return;
   uint32_t o = p.off[j];
   const uint32_t n = p.off[j + 1] - o;
-  if (n == 0 || n > kBig) return;  // big footprints: big_kernel
-  const uint32_t prim = p.list[j];
+  if (n == 0 || n > kSmallEntries) return;  // big footprints: big_kernel
   const Footprint fp = p.fp[j];
+  int r0, r1;
+  if (!raster_rows(p, fp, r0, r1) || (r1 >> 3) - (r0 >> 3) + 1 > kSmallRows) return;
+  const uint32_t prim = p.list[j];
   raster(p, fp, [&](uint32_t t) {
     p.keys[o] = t;
     p.vals[o] = prim;
@@ -569,34 +625,29 @@ __global__ __launch_bounds__(256) void emit_kernel(CandParams p) {
   });
 }
 
-// One workgroup per big footprint: its tile rows are spread over the
-// threads, a block scan places each thread's entries.
-__global__ __launch_bounds__(256) void big_kernel(CandParams p) {
-  const uint32_t j = p.big[blockIdx.x], prim = p.list[j];
-  const Footprint fp = p.fp[j];
-  int r0 = 0, r1 = -1;
-  const bool rows = raster_rows(p, fp, r0, r1);
-  const int ty0 = r0 >> 3, ty1 = r1 >> 3, tid = threadIdx.x;
-  uint32_t cnt = 0;
-  if (rows)
-    for (int ty = ty0 + tid; ty <= ty1; ty += 256) cnt += count_row(p, fp, ty, r0, r1);
-  __shared__ uint32_t sh[256];
-  sh[tid] = cnt;
-  __syncthreads();
-  for (int off = 1; off < 256; off <<= 1) {  // inclusive Hillis-Steele scan
-    const uint32_t y = tid >= off ? sh[tid - off] : 0u;
-    __syncthreads();
-    sh[tid] += y;
-    __syncthreads();
+// Pass 2b: one wave per big footprint; each lane emits its tile rows at the
+// offset a wave prefix sum of the lanes' counts gives it.
+__global__ __launch_bounds__(64) void big_kernel(CandParams p) {
+  const int lane = threadIdx.x;
+  const uint32_t nbig = p.ctr[2];
+  for (uint32_t b = blockIdx.x; b < nbig; b += gridDim.x) {
+    const uint32_t j = p.big[b], prim = p.list[j];
+    const Footprint fp = p.fp[j];
+    int r0 = 0, r1 = -1;
+    const bool rows = raster_rows(p, fp, r0, r1);
+    const int ty0 = r0 >> 3, ty1 = r1 >> 3;
+    uint32_t cnt = 0;
+    if (rows)
+      for (int ty = ty0 + lane; ty <= ty1; ty += 64) cnt += count_row(p, fp, ty, r0, r1);
+    uint32_t o = p.off[j] + wave_excl_scan(cnt, lane);
+    if (rows)
+      for (int ty = ty0 + lane; ty <= ty1; ty += 64)
+        raster_row(p, fp, ty, r0, r1, [&](uint32_t t) {
+          p.keys[o] = t;
+          p.vals[o] = prim;
+          o++;
+        });
   }
-  uint32_t o = p.off[j] + sh[tid] - cnt;
-  if (rows)
-    for (int ty = ty0 + tid; ty <= ty1; ty += 256)
-      raster_row(p, fp, ty, r0, r1, [&](uint32_t t) {
-        p.keys[o] = t;
-        p.vals[o] = prim;
-        o++;
-      });
 }
 
 __global__ __launch_bounds__(256) void prim_leaf_kernel(const float4* node, uint32_t nnode,
@@ -722,6 +773,12 @@ extern "C" hipError_t rt_cand_count(const CandParams* p, hipStream_t s) {
   return hipGetLastError();
 }
 
+extern "C" hipError_t rt_cand_big_count(const CandParams* p, hipStream_t s) {
+  if (p->nprim == 0) return hipSuccess;
+  hipLaunchKernelGGL(rtc::big_count_kernel, dim3(rtc::kBigWaves), dim3(64), 0, s, *p);
+  return hipGetLastError();
+}
+
 extern "C" hipError_t rt_cand_emit(const CandParams* p, hipStream_t s) {
   if (p->nprim == 0) return hipSuccess;
   hipLaunchKernelGGL(rtc::emit_kernel, dim3((p->nprim + 255) / 256), dim3(256), 0, s, *p);
@@ -730,7 +787,8 @@ extern "C" hipError_t rt_cand_emit(const CandParams* p, hipStream_t s) {
 
 extern "C" hipError_t rt_cand_big(const CandParams* p, uint32_t nbig, hipStream_t s) {
   if (nbig == 0) return hipSuccess;
-  hipLaunchKernelGGL(rtc::big_kernel, dim3(nbig), dim3(256), 0, s, *p);
+  const uint32_t g = nbig < (uint32_t)rtc::kBigWaves ? nbig : (uint32_t)rtc::kBigWaves;
+  hipLaunchKernelGGL(rtc::big_kernel, dim3(g), dim3(64), 0, s, *p);
   return hipGetLastError();
 }
 

@@ -28,6 +28,12 @@ extern "C" {
 #ifndef RT_EPS_ULPS_DEFAULT
 #define RT_EPS_ULPS_DEFAULT 64
 #endif
+// camera rays (bounce depth 0): a wider slack lets the walk itself find most
+// triangles whose float-MT error region is beyond the secondary rays' slack,
+// so far fewer go through the per-frame candidate lists
+#ifndef RT_CAM_EPS_ULPS_DEFAULT
+#define RT_CAM_EPS_ULPS_DEFAULT 64
+#endif
 
 #define HIP_TRY(expr)                                                                    \
   do {                                                                                   \
@@ -58,6 +64,7 @@ struct rt_hip_ctx {
   rt_accel_info info{};
   float scene_c[3]{}, scene_r = 0;
   float eps_ulps = RT_EPS_ULPS_DEFAULT;
+  float cam_eps_ulps = RT_CAM_EPS_ULPS_DEFAULT;
   int policy = RT_POLICY_DEFAULT;  // traversal policy (tests / A/B only: rt_hip_set_policy)
   float* d_terms = nullptr;        // deep reflection terms (KParams::terms)
   unsigned long long* d_tile_cycles = nullptr;  // COUNT pass: per-item clocks
@@ -322,6 +329,13 @@ extern "C" int rt_hip_accel_validate(const rt_hip_ctx* c) {
 extern "C" int rt_hip_set_cull_slack(rt_hip_ctx* c, float ulps) {
   if (!c || !(ulps >= 0.0f)) return rt_set_error(RT_EINVAL, "bad slack");
   c->eps_ulps = ulps;
+  c->cam_eps_ulps = ulps;
+  return RT_OK;
+}
+
+extern "C" int rt_hip_set_camera_slack(rt_hip_ctx* c, float ulps) {
+  if (!c || !(ulps >= 0.0f)) return rt_set_error(RT_EINVAL, "bad slack");
+  c->cam_eps_ulps = ulps;
   return RT_OK;
 }
 
@@ -558,7 +572,8 @@ static int ensure_tmp(rt_hip_ctx* c, size_t bytes) {
 // order is deterministic.
 static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream_t s) {
   CandParams cp;
-  int rc = cand_params(f, c->scene_c, c->scene_r, c->eps_ulps, c->bound_scale, kp->rank, kp->nranks, &cp);
+  int rc = cand_params(f, c->scene_c, c->scene_r, c->cam_eps_ulps, c->bound_scale, kp->rank, kp->nranks,
+                       &cp);
   if (rc) return rc;
   cp.tri = c->d_tri_prim;
   cp.nprim = c->nprim;
@@ -609,6 +624,7 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
   HIP_TRY(hipMemsetAsync(c->d_cand_visits, 0, (np + 1) * sizeof(uint32_t), s));
   // pass 1: footprints and tile counts of the listed prims
   HIP_TRY(rt_cand_count(&cp, s));
+  HIP_TRY(rt_cand_big_count(&cp, s));
   tb = c->scan_tmp_bytes;
   HIP_TRY(rt_cand_scan(c->d_cand_visits, c->d_cand_off, (uint32_t)np, c->d_scan_tmp, &tb, s));
   HIP_TRY(hipMemcpyAsync(c->h_cand, c->d_cand_off + np, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
@@ -699,6 +715,7 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
   // culling slack: eps_ulps ulps of the origin-to-geometry distance
   // (DESIGN.md "Conservative culling")
   p.eps_rel = c->eps_ulps * 5.9604645e-8f;
+  p.eps_rel_cam = c->cam_eps_ulps * 5.9604645e-8f;
   p.terms = c->d_terms;
   if ((size_t)p.ntiles_local > c->samples_cap) {
     (void)hipFree(c->d_samples);
@@ -768,6 +785,10 @@ extern "C" int rt_hip_stats(rt_hip_ctx* c, rt_stats* out) {
   out->closest_tri_lanes = h[9];
   out->shadow_node_lanes = h[10];
   out->shadow_tri_lanes = h[11];
+  out->cycles_camera = h[12];
+  out->cycles_cand = h[13];
+  out->cycles_secondary = h[14];
+  out->cycles_shadow = h[15];
   out->cand_prims = c->cand_prims;
   out->cand_entries = c->cand_entries;
   out->cand_global = c->cand_global;

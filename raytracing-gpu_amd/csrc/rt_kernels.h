@@ -12,7 +12,7 @@
 #define RT_MAT_FLOATS_D 12
 #define RT_LIGHT_FLOATS_D 8
 #define RT_MAX_DEPTH 32
-#define RT_NSTATS 12
+#define RT_NSTATS 16
 // per-lane global overflow area of the traversal stack (entries beyond LDS)
 #define RT_SPILL_STACK 112
 // reflection terms of a path kept in LDS (deeper ones: KParams::terms)
@@ -33,6 +33,10 @@ struct WorkCount {
   // per-lane node visits / triangle tests of closest-hit and shadow queries
   // (COUNT pass): a record tested by k lanes counts k times
   uint32_t cl_nodes, cl_tris, sh_nodes, sh_tris;
+  // COUNT pass: shader clocks a wave spent in the camera-ray walk, the
+  // camera candidate tests, the secondary closest-hit walks and the shadow
+  // queries (wall clock of the wave, so shares of its time)
+  uint32_t cy_cam, cy_cand, cy_sec, cy_shadow;
 };
 
 struct KParams {
@@ -54,6 +58,7 @@ struct KParams {
   float scene_cmag;             // max-norm of scene_c
   float scene_r;                // scene box half-extent (max-norm)
   float eps_rel;                // culling slack, rt_cull.h rt_cull_eps()
+  float eps_rel_cam;            // the same for camera rays (bounce depth 0)
   unsigned long long* tile_cycles;  // COUNT pass: shader clocks of each work item (tile, sample) (NULL: none)
   float* terms;                 // (RT_MAX_DEPTH - RT_LDS_TERMS) x grid*64 lanes x 3: deep reflection terms
   // camera-ray candidate lists (csrc/rt_cand.hip); cand_start == NULL: none

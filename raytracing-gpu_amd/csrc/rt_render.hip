@@ -62,12 +62,12 @@ struct Ray {
   f3 oh, ol;   // o + eps, o - eps: the grown slab planes' offsets (rt_cull.h)
 };
 
-__device__ __forceinline__ Ray make_ray(const KParams& p, f3 o, f3 d) {
+__device__ __forceinline__ Ray make_ray(const KParams& p, f3 o, f3 d, float eps_rel) {
   Ray r;
   r.o = o;
   r.d = d;
   r.dlen = length(d);
-  r.eps = rt_cull_eps(p.eps_rel, o.x - p.scene_c.x, o.y - p.scene_c.y, o.z - p.scene_c.z,
+  r.eps = rt_cull_eps(eps_rel, o.x - p.scene_c.x, o.y - p.scene_c.y, o.z - p.scene_c.z,
                       p.scene_cmag, p.scene_r);
   r.oh = f3{o.x + r.eps, o.y + r.eps, o.z + r.eps};
   r.ol = f3{o.x - r.eps, o.y - r.eps, o.z - r.eps};
@@ -777,7 +777,7 @@ __device__ __forceinline__ bool shadow_q(const KParams& p, f3 o, f3 d, uint32_t 
                                          Stack& s, WaveCtx& w, WorkCount& wc) {
   uint64_t am = __ballot(act);
   wc.shadow += (uint32_t)__popcll(am);
-  Ray r = make_ray(p, o, d);
+  Ray r = make_ray(p, o, d, p.eps_rel);
   if (ACCEL == RT_ACCEL_FLAT_D) return flat_any_w<COUNT>(p, r, act, w, wc);
   bool staged = POL == RT_POLICY_STAGED ||
                 (POL == RT_POLICY_DIR_STAGED && type == 1 && __popcll(am) >= kPacketMin);
@@ -848,7 +848,9 @@ __device__ col apply_light(const KParams& p, bool hit, const float* m, f3 P, f3 
     if (type == 0) {  // AMBIENT
       if (hit) acc = color_add(acc, color_mul2(lc, init_color(m[0], m[1], m[2])));
     } else if (type == 1 || type == 2) {
+      const uint64_t c0 = COUNT ? __builtin_readcyclecounter() : 0ull;
       bool sh = shadow_q<ACCEL, COUNT, POL>(p, P, shadow_dir(type, lv, P), type, hit, s, w, wc);
+      if (COUNT) wc.cy_shadow += (uint32_t)(__builtin_readcyclecounter() - c0);
       if (hit && !sh) acc = color_add(acc, light_lit(type, lc, lv, m, P, N));
     }
   }
@@ -972,12 +974,13 @@ __device__ __forceinline__ col trace_path(const KParams& p, bool valid, f3 o, f3
                                           Terms& T) {
   int depth = 0;
   bool alive = valid;
+  bool first = true;  // wave-uniform: the camera query (bounce depth 0)
   for (;;) {
     alive = alive && !((double)coef < 0.01);  // checked before the query
     uint64_t am = __ballot(alive);
     if (am == 0) break;
     wc.closest += (uint32_t)__popcll(am);  // wave-uniform counters (SGPRs)
-    Ray r = make_ray(p, o, d);
+    Ray r = make_ray(p, o, d, first ? p.eps_rel_cam : p.eps_rel);
     Best b;
     b.dist = __builtin_inff();
     b.t_cut = __builtin_inff();
@@ -985,8 +988,16 @@ __device__ __forceinline__ col trace_path(const KParams& p, bool valid, f3 o, f3
     b.obj = 0;
     b.u = b.v = 0.0f;
     b.t = 0.0f;
+    uint64_t c0 = COUNT ? __builtin_readcyclecounter() : 0ull;
     closest_q<ACCEL, COUNT, POL>(p, r, alive, depth, b, s, w, wc);
-    if (ACCEL != RT_ACCEL_FLAT_D && depth == 0) cand_closest<COUNT>(p, r, alive, tile, b, w, wc);
+    if (COUNT) {
+      const uint64_t c1 = __builtin_readcyclecounter();
+      (first ? wc.cy_cam : wc.cy_sec) += (uint32_t)(c1 - c0);
+      c0 = c1;
+    }
+    if (ACCEL != RT_ACCEL_FLAT_D && first) cand_closest<COUNT>(p, r, alive, tile, b, w, wc);
+    if (COUNT) wc.cy_cand += (uint32_t)(__builtin_readcyclecounter() - c0);
+    first = false;
     bool hit = alive && b.dist != __builtin_inff();
     f3 N = f3{0.0f, 0.0f, 0.0f};
     wc.hits += (uint32_t)__popcll(__ballot(hit));
@@ -1104,7 +1115,8 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES) void render_kernel(KParams p) {
   // the counters are wave totals already: one atomic per counter per wave
   uint32_t v[RT_NSTATS] = {wc.closest, wc.shadow,   wc.pixels,      wc.nodes,
                            wc.tris,    wc.overflow, wc.zero_normal, wc.hits,
-                           wc.cl_nodes, wc.cl_tris, wc.sh_nodes,   wc.sh_tris};
+                           wc.cl_nodes, wc.cl_tris, wc.sh_nodes,   wc.sh_tris,
+                           wc.cy_cam,   wc.cy_cand, wc.cy_sec,     wc.cy_shadow};
 #pragma unroll
   for (int k = 0; k < RT_NSTATS; k++)
     if (lane == 0 && v[k]) atomicAdd(p.stats + k, (unsigned long long)v[k]);

@@ -89,7 +89,9 @@ class Stats(C.Structure):
                 ("cand_prims", C.c_ulonglong), ("cand_entries", C.c_ulonglong),
                 ("cand_global", C.c_ulonglong),
                 ("closest_node_lanes", C.c_ulonglong), ("closest_tri_lanes", C.c_ulonglong),
-                ("shadow_node_lanes", C.c_ulonglong), ("shadow_tri_lanes", C.c_ulonglong)]
+                ("shadow_node_lanes", C.c_ulonglong), ("shadow_tri_lanes", C.c_ulonglong),
+                ("cycles_camera", C.c_ulonglong), ("cycles_cand", C.c_ulonglong),
+                ("cycles_secondary", C.c_ulonglong), ("cycles_shadow", C.c_ulonglong)]
 
     def as_dict(self):
         return {k: int(getattr(self, k)) for k, _ in self._fields_}
@@ -139,6 +141,7 @@ _PROTOS = [
     ("rt_hip_stats", C.c_int, [C.c_void_p, C.POINTER(Stats)]),
     ("rt_hip_set_count_work", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_set_cull_slack", C.c_int, [C.c_void_p, C.c_float]),
+    ("rt_hip_set_camera_slack", C.c_int, [C.c_void_p, C.c_float]),
     ("rt_hip_set_exact_camera", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_set_policy", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_tile_cycles", C.c_int, [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_size_t]),
@@ -401,6 +404,9 @@ class Context:
 
     def set_cull_slack(self, ulps):
         _check(lib().rt_hip_set_cull_slack(self.h, float(ulps)), "cull_slack")
+
+    def set_camera_slack(self, ulps):
+        _check(lib().rt_hip_set_camera_slack(self.h, float(ulps)), "camera_slack")
 
     def render(self, frame, rank, nranks, d_tiles, stream=None):
         _check(lib().rt_hip_render(self.h, C.byref(frame), rank, nranks, C.c_void_p(d_tiles),

@@ -309,9 +309,14 @@ def test_zero_normal_is_an_error(gpu, tmp_path):
     interpolated normal; that rule is not reproduced, so a render that meets
     it must fail loudly (RT_EZERONORMAL from rt_hip_stats), never write a
     silently different image."""
+    # v0 = (-2,0,0), v1 = (2,0,0), v2 = (-2,2,0) (LIFO order), normals
+    # +z, -z, +z: on x = 0 (u = 0.5 exactly for the camera rays of column 16)
+    # the interpolated normal (0.5 - v) - 0.5 + v is exactly zero -- the
+    # oracle skips those hits (6 pixels of column 16 differ from the same
+    # scene with n1 = +z).  (A zero vn would not do: normalize(0) is NaN.)
     sv = tmp_path / "zn.svati"
     sv.write_text("camera 32 32 0 0 -5 1 0 0 0 -1 0 60\na_light 1 1 1\n\nobject 3\nKa 1 1 1\n"
-                  "v -2 -2 0\nv 2 -2 0\nv 0 2 0\nvn 0 0 0\nvn 0 0 0\nvn 0 0 0\n")
+                  "v -2 2 0\nv 2 0 0\nv -2 0 0\nvn 0 0 1\nvn 0 0 -1\nvn 0 0 1\n")
     s = gpu.Scene.load_svati(str(sv))
     with pytest.raises(gpu.RtError) as e:
         gpu.Context(s, "flat").render_image(s.frame())
