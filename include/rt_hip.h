@@ -182,6 +182,13 @@ int rt_hip_set_camera_bound_scale(rt_hip_ctx *ctx, double scale);
 int rt_cand_survey(const rt_scene *scene, float eps_ulps, double bound_scale, int threads,
                    int use_leaves, unsigned long long out[36]);
 
+/* Test hook: after an rt_hip_render of (frame, rank, nranks) with exact
+ * camera rays, re-derive its candidate lists on the host from the same code
+ * and compare.  out = {listed prims, entries, footprint mismatches, tiles
+ * whose list differs, prims on the global list}. */
+int rt_hip_cand_verify(rt_hip_ctx *ctx, const rt_frame *frame, int rank, int nranks,
+                       unsigned long long out[5]);
+
 /* d_gathered = nranks consecutive tile buffers (rank-major, as an RCCL gather
  * delivers them); writes the PPM-order image (W*H*3 floats) to d_rgb. */
 int rt_hip_assemble(rt_hip_ctx *ctx, const rt_frame *frame, const float *d_gathered, int nranks,
@@ -192,6 +199,19 @@ int rt_hip_assemble(rt_hip_ctx *ctx, const rt_frame *frame, const float *d_gathe
 int rt_hip_render_image(rt_hip_ctx *ctx, const rt_frame *frame, float *h_rgb, rt_stats *stats);
 
 /* Device memory helpers so C callers need no HIP headers. */
+/* gpu/rt compatibility mode (gpu/raytracer.cu:31-129,
+ * gpu/light.cu, gpu/colors.cu): the camera's frame rendered at 3x width and
+ * height with one ray per high-resolution pixel, uint8 saturating colours,
+ * reflections summed front to back over at most 11 closest-hit queries, then
+ * a 3x3 box downscale.  h_rgba receives width x height RGBA8 pixels (alpha
+ * 255) in gpu/rt's PNG row order.  stats as rt_hip_stats (camera = pixels =
+ * high-resolution rays).  No camera candidate lists in this mode. */
+int rt_hip_render_compat(rt_hip_ctx *ctx, const rt_camera *cam, unsigned char *h_rgba,
+                         rt_stats *stats);
+/* Drop-in for gpu/rt's main (gpu/rt.cpp:56-97): load, render in
+ * compatibility mode on GPU 0, write an 8-bit RGBA PNG.  accel < 0: choose. */
+int rt_raytrace_gpu(const char *input, const char *output, int accel);
+
 int rt_hip_malloc(int device, size_t bytes, void **d_ptr);
 int rt_hip_free(void *d_ptr);
 int rt_hip_memcpy_d2h(void *h_dst, const void *d_src, size_t bytes);

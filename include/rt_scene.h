@@ -124,6 +124,10 @@ void rt_scene_free(rt_scene *scene);
  * cpu/raytracer.c:128-134 (one line of "%d %d %d " after the header, int
  * truncation).  rgb = width*height*3 floats in PPM order. */
 int rt_ppm_write(const char *path, int width, int height, const float *rgb);
+/* 8-bit RGBA PNG, rows top down (gpu/rt.cpp:14-54 writes the same image
+ * through libpng: colour type RGBA, bit depth 8, no interlace).  zlib
+ * deflate, filter 0 on every row. */
+int rt_png_write_rgba(const char *path, int width, int height, const unsigned char *rgba);
 
 #ifdef __cplusplus
 }

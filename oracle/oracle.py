@@ -45,6 +45,9 @@ def lib():
         L.oracle_render.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p,
                                     C.POINTER(Counts)]
         L.oracle_render.restype = C.c_int
+        L.oracle_render_gpu.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p,
+                                        C.POINTER(Counts)]
+        L.oracle_render_gpu.restype = C.c_int
         L.oracle_init_color.argtypes = [C.c_float, C.c_float, C.c_float]
         L.oracle_init_color.restype = ColorS
         L.oracle_color_add.argtypes = [ColorS, ColorS]
@@ -145,4 +148,30 @@ def render(scene_ptr, width, height, pixels=None, threads=0):
     counts = {"closest": cnt.closest, "shadow": cnt.shadow, "max_depth": cnt.max_depth}
     if pixels is None:
         out = out.reshape(height, width, 3)
+    return out, counts
+
+
+def render_gpu(scene_ptr, width, height, pixels=None, threads=0):
+    """gpu/rt compatibility mode with the oracle (oracle_render_gpu).
+    pixels: None (whole W x H image, gpu/rt's PNG row order) or an (N, 2)
+    (row, col) array.  Returns (uint8 (N, 4) or (H, W, 4), counts)."""
+    if pixels is None:
+        n = width * height
+        pix_ptr = None
+    else:
+        pixels = np.ascontiguousarray(pixels, dtype=np.int32)
+        n = len(pixels)
+        pix_ptr = pixels.ctypes.data_as(C.c_void_p)
+    out = np.zeros((n, 4), np.uint8)
+    cnt = Counts()
+    ptr = scene_ptr.ptr if isinstance(scene_ptr, OracleScene) else scene_ptr
+    if not isinstance(ptr, C.c_void_p):
+        ptr = C.cast(ptr, C.c_void_p)
+    rc = lib().oracle_render_gpu(ptr, pix_ptr, n, threads, out.ctypes.data_as(C.c_void_p),
+                                 C.byref(cnt))
+    if rc != 0:
+        raise RuntimeError(f"oracle_render_gpu = {rc}")
+    counts = {"closest": cnt.closest, "shadow": cnt.shadow, "max_depth": cnt.max_depth}
+    if pixels is None:
+        out = out.reshape(height, width, 4)
     return out, counts

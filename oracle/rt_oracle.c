@@ -338,6 +338,171 @@ static color render_pixel(const struct or_scene *scene, vec3 u, vec3 v, vec3 C, 
   return acc;
 }
 
+/* ---- gpu/rt compatibility mode ----
+ * gpu/raytracer.cu:31-129, gpu/light.cu:12-126, gpu/colors.cu:3-49 as the
+ * sources read (PARTITIONING_NONE order of gpu/hit.cu:83-116, which is
+ * cpu/hit.c's), without nvcc's default FMA contraction, with pow(float,
+ * float) taken as the f64 pow rounded to float.  uint8 colours. */
+typedef struct { unsigned char r, g, b; } color8;
+
+/* gpu/colors.cu:3-20 */
+static unsigned char chan8(float x)
+{
+  x = x * 255;
+  if (x > 255)
+    x = 255;
+  if (x < 0)
+    x = 0;
+  return x == x ? (unsigned char)x : 0;
+}
+static color8 init8(float r, float g, float b)
+{
+  color8 c = { chan8(r), chan8(g), chan8(b) };
+  return c;
+}
+/* gpu/colors.cu:23-35 */
+static color8 add8(color8 a, color8 b)
+{
+  int r = a.r + b.r, g = a.g + b.g, bl = a.b + b.b;
+  color8 c = { (unsigned char)(r > 255 ? 255 : r), (unsigned char)(g > 255 ? 255 : g),
+               (unsigned char)(bl > 255 ? 255 : bl) };
+  return c;
+}
+/* gpu/colors.cu:37-40 */
+static color8 mul8(color8 a, float coef)
+{
+  return init8((float)a.r / 255 * coef, (float)a.g / 255 * coef, (float)a.b / 255 * coef);
+}
+/* gpu/colors.cu:42-47 */
+static color8 mults8(color8 a, color8 b)
+{
+  return init8(((float)a.r / 255) * ((float)b.r / 255), ((float)a.g / 255) * ((float)b.g / 255),
+               ((float)a.b / 255) * ((float)b.b / 255));
+}
+
+/* gpu/light.cu:12-28 */
+static void specular8(color8 *acc, ray incident, ray hit, const struct or_object *obj)
+{
+  color8 k = init8(obj->ks.x, obj->ks.y, obj->ks.z);
+  vec3 V = v_sub(incident.origin, hit.origin);
+  vec3 R = v_sub(incident.direction,
+                 v_scale(hit.direction, 2 * v_dot(hit.direction, incident.direction)));
+  R = v_normalize(R);
+  V = v_normalize(V);
+  float d = v_dot(R, V);
+  float m = d > 0.0f ? d : 0.0f; /* cufmax(d, 0.0) */
+  float ls = (float)pow((double)m, (double)obj->ns);
+  k = mul8(k, ls);
+  *acc = add8(*acc, k);
+}
+
+/* gpu/light.cu:46-126 */
+static color8 shade8(const struct or_scene *scene, const struct or_object *obj, ray hit,
+                     struct tls_counts *cnt)
+{
+  color8 acc = init8(0, 0, 0);
+  for (size_t i = 0; i < scene->light_count; i++)
+  {
+    const struct or_light *l = &scene->lights[i];
+    if (l->type == OR_AMBIENT)
+    {
+      color8 t = mults8(init8(l->r, l->g, l->b), init8(obj->ka.x, obj->ka.y, obj->ka.z));
+      acc = add8(acc, t);
+    }
+    else if (l->type == OR_DIRECTIONAL)
+    {
+      ray sr = { hit.origin, v_scale(l->v, -1) };
+      if (shadowed(scene, sr, cnt))
+        continue;
+      vec3 L = v_scale(l->v, -1);
+      color8 t = mults8(init8(l->r, l->g, l->b), init8(obj->kd.x, obj->kd.y, obj->kd.z));
+      t = mul8(t, v_dot(L, hit.direction));
+      ray inc = { v_add(hit.origin, v_scale(l->v, -10)), l->v };
+      specular8(&t, inc, hit, obj);
+      acc = add8(acc, t);
+    }
+    else if (l->type == OR_POINT)
+    {
+      vec3 L = v_scale(l->v, -1);
+      vec3 N = hit.direction;
+      if (v_dot(L, N) < 0)
+        N = v_scale(N, -1);
+      vec3 to_light = v_sub(l->v, hit.origin);
+      float dist = v_length(v_sub(l->v, hit.origin));
+      ray sr = { hit.origin, to_light };
+      if (shadowed(scene, sr, cnt))
+        continue;
+      color8 t = mults8(init8(l->r, l->g, l->b), init8(obj->kd.x, obj->kd.y, obj->kd.z));
+      t = mul8(t, v_dot(L, N) * 1 / dist);
+      ray inc = { v_add(hit.origin, v_scale(to_light, -10)), to_light };
+      specular8(&t, inc, hit, obj);
+      acc = add8(acc, t);
+    }
+  }
+  return acc;
+}
+
+/* gpu/raytracer.cu:88-125: one high-resolution pixel (px, py) of the frame
+ * whose camera (width, height) is already the upscaled one */
+static color8 gpu_ray_pixel(const struct or_scene *scene, vec3 u, vec3 v, vec3 C, int px, int py,
+                            struct tls_counts *cnt)
+{
+  const int W = scene->camera.width, H = scene->camera.height;
+  vec3 ui = v_scale(u, (float)(px - W / 2));
+  vec3 vj = v_scale(v, (float)(py - H / 2));
+  vec3 point = v_add(v_add(C, ui), vj);
+  ray r = { point, v_normalize(v_sub(scene->camera.position, point)) };
+  float nr_ = 1;
+  float r_rn = nr_;
+  int max_bounce = 10;
+  color8 color = init8(0, 0, 0);
+  do
+  {
+    /* trace(), gpu/raytracer.cu:31-46 */
+    color8 tmp = init8(0, 0, 0);
+    cnt->closest++;
+    int oi = -1;
+    ray hit = oracle_collide(scene, r, &oi);
+    if (!v_is_zero(hit.direction))
+    {
+      const struct or_object *obj = &scene->objects[oi];
+      tmp = shade8(scene, obj, hit, cnt);
+      if (obj->nr > 0)
+        r = bounce(r, hit);
+      r_rn = obj->nr;
+    }
+    else
+      r_rn = 0;
+    tmp = mul8(tmp, nr_);
+    color = add8(color, tmp);
+    nr_ *= r_rn;
+  } while (nr_ > 0.01f && max_bounce-- > 0);
+  return color;
+}
+
+/* gpu/raytracer.cu:48-85 + gpu/rt.cpp's row order: output pixel (row, col)
+ * of the W x H image, RGBA8 */
+static void render_pixel_gpu(const struct or_scene *hi, vec3 u, vec3 v, vec3 C, int W, int H,
+                             int row, int col, unsigned char *out, struct tls_counts *cnt)
+{
+  const int px = W - 1 - col, py = H - 1 - row;
+  float r = 0, g = 0, b = 0;
+  for (int hy = 3 * py; hy < 3 * py + 3; ++hy)
+    for (int hx = 3 * px; hx < 3 * px + 3; ++hx)
+    {
+      color8 c = gpu_ray_pixel(hi, u, v, C, hx, hy, cnt);
+      r += (float)c.r;
+      g += (float)c.g;
+      b += (float)c.b;
+    }
+  float ali2 = 255.0f * 3.0f * 3.0f;
+  color8 e = init8(r / ali2, g / ali2, b / ali2);
+  out[0] = e.r;
+  out[1] = e.g;
+  out[2] = e.b;
+  out[3] = 255;
+}
+
 struct job {
   const struct or_scene *scene;
   const int *pixels;
@@ -348,6 +513,8 @@ struct job {
   size_t chunk;  /* pixels per grab: small batches must still spread over every thread */
   pthread_mutex_t lock;
   struct or_counts total;
+  unsigned char *out8;  /* gpu/rt mode: RGBA8 per pixel (scene = the 3x camera) */
+  int W8, H8;           /* gpu/rt mode: output size */
 };
 
 static void *worker(void *arg)
@@ -371,8 +538,15 @@ static void *worker(void *arg)
       }
       else
       {
-        row = (int)(p / (size_t)W);
-        col = (int)(p % (size_t)W);
+        const int Wp = jb->out8 ? jb->W8 : W;
+        row = (int)(p / (size_t)Wp);
+        col = (int)(p % (size_t)Wp);
+      }
+      if (jb->out8)
+      {
+        render_pixel_gpu(jb->scene, jb->u, jb->v, jb->C, jb->W8, jb->H8, row, col, jb->out8 + 4 * p,
+                         &cnt);
+        continue;
       }
       color c = render_pixel(jb->scene, jb->u, jb->v, jb->C, row, col, &cnt);
       jb->out[3 * p + 0] = c.r;
@@ -389,40 +563,70 @@ static void *worker(void *arg)
   return NULL;
 }
 
+static int run_job(struct job *jb, int nthreads, struct or_counts *counts);
+
 int oracle_render(const struct or_scene *scene, const int *pixels, size_t npix, int nthreads,
                   float *out, struct or_counts *counts)
 {
   if (!scene || !out)
     return -1;
-  if (nthreads <= 0)
-    nthreads = (int)sysconf(_SC_NPROCESSORS_ONLN);
-  if (nthreads < 1)
-    nthreads = 1;
   struct job jb;
   memset(&jb, 0, sizeof jb);
   jb.scene = scene;
   jb.pixels = pixels;
   jb.npix = npix;
   jb.out = out;
-  atomic_init(&jb.next, 0);
-  jb.chunk = npix / ((size_t)nthreads * 4);
-  if (jb.chunk < 1)
-    jb.chunk = 1;
-  if (jb.chunk > 16)
-    jb.chunk = 16;
-  pthread_mutex_init(&jb.lock, NULL);
   oracle_camera_frame(scene, &jb.u, &jb.v, &jb.C);
+  return run_job(&jb, nthreads, counts);
+}
+
+int oracle_render_gpu(const struct or_scene *scene, const int *pixels, size_t npix, int nthreads,
+                      unsigned char *out, struct or_counts *counts)
+{
+  if (!scene || !out)
+    return -1;
+  /* gpu/rt.cpp:72-83: the camera's width and height times 3, then the frame
+   * (L and C) of that camera */
+  struct or_scene hi = *scene;
+  hi.camera.width = 3 * scene->camera.width;
+  hi.camera.height = 3 * scene->camera.height;
+  struct job jb;
+  memset(&jb, 0, sizeof jb);
+  jb.scene = &hi;
+  jb.pixels = pixels;
+  jb.npix = npix;
+  jb.out8 = out;
+  jb.W8 = scene->camera.width;
+  jb.H8 = scene->camera.height;
+  oracle_camera_frame(&hi, &jb.u, &jb.v, &jb.C);
+  return run_job(&jb, nthreads, counts);
+}
+
+/* Runs a prepared job on nthreads threads (<= 0: all online CPUs). */
+static int run_job(struct job *jb, int nthreads, struct or_counts *counts)
+{
+  if (nthreads <= 0)
+    nthreads = (int)sysconf(_SC_NPROCESSORS_ONLN);
+  if (nthreads < 1)
+    nthreads = 1;
+  atomic_init(&jb->next, 0);
+  jb->chunk = jb->npix / ((size_t)nthreads * 4);
+  if (jb->chunk < 1)
+    jb->chunk = 1;
+  if (jb->chunk > 16)
+    jb->chunk = 16;
+  pthread_mutex_init(&jb->lock, NULL);
   pthread_t *tid = calloc((size_t)nthreads, sizeof *tid);
   if (!tid)
     return -1;
   for (int t = 0; t < nthreads; t++)
-    pthread_create(&tid[t], NULL, worker, &jb);
+    pthread_create(&tid[t], NULL, worker, jb);
   for (int t = 0; t < nthreads; t++)
     pthread_join(tid[t], NULL);
   free(tid);
-  pthread_mutex_destroy(&jb.lock);
+  pthread_mutex_destroy(&jb->lock);
   if (counts)
-    *counts = jb.total;
+    *counts = jb->total;
   return 0;
 }
 

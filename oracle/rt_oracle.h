@@ -57,6 +57,14 @@ void oracle_camera_frame(const struct or_scene *scene, struct or_vec3 *u,
 int oracle_render(const struct or_scene *scene, const int *pixels, size_t npix,
                   int nthreads, float *out, struct or_counts *counts);
 
+/* gpu/rt compatibility mode (gpu/raytracer.cu:31-129, gpu/light.cu,
+ * gpu/colors.cu, gpu/rt.cpp:56-97): output pixels (row, col) of the
+ * camera's W x H image (pixels as above; NULL = whole image, row-major in
+ * gpu/rt's PNG order), each the 3x3 downscale of the 3x frame; out receives
+ * npix*4 bytes (RGBA8, alpha 255).  counts: queries of the 3x rays. */
+int oracle_render_gpu(const struct or_scene *scene, const int *pixels, size_t npix,
+                      int nthreads, unsigned char *out, struct or_counts *counts);
+
 /* Single-function entry points, for unit known-answer tests. */
 struct or_color oracle_init_color(float r, float g, float b);
 struct or_color oracle_color_add(struct or_color a, struct or_color b);

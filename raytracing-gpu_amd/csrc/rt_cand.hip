@@ -606,6 +606,41 @@ __global__ __launch_bounds__(64) void big_count_kernel(CandParams p) {
   }
 }
 
+// The rank's tiles of one tile-row column interval [x0, x1] (base = first
+// global tile of the row): global tiles g0 + m n, local indices q0 + m with
+// q0 = g0 / n -- one division per interval, none per tile.  Returns the
+// count written at keys/vals[o ..].
+__device__ __forceinline__ uint32_t emit_interval(const CandParams& p, uint32_t base, int x0, int x1,
+                                                  uint32_t o, uint32_t prim) {
+  if (x0 > x1) return 0;
+  const uint32_t n = (uint32_t)p.nranks, r = (uint32_t)p.rank;
+  const uint32_t lo = base + (uint32_t)x0, hi = base + (uint32_t)x1;
+  const uint32_t cnt = rank_tiles(lo, hi, n, r);
+  const uint32_t q0 = (lo + (r + n - lo % n) % n) / n;
+  for (uint32_t m = 0; m < cnt; m++) {
+    p.keys[o + m] = q0 + m;
+    p.vals[o + m] = prim;
+  }
+  return cnt;
+}
+
+// One tile row of a footprint (raster_row's tiles: [a0, a1] and the parts
+// of [b0, b1] outside it); returns the entries written.
+__device__ __forceinline__ uint32_t emit_row(const CandParams& p, const Footprint& fp, int ty, int r0,
+                                             int r1, uint32_t o, uint32_t prim) {
+  int a0, a1, b0, b1;
+  row_tiles(p, fp, ty, r0, r1, a0, a1, b0, b1);
+  const uint32_t base = (uint32_t)ty * (uint32_t)p.tiles_x;
+  uint32_t k = emit_interval(p, base, a0, a1, o, prim);
+  if (a0 > a1) {
+    k += emit_interval(p, base, b0, b1, o + k, prim);
+  } else {
+    k += emit_interval(p, base, b0, b1 < a0 - 1 ? b1 : a0 - 1, o + k, prim);
+    k += emit_interval(p, base, b0 > a1 + 1 ? b0 : a1 + 1, b1, o + k, prim);
+  }
+  return k;
+}
+
 // Pass 2 (after the scan of visits): the small footprints write their
 // (tile, prim) pairs at their offsets.
 __global__ __launch_bounds__(256) void emit_kernel(CandParams p) {
@@ -618,15 +653,11 @@ __global__ __launch_bounds__(256) void emit_kernel(CandParams p) {
   int r0, r1;
   if (!raster_rows(p, fp, r0, r1) || (r1 >> 3) - (r0 >> 3) + 1 > kSmallRows) return;
   const uint32_t prim = p.list[j];
-  raster(p, fp, [&](uint32_t t) {
-    p.keys[o] = t;
-    p.vals[o] = prim;
-    o++;
-  });
+  for (int ty = r0 >> 3; ty <= (r1 >> 3); ty++) o += emit_row(p, fp, ty, r0, r1, o, prim);
 }
 
-// Pass 2b: one wave per big footprint; each lane emits its tile rows at the
-// offset a wave prefix sum of the lanes' counts gives it.
+// Pass 2b: one wave per big footprint, its tile rows over the lanes; a wave
+// prefix sum of the lanes' row counts places each lane's entries.
 __global__ __launch_bounds__(64) void big_kernel(CandParams p) {
   const int lane = threadIdx.x;
   const uint32_t nbig = p.ctr[2];
@@ -641,12 +672,7 @@ __global__ __launch_bounds__(64) void big_kernel(CandParams p) {
       for (int ty = ty0 + lane; ty <= ty1; ty += 64) cnt += count_row(p, fp, ty, r0, r1);
     uint32_t o = p.off[j] + wave_excl_scan(cnt, lane);
     if (rows)
-      for (int ty = ty0 + lane; ty <= ty1; ty += 64)
-        raster_row(p, fp, ty, r0, r1, [&](uint32_t t) {
-          p.keys[o] = t;
-          p.vals[o] = prim;
-          o++;
-        });
+      for (int ty = ty0 + lane; ty <= ty1; ty += 64) o += emit_row(p, fp, ty, r0, r1, o, prim);
   }
 }
 
@@ -686,6 +712,7 @@ __global__ __launch_bounds__(256) void entry_skip_kernel(const uint32_t* cand, c
 
 }  // namespace rtc
 
+#include <algorithm>
 #include <thread>
 #include <vector>
 
@@ -751,6 +778,55 @@ extern "C" int rt_cand_survey_host(const CandParams* p, const float* tri, const 
   unsigned long long nbad = 0;
   for (int t = 0; t < threads; t++) nbad += bad[t];
   return nbad ? -1 : 0;
+}
+
+// Host check of the device-built lists of one frame (tests): every prim the
+// float fast path listed is re-classified on the host (same code, so the
+// same f64 bits; the safe ones have no tiles), every kept footprint compared
+// bit for bit, and every tile's list equal, as a multiset, to the tiles the
+// host raster gives the listed footprints.  out: [0] listed prims, [1] entries,
+// [2] footprint mismatches, [3] tile-list mismatches (tiles), [4] globals.
+extern "C" int rt_cand_verify_host(const CandParams* p, const float* tri, const float* node,
+                                   const uint32_t* prim_leaf, const uint32_t* list, uint32_t nlist,
+                                   const void* fp_dev, const uint32_t* start, const uint32_t* cand,
+                                   uint32_t ntiles, unsigned long long out[5]) {
+  for (int k = 0; k < 5; k++) out[k] = 0;
+  out[0] = nlist;
+  out[1] = start[ntiles];
+  const rtc::Footprint* fpd = (const rtc::Footprint*)fp_dev;
+  std::vector<std::vector<uint32_t>> want(ntiles);
+  for (uint32_t j = 0; j < nlist; j++) {
+    const uint32_t prim = list[j];
+    rtc::Footprint fp;
+    std::memset(&fp, 0, sizeof fp);
+    const float* lb = prim_leaf ? node + 8 * (size_t)prim_leaf[prim] : nullptr;
+    const int c = rtc::classify(*p, tri + 12 * (size_t)prim, lb, fp);
+    if (c == rtc::GLOBAL) {
+      out[4]++;
+      continue;
+    }
+    if (c != rtc::FOOTPRINT) continue;  // safe after all (leaf box): no tiles
+    uint32_t n = 0;
+    rtc::raster(*p, fp, [&](uint32_t t) {
+      if (t < ntiles) want[t].push_back(prim);
+      n++;
+    });
+    if (n == 0) continue;  // the device keeps no footprint without tiles
+    const rtc::Footprint& d = fpd[j];
+    // (k, l, dimg are only set -- and only read -- with tri_ok)
+    bool same = d.tri_ok == fp.tri_ok && d.b0 == fp.b0 && d.b1 == fp.b1 && d.b2 == fp.b2 &&
+                d.hw == fp.hw && d.hw0 == fp.hw0 && d.skip == fp.skip;
+    if (same && fp.tri_ok) same = d.dimg == fp.dimg;
+    for (int k = 0; k < 3 && same && fp.tri_ok; k++) same = d.k[k] == fp.k[k] && d.l[k] == fp.l[k];
+    if (!same) out[2]++;
+  }
+  for (uint32_t t = 0; t < ntiles; t++) {
+    std::vector<uint32_t> got(cand + start[t], cand + start[t + 1]);
+    std::sort(got.begin(), got.end());
+    std::sort(want[t].begin(), want[t].end());
+    if (got != want[t]) out[3]++;
+  }
+  return 0;
 }
 
 extern "C" size_t rt_cand_footprint_bytes(void) { return sizeof(rtc::Footprint); }

@@ -407,6 +407,47 @@ extern "C" int rt_cand_survey(const rt_scene* scene, float eps_ulps, double boun
   return rc;
 }
 
+extern "C" int rt_hip_cand_verify(rt_hip_ctx* c, const rt_frame* f, int rank, int nranks,
+                                  unsigned long long out[5]) {
+  if (!c || !f || !out) return rt_set_error(RT_EINVAL, "null argument");
+  if (!c->d_cand_start || !c->d_cand || !c->d_cand_list)
+    return rt_set_error(RT_EINVAL, "no candidate lists (render a frame with exact camera rays first)");
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = c->last_stream ? c->last_stream : c->stream;
+  HIP_TRY(hipStreamSynchronize(s));
+  CandParams cp;
+  int rc = cand_params(f, c->scene_c, c->scene_r, c->cam_eps_ulps, c->bound_scale, rank, nranks, &cp);
+  if (rc) return rc;
+  cp.nprim = c->nprim;
+  const uint32_t nt = (uint32_t)cp.ntiles_local;
+  uint32_t ctr[4];
+  HIP_TRY(hipMemcpy(ctr, c->d_cand_ctr, sizeof ctr, hipMemcpyDeviceToHost));
+  const uint32_t nlist = ctr[3];
+  std::vector<uint32_t> start(nt + 1), list(nlist + 1), pl;
+  HIP_TRY(hipMemcpy(start.data(), c->d_cand_start, (nt + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  std::vector<uint32_t> cand(start[nt] + 1);
+  if (start[nt])
+    HIP_TRY(hipMemcpy(cand.data(), c->d_cand, start[nt] * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  if (nlist) HIP_TRY(hipMemcpy(list.data(), c->d_cand_list, nlist * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  const size_t fpb = rt_cand_footprint_bytes();
+  std::vector<unsigned char> fp((size_t)nlist * fpb + 1);
+  if (nlist) HIP_TRY(hipMemcpy(fp.data(), c->d_cand_fp, (size_t)nlist * fpb, hipMemcpyDeviceToHost));
+  std::vector<float> tri((size_t)c->nprim * RT_TRI_FLOATS + 1), node;
+  HIP_TRY(hipMemcpy(tri.data(), c->d_tri_prim, (size_t)c->nprim * RT_TRI_FLOATS * sizeof(float),
+                    hipMemcpyDeviceToHost));
+  if (c->d_prim_leaf) {
+    pl.resize(c->nprim + 1);
+    HIP_TRY(hipMemcpy(pl.data(), c->d_prim_leaf, c->nprim * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    node.resize((size_t)c->info.nodes * RT_NODE_FLOATS + 1);
+    HIP_TRY(hipMemcpy(node.data(), c->d_node, (size_t)c->info.nodes * RT_NODE_FLOATS * sizeof(float),
+                      hipMemcpyDeviceToHost));
+  }
+  rt_cand_verify_host(&cp, tri.data(), c->d_prim_leaf ? node.data() : nullptr,
+                      c->d_prim_leaf ? pl.data() : nullptr, list.data(), nlist, fp.data(),
+                      start.data(), cand.data(), nt, out);
+  return RT_OK;
+}
+
 extern "C" int rt_hip_set_timing(rt_hip_ctx* c, int enable) {
   if (!c) return rt_set_error(RT_EINVAL, "null context");
   HIP_TRY(hipSetDevice(c->device));
@@ -837,6 +878,96 @@ extern "C" int rt_hip_render_image(rt_hip_ctx* c, const rt_frame* f, float* h_rg
   if (!rc) rc = rt_hip_stats(c, st ? st : &tmp);
   (void)hipFree(d_tiles);
   (void)hipFree(d_rgb);
+  return rc;
+}
+
+static int choose_accel(const rt_scene* s);
+
+// gpu/rt compatibility mode (csrc/rt_render.hip compat_kernel): the frame
+// of the camera at 3x its size (gpu/rt.cpp:72-83: width and height scaled,
+// so L and C follow), one ray per high-resolution pixel, then the 3x3
+// downscale; h_rgba = width x height RGBA8 in gpu/rt's PNG row order.
+extern "C" int rt_hip_render_compat(rt_hip_ctx* c, const rt_camera* cam, unsigned char* h_rgba,
+                                    rt_stats* st) {
+  if (!c || !cam || !h_rgba) return rt_set_error(RT_EINVAL, "null argument");
+  if (cam->width <= 0 || cam->height <= 0) return rt_set_error(RT_EINVAL, "empty frame");
+  if ((long long)cam->width * cam->height > (1ll << 28) / 9)
+    return rt_set_error(RT_EINVAL, "frame too large for the 3x render");
+  HIP_TRY(hipSetDevice(c->device));
+  rt_camera big = *cam;
+  big.width = 3 * cam->width;
+  big.height = 3 * cam->height;
+  rt_frame f;
+  int rc = rt_frame_from_camera(&big, &f);
+  if (rc) return rc;
+  const size_t nhi = (size_t)big.width * big.height, nlo = (size_t)cam->width * cam->height;
+  uint32_t *d_hi = nullptr, *d_lo = nullptr;
+  HIP_TRY(hipMalloc((void**)&d_hi, nhi * sizeof(uint32_t)));
+  if (hipMalloc((void**)&d_lo, nlo * sizeof(uint32_t)) != hipSuccess) {
+    (void)hipFree(d_hi);
+    return rt_set_error(RT_EHIP, "hipMalloc image");
+  }
+  hipStream_t s = c->stream;
+  KParams p;
+  std::memset(&p, 0, sizeof p);
+  p.tri = c->d_tri;
+  p.nrm = c->d_nrm;
+  p.mat = c->d_mat;
+  p.light = c->d_light;
+  p.node = c->d_node;
+  p.nrec = c->nrec;
+  p.nlight = c->nlight;
+  p.u = rt::f3{f.u.x, f.u.y, f.u.z};
+  p.v = rt::f3{f.v.x, f.v.y, f.v.z};
+  p.C = rt::f3{f.C.x, f.C.y, f.C.z};
+  p.pos = rt::f3{f.position.x, f.position.y, f.position.z};
+  p.W = big.width;
+  p.H = big.height;
+  p.tiles_x = tiles_x_of(big.width);
+  p.ntiles_total = tiles_x_of(big.width) * tiles_y_of(big.height);
+  p.nranks = 1;
+  p.ntiles_local = p.ntiles_total;
+  p.out = (float*)d_hi;
+  p.tile_counter = c->d_counter;
+  p.stats = c->d_stats;
+  p.scene_c = rt::f3{c->scene_c[0], c->scene_c[1], c->scene_c[2]};
+  p.scene_r = c->scene_r;
+  p.scene_cmag = std::fmax(std::fabs(c->scene_c[0]), std::fmax(std::fabs(c->scene_c[1]),
+                                                               std::fabs(c->scene_c[2])));
+  p.spill = c->d_spill;
+  p.eps_rel = c->eps_ulps * 5.9604645e-8f;
+  p.eps_rel_cam = c->cam_eps_ulps * 5.9604645e-8f;
+  p.terms = c->d_terms;
+  const int accel = (c->accel == RT_ACCEL_FLAT || !c->d_node) ? RT_ACCEL_FLAT_D : RT_ACCEL_OCTREE_D;
+  if (hipMemsetAsync(c->d_counter, 0, 8 * 128, s) != hipSuccess ||
+      hipMemsetAsync(c->d_stats, 0, RT_NSTATS * sizeof(unsigned long long), s) != hipSuccess ||
+      rt_launch_compat(&p, accel, c->grid, s) != hipSuccess ||
+      rt_launch_downscale(d_hi, d_lo, cam->width, cam->height, s) != hipSuccess ||
+      hipMemcpyAsync(h_rgba, d_lo, nlo * sizeof(uint32_t), hipMemcpyDeviceToHost, s) != hipSuccess)
+    rc = rt_set_error(RT_EHIP, "compat render: %s", hipGetErrorString(hipGetLastError()));
+  c->last_stream = s;
+  rt_stats tmp;
+  if (!rc) rc = rt_hip_stats(c, st ? st : &tmp);
+  if (st) st->camera = st->pixels;  // one camera ray per high-resolution pixel
+  (void)hipFree(d_hi);
+  (void)hipFree(d_lo);
+  return rc;
+}
+
+// gpu/rt.cpp:56-97: `rt file.svati output.png` with gpu/rt's semantics
+extern "C" int rt_raytrace_gpu(const char* input, const char* output, int accel) {
+  rt_scene* scene = nullptr;
+  int rc = rt_scene_load_svati(input, &scene);
+  if (rc) return rc;
+  if (accel < 0) accel = choose_accel(scene);
+  rt_hip_ctx* ctx = nullptr;
+  std::vector<unsigned char> img((size_t)4 * (scene->camera.width > 0 ? scene->camera.width : 0) *
+                                 (scene->camera.height > 0 ? scene->camera.height : 0) + 4);
+  rc = rt_hip_create(0, scene, accel, &ctx);
+  if (!rc) rc = rt_hip_render_compat(ctx, &scene->camera, img.data(), nullptr);
+  if (!rc) rc = rt_png_write_rgba(output, scene->camera.width, scene->camera.height, img.data());
+  if (ctx) rt_hip_destroy(ctx);
+  rt_scene_free(scene);
   return rc;
 }
 

@@ -73,6 +73,11 @@ struct KParams {
 // policy = RT_POLICY_* (octree only)
 extern "C" hipError_t rt_launch_render(const KParams* p, int accel, int count_work, int policy,
                                        int grid, hipStream_t stream);
+// gpu/rt compatibility mode: p->W x p->H = the 3x upscaled frame, p->out =
+// its packed RGBA8 image; then the 3x3 downscale to W x H (PNG row order)
+extern "C" hipError_t rt_launch_compat(const KParams* p, int accel, int grid, hipStream_t stream);
+extern "C" hipError_t rt_launch_downscale(const uint32_t* hi, uint32_t* lo, int W, int H,
+                                          hipStream_t stream);
 extern "C" hipError_t rt_launch_assemble(const float* tiles, float* rgb, int W, int H, int tiles_x,
                                          int ntiles, int nranks, int tiles_per_rank,
                                          hipStream_t stream);

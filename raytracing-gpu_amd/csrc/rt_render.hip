@@ -1151,6 +1151,203 @@ __global__ __launch_bounds__(256) void combine_kernel(const float* __restrict__ 
   o[2] = acc.b;
 }
 
+// ------------------------------------------------ gpu/rt compatibility mode
+// The reference's GPU renderer's own output semantics (SURVEY.md §8(f) item
+// 4): the frame rendered at 3x the size with one ray per high-resolution
+// pixel (gpu/rt.cpp:72-83, gpu/raytracer.cu:88-125), colours as saturating
+// uint8 (gpu/colors.cu:3-49), reflections accumulated front to back for at
+// most 11 queries (gpu/raytracer.cu:31-46,113-120), the light model of
+// gpu/light.cu (cpu/light.c's, in uint8 colours), then a 3x3 box downscale
+// (gpu/raytracer.cu:48-85).  Geometry, closest hit and shadow queries are
+// cpu/rt's (gpu/hit.cu:4-123 restates cpu/hit.c) and run through the same
+// walks.  uint8 channels are held as integral floats.
+
+// init_color (gpu/colors.cu:3-20): x*255 clamped, then the (unsigned char)
+// conversion truncates (a NaN converts to 0)
+__device__ __forceinline__ float chan8(float x) {
+  float y = x * 255.0f;
+  if (y > 255.0f) y = 255.0f;
+  if (y < 0.0f) y = 0.0f;
+  y = __builtin_truncf(y);
+  return y == y ? y : 0.0f;
+}
+__device__ __forceinline__ col init8(float r, float g, float b) { return col{chan8(r), chan8(g), chan8(b)}; }
+// color_add: integer sum, saturated at 255
+__device__ __forceinline__ col add8(col a, col b) {
+  return col{fminf(a.r + b.r, 255.0f), fminf(a.g + b.g, 255.0f), fminf(a.b + b.b, 255.0f)};
+}
+// color_mul: init_color(float(a.r) / 255 * coef, ...)
+__device__ __forceinline__ col mul8(col a, float coef) {
+  return init8(a.r / 255.0f * coef, a.g / 255.0f * coef, a.b / 255.0f * coef);
+}
+// color_mults: init_color((a.r / 255) * (b.r / 255), ...)
+__device__ __forceinline__ col mults8(col a, col b) {
+  return init8((a.r / 255.0f) * (b.r / 255.0f), (a.g / 255.0f) * (b.g / 255.0f),
+               (a.b / 255.0f) * (b.b / 255.0f));
+}
+
+// gpu/light.cu:12-28 (pow(cufmax(R.V, 0), ns): the f32 pow, taken as the
+// correctly rounded f64 pow rounded to float, as in cpu mode)
+__device__ __forceinline__ col specular8(col tmp, f3 inc_o, f3 inc_d, f3 P, f3 N, const float* m) {
+  col k = init8(m[6], m[7], m[8]);
+  f3 V = sub(inc_o, P);
+  f3 R = sub(inc_d, scale(N, 2.0f * dot(N, inc_d)));
+  R = normalize(R);
+  V = normalize(V);
+  float ls = spec_pow((double)dot(R, V), (double)m[9]);
+  k = mul8(k, ls);
+  return add8(tmp, k);
+}
+
+// gpu/light.cu:66-118, the lit branch of a directional (1) or point (2) light
+__device__ __forceinline__ col light_lit8(uint32_t type, col lc, f3 lv, const float* m, f3 P, f3 N) {
+  if (type == 1) {
+    col tmp = mults8(lc, init8(m[3], m[4], m[5]));
+    tmp = mul8(tmp, dot(scale(lv, -1.0f), N));
+    return specular8(tmp, add(P, scale(lv, -10.0f)), lv, P, N, m);
+  }
+  f3 to_l = sub(lv, P);
+  f3 Lp = scale(lv, -1.0f);
+  f3 Nf = N;
+  if (dot(Lp, Nf) < 0.0f) Nf = scale(Nf, -1.0f);
+  float dist = length(sub(lv, P));
+  col tmp = mults8(lc, init8(m[3], m[4], m[5]));
+  tmp = mul8(tmp, dot(Lp, Nf) * 1.0f / dist);
+  return specular8(tmp, add(P, scale(to_l, -10.0f)), to_l, P, N, m);
+}
+
+// gpu/light.cu:46-126 for the lanes with hit; converged shadow queries
+template <int ACCEL, int POL>
+__device__ col apply_light8(const KParams& p, bool hit, const float* m, f3 P, f3 N, Stack& s,
+                            WaveCtx& w, WorkCount& wc) {
+  col acc = col{0.0f, 0.0f, 0.0f};
+  for (uint32_t li = 0; li < p.nlight; li++) {
+    const float* L = p.light + RT_LIGHT_FLOATS_D * li;
+    uint32_t type = __float_as_uint(L[0]);
+    col lc = init8(L[1], L[2], L[3]);
+    f3 lv = f3{L[4], L[5], L[6]};
+    if (type == 0) {
+      if (hit) acc = add8(acc, mults8(lc, init8(m[0], m[1], m[2])));
+    } else if (type == 1 || type == 2) {
+      bool sh = shadow_q<ACCEL, false, POL>(p, P, shadow_dir(type, lv, P), type, hit, s, w, wc);
+      if (hit && !sh) acc = add8(acc, light_lit8(type, lc, lv, m, P, N));
+    }
+  }
+  return acc;
+}
+
+// One high-resolution pixel per lane, one 8x8 tile of the 3W x 3H image per
+// wave (persistent waves, one tile counter).  p.W, p.H, p.u/v/C/pos: the
+// upscaled frame; p.out: 3W x 3H packed RGBA8, row-major (row = py).
+template <int ACCEL, int POL>
+__global__ __launch_bounds__(64, RT_MIN_WAVES) void compat_kernel(KParams p) {
+  const int lane = threadIdx.x & 63;
+  WorkCount wc = {};
+  __shared__ float4 s_stack[ACCEL == RT_ACCEL_FLAT_D ? 1 : kStackArea];
+  __shared__ float4 s_stage[ACCEL == RT_ACCEL_FLAT_D ? kStageFlat : kStageOct];
+  const size_t gl = (size_t)blockIdx.x * 64 + (size_t)lane;
+  Stack stk;
+  stk.idx = (uint32_t*)s_stack;
+  stk.tt = (float*)s_stack + kLdsStack * 64;
+  stk.spill = p.spill + gl * kSpillStack;
+  stk.lane = lane;
+  stk.sp = 0;
+  WaveCtx w;
+  w.stk2 = s_stack;
+  w.stkm = (uint64_t*)(s_stack + 2 * kStack2);
+  w.stage = s_stage;
+  w.lane = lane;
+  uint32_t* img = (uint32_t*)p.out;
+  for (;;) {
+    uint32_t t = 0;
+    if (lane == 0) t = atomicAdd(p.tile_counter, 1u);
+    t = uni(t);
+    if (t >= (uint32_t)p.ntiles_total) break;
+    const int ty = (int)(t / (uint32_t)p.tiles_x), tx = (int)(t % (uint32_t)p.tiles_x);
+    const int py = ty * 8 + (lane >> 3), px = tx * 8 + (lane & 7);
+    const bool valid = py < p.H && px < p.W;
+    wc.pixels += (uint32_t)__popcll(__ballot(valid));
+    // gpu/raytracer.cu:97-103
+    f3 o = add(add(p.C, scale(p.u, (float)(px - p.W / 2))), scale(p.v, (float)(py - p.H / 2)));
+    f3 d = normalize(sub(p.pos, o));
+    col color = col{0.0f, 0.0f, 0.0f};
+    float nr = 1.0f;
+    int max_bounce = 10;
+    bool alive = valid;
+    for (int depth = 0;; depth++) {  // gpu/raytracer.cu:113-120
+      const uint64_t am = __ballot(alive);
+      if (am == 0) break;
+      wc.closest += (uint32_t)__popcll(am);
+      Ray r = make_ray(p, o, d, depth == 0 ? p.eps_rel_cam : p.eps_rel);
+      Best b;
+      b.dist = __builtin_inff();
+      b.t_cut = __builtin_inff();
+      b.prim = 0xffffffffu;
+      b.obj = 0;
+      b.u = b.v = 0.0f;
+      b.t = 0.0f;
+      closest_q<ACCEL, false, POL>(p, r, alive, depth, b, stk, w, wc);
+      bool hit = alive && b.dist != __builtin_inff();
+      f3 N = f3{0.0f, 0.0f, 0.0f};
+      wc.hits += (uint32_t)__popcll(__ballot(hit));
+      bool zero = false;
+      if (hit) {
+        const float* nm = p.nrm + 9 * (size_t)b.prim;
+        float w0 = 1.0f - b.u - b.v;
+        N = add(add(scale(ld3(nm), w0), scale(ld3(nm + 3), b.u)), scale(ld3(nm + 6), b.v));
+        zero = is_zero(N);
+      }
+      wc.zero_normal += (uint32_t)__popcll(__ballot(zero));
+      hit = hit && !zero;
+      const float* m = p.mat + RT_MAT_FLOATS_D * (hit ? b.obj : 0u);
+      f3 P = hit ? hit_point(r, b.t) : o;
+      col local = apply_light8<ACCEL, POL>(p, hit, m, P, N, stk, w, wc);  // trace(), :31-46
+      if (alive) {
+        if (!hit) local = col{0.0f, 0.0f, 0.0f};
+        const float loc_nr = hit ? m[10] : 0.0f;
+        if (hit && m[10] > 0.0f) {
+          d = bounce_dir(d, N);
+          o = P;
+        }
+        color = add8(color, mul8(local, nr));
+        nr *= loc_nr;
+        alive = nr > 0.01f && max_bounce-- > 0;
+      }
+    }
+    if (valid)
+      img[(size_t)py * (size_t)p.W + (size_t)px] = (uint32_t)color.r | ((uint32_t)color.g << 8) |
+                                                   ((uint32_t)color.b << 16) | 0xff000000u;
+  }
+  uint32_t v[RT_NSTATS] = {wc.closest, wc.shadow, wc.pixels, wc.nodes, wc.tris, wc.overflow,
+                           wc.zero_normal, wc.hits};
+#pragma unroll
+  for (int k = 0; k < RT_NSTATS; k++)
+    if (lane == 0 && v[k]) atomicAdd(p.stats + k, (unsigned long long)v[k]);
+}
+
+// gpu/raytracer.cu:48-85: output pixel (row R, column c) of the W x H image
+// (PNG order: gpu/rt.cpp writes buffer rows top down) is the 3x3 block of
+// high-resolution pixels px = 3 (W - 1 - c) .., py = 3 (H - 1 - R) .., summed
+// as floats, / (255 * 9), through init_color.
+__global__ __launch_bounds__(256) void downscale_kernel(const uint32_t* __restrict__ hi,
+                                                        uint32_t* __restrict__ lo, int W, int H) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= W * H) return;
+  const int R = idx / W, c = idx % W;
+  const int px = W - 1 - c, py = H - 1 - R, HW = 3 * W;
+  float r = 0.0f, g = 0.0f, b = 0.0f;
+  for (int hy = 3 * py; hy < 3 * py + 3; ++hy)
+    for (int hx = 3 * px; hx < 3 * px + 3; ++hx) {
+      const uint32_t q = hi[(size_t)hy * HW + hx];
+      r += (float)(q & 0xffu);
+      g += (float)((q >> 8) & 0xffu);
+      b += (float)((q >> 16) & 0xffu);
+    }
+  const float ali2 = 255.0f * 3.0f * 3.0f;
+  col e = init8(r / ali2, g / ali2, b / ali2);
+  lo[idx] = (uint32_t)e.r | ((uint32_t)e.g << 8) | ((uint32_t)e.b << 16) | 0xff000000u;
+}
+
 // tiles of all ranks (rank-major, as gathered) -> PPM-order image
 __global__ __launch_bounds__(256) void assemble_kernel(const float* __restrict__ tiles,
                                                        float* __restrict__ rgb, int W, int H,
@@ -1227,5 +1424,21 @@ extern "C" hipError_t rt_launch_assemble(const float* tiles, float* rgb, int W, 
   dim3 g((unsigned)((npx + 255) / 256)), b(256);
   hipLaunchKernelGGL(rt::assemble_kernel, g, b, 0, stream, tiles, rgb, W, H, tiles_x, ntiles,
                      nranks, tiles_per_rank);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t rt_launch_compat(const KParams* p, int accel, int grid, hipStream_t stream) {
+  dim3 g(grid), b(64);
+  if (accel == RT_ACCEL_FLAT_D)
+    hipLaunchKernelGGL((rt::compat_kernel<RT_ACCEL_FLAT_D, 0>), g, b, 0, stream, *p);
+  else
+    hipLaunchKernelGGL((rt::compat_kernel<RT_ACCEL_OCTREE_D, RT_POLICY_DEFAULT>), g, b, 0, stream, *p);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t rt_launch_downscale(const uint32_t* hi, uint32_t* lo, int W, int H,
+                                          hipStream_t stream) {
+  const int n = W * H;
+  hipLaunchKernelGGL(rt::downscale_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, hi, lo, W, H);
   return hipGetLastError();
 }

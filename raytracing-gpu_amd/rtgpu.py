@@ -124,6 +124,7 @@ _PROTOS = [
     ("rt_scene_triangle_count", C.c_size_t, [C.POINTER(SceneStruct)]),
     ("rt_scene_free", None, [C.POINTER(SceneStruct)]),
     ("rt_ppm_write", C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_void_p]),
+    ("rt_png_write_rgba", C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_void_p]),
     ("rt_frame_from_camera", C.c_int, [C.POINTER(Camera), C.POINTER(Frame)]),
     ("rt_accel_build_info", C.c_int, [C.POINTER(SceneStruct), C.c_int, C.POINTER(AccelInfo)]),
     ("rt_accel_validate", C.c_int, [C.POINTER(SceneStruct), C.c_int]),
@@ -142,6 +143,7 @@ _PROTOS = [
     ("rt_hip_set_count_work", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_set_cull_slack", C.c_int, [C.c_void_p, C.c_float]),
     ("rt_hip_set_camera_slack", C.c_int, [C.c_void_p, C.c_float]),
+    ("rt_hip_cand_verify", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
     ("rt_hip_set_exact_camera", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_set_policy", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_tile_cycles", C.c_int, [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_size_t]),
@@ -160,6 +162,9 @@ _PROTOS = [
     ("rt_hip_memcpy_d2h", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
     ("rt_hip_memcpy_h2d", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
     ("rt_raytrace", C.c_int, [C.c_char_p, C.c_char_p]),
+    ("rt_hip_render_compat", C.c_int, [C.c_void_p, C.POINTER(Camera), C.c_void_p,
+                                       C.POINTER(Stats)]),
+    ("rt_raytrace_gpu", C.c_int, [C.c_char_p, C.c_char_p, C.c_int]),
     ("rt_raytrace_multi", C.c_int, [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.POINTER(Stats),
                                     C.POINTER(C.c_double)]),
 ]
@@ -405,6 +410,14 @@ class Context:
     def set_cull_slack(self, ulps):
         _check(lib().rt_hip_set_cull_slack(self.h, float(ulps)), "cull_slack")
 
+    def cand_verify(self, frame, rank=0, nranks=1):
+        """Host re-derivation of the last render's candidate lists:
+        {listed, entries, fp_mismatch, tile_mismatch, global}."""
+        out = (C.c_ulonglong * 5)()
+        _check(lib().rt_hip_cand_verify(self.h, C.byref(frame), rank, nranks, out), "cand_verify")
+        return dict(zip(("listed", "entries", "fp_mismatch", "tile_mismatch", "global"),
+                        (int(x) for x in out)))
+
     def set_camera_slack(self, ulps):
         _check(lib().rt_hip_set_camera_slack(self.h, float(ulps)), "camera_slack")
 
@@ -431,6 +444,17 @@ class Context:
                "rt_hip_render_image")
         return img, st.as_dict()
 
+    def render_compat(self, camera):
+        """gpu/rt compatibility mode (rt_hip_render_compat) -> (H, W, 4)
+        uint8 RGBA in gpu/rt's PNG row order, stats."""
+        img = np.empty((camera.height, camera.width, 4), np.uint8)
+        st = Stats()
+        cam = Camera()
+        C.pointer(cam)[0] = camera
+        _check(lib().rt_hip_render_compat(self.h, C.byref(cam), img.ctypes.data_as(C.c_void_p),
+                                          C.byref(st)), "rt_hip_render_compat")
+        return img, st.as_dict()
+
     def close(self):
         if self.h:
             lib().rt_hip_destroy(self.h)
@@ -447,6 +471,20 @@ def write_ppm(path, rgb):
     rgb = np.ascontiguousarray(rgb, dtype=np.float32)
     h, w, _ = rgb.shape
     _check(lib().rt_ppm_write(os.fsencode(path), w, h, rgb.ctypes.data_as(C.c_void_p)), "ppm")
+
+
+def write_png(path, rgba):
+    """8-bit RGBA PNG (rt_png_write_rgba); rgba = (H, W, 4) uint8."""
+    rgba = np.ascontiguousarray(rgba, dtype=np.uint8)
+    h, w, _ = rgba.shape
+    _check(lib().rt_png_write_rgba(os.fsencode(path), w, h, rgba.ctypes.data_as(C.c_void_p)), "png")
+
+
+def raytrace_gpu(input_path, output_path, accel=None):
+    """Drop-in for gpu/rt's main (gpu/rt.cpp:56-97): PNG in compatibility mode."""
+    a = -1 if accel is None else (ACCEL[accel] if isinstance(accel, str) else accel)
+    _check(lib().rt_raytrace_gpu(os.fsencode(input_path), os.fsencode(output_path), a),
+           "rt_raytrace_gpu")
 
 
 def raytrace(input_path, output_path, gpus=1, accel=None):
