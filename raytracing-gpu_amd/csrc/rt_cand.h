@@ -46,6 +46,8 @@ struct CandParams {
   uint32_t* ctr;          // [1] global prims, [2] big footprints, [3] list length
   uint32_t* big;          // nprim: list entries with big footprints (rt_cand.hip kSmallRows)
   float* skip;            // nprim: depth-skip bound of each listed prim
+  uint32_t* big_lane;     // big_cap x 64: per big footprint, each lane's row-count subtotal
+  uint32_t big_cap;       // (big_count_kernel -> big_kernel; beyond it big_kernel recounts)
 };
 
 // Host mirror for surveys (same classify/raster code): safe / footprint /

@@ -601,6 +601,7 @@ __global__ __launch_bounds__(64) void big_count_kernel(CandParams p) {
     uint32_t cnt = 0;
     if (raster_rows(p, fp, r0, r1))
       for (int ty = (r0 >> 3) + lane; ty <= (r1 >> 3); ty += 64) cnt += count_row(p, fp, ty, r0, r1);
+    if (b < p.big_cap) p.big_lane[(size_t)b * 64 + lane] = cnt;  // big_kernel's offsets
     cnt = wave_sum(cnt);
     if (lane == 0) p.visits[j] = cnt;
   }
@@ -668,7 +669,9 @@ __global__ __launch_bounds__(64) void big_kernel(CandParams p) {
     const bool rows = raster_rows(p, fp, r0, r1);
     const int ty0 = r0 >> 3, ty1 = r1 >> 3;
     uint32_t cnt = 0;
-    if (rows)
+    if (b < p.big_cap)
+      cnt = p.big_lane[(size_t)b * 64 + lane];  // big_count_kernel's row subtotals
+    else if (rows)
       for (int ty = ty0 + lane; ty <= ty1; ty += 64) cnt += count_row(p, fp, ty, r0, r1);
     uint32_t o = p.off[j] + wave_excl_scan(cnt, lane);
     if (rows)

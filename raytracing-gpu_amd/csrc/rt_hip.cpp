@@ -88,6 +88,7 @@ struct rt_hip_ctx {
   uint32_t* d_cand_big = nullptr;     // nprim
   uint32_t* d_cand_ctr = nullptr;     // 4
   float* d_cand_skip = nullptr;       // nprim
+  uint32_t* d_cand_big_lane = nullptr;  // kBigLaneCap x 64 lane subtotals of big footprints
   uint32_t* d_prim_leaf = nullptr;    // nprim: a leaf holding each prim (camera-independent)
   uint32_t* d_cand = nullptr;
   size_t cand_cap = 0, cand_tiles_cap = 0;
@@ -165,6 +166,7 @@ extern "C" void rt_hip_destroy(rt_hip_ctx* c) {
   (void)hipFree(c->d_cand_global);
   (void)hipFree(c->d_cand_big);
   (void)hipFree(c->d_cand_ctr);
+  (void)hipFree(c->d_cand_big_lane);
   (void)hipFree(c->d_cand_skip);
   (void)hipFree(c->d_prim_leaf);
   (void)hipFree(c->d_cand);
@@ -510,6 +512,10 @@ static int grow_dev(T** p, size_t* cap, size_t need) {
 
 static double d3dot(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
 
+// big footprints whose per-lane row counts big_count_kernel keeps for
+// big_kernel (C5: ~5e4 per frame; beyond this big_kernel recounts)
+static constexpr uint32_t kBigLaneCap = 1u << 17;
+
 // Frame constants of the candidate lists for rank/nranks (no device work).
 static int cand_params(const rt_frame* f, const float scene_c[3], float scene_r, float eps_ulps,
                        double bound_scale, int rank, int nranks, CandParams* out) {
@@ -635,6 +641,7 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
     HIP_TRY(hipMalloc((void**)&c->d_cand_big, (np + 1) * sizeof(uint32_t)));
     HIP_TRY(hipMalloc((void**)&c->d_cand_ctr, 4 * sizeof(uint32_t)));
     HIP_TRY(hipMalloc((void**)&c->d_cand_skip, (np + 1) * sizeof(float)));
+    HIP_TRY(hipMalloc((void**)&c->d_cand_big_lane, (size_t)kBigLaneCap * 64 * sizeof(uint32_t)));
     HIP_TRY(hipHostMalloc((void**)&c->h_cand, 4 * sizeof(uint32_t), hipHostMallocDefault));
   }
   if (nt + 1 > c->cand_tiles_cap) {
@@ -651,6 +658,8 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
   cp.big = c->d_cand_big;
   cp.ctr = c->d_cand_ctr;
   cp.skip = c->d_cand_skip;
+  cp.big_lane = c->d_cand_big_lane;
+  cp.big_cap = kBigLaneCap;
   HIP_TRY(hipMemsetAsync(c->d_cand_visits + np, 0, sizeof(uint32_t), s));
   HIP_TRY(hipMemsetAsync(c->d_cand_ctr, 0, 4 * sizeof(uint32_t), s));
   size_t tb = 0;
