@@ -187,6 +187,9 @@ def main():
                     help="octree culling slack override (tuning; default = library default)")
     ap.add_argument("--camera-slack", type=float, default=None,
                     help="camera-ray culling slack override (tuning; default = library default)")
+    ap.add_argument("--policy", type=int, default=None,
+                    help="octree traversal policy (A/B only; rt_hip_set_policy, default = library "
+                         "default 0)")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary (tools/pmc_traffic.py) to report as roofline.traffic")
     ap.add_argument("--valu-json", default=None,
@@ -214,6 +217,8 @@ def main():
         ctx.set_cull_slack(args.cull_slack)
     if args.camera_slack is not None:
         ctx.set_camera_slack(args.camera_slack)
+    if args.policy is not None:
+        ctx.set_policy(args.policy)
     info = ctx.info()
     log(f"[rank {rank}] scene {ntri} triangles, accel {wl['accel']}: {info['tri_refs']} records, "
         f"{info['nodes']} nodes, build {info['build_seconds']:.1f}s, setup {time.perf_counter()-t:.1f}s")
@@ -289,6 +294,10 @@ def main():
     phase_share = ({k: round(v / sum(cyc), 4) for k, v in
                     zip(("camera_walk", "camera_candidates", "secondary_walks", "shadow_queries"), cyc)}
                    if sum(cyc) > 0 else None)
+    if phase_share:  # the shadow share split by light type (cpu/light.c:49 vs :70)
+        sd = float(work["cycles_shadow_directional"]) / sum(cyc)
+        phase_share["shadow_directional"] = round(sd, 4)
+        phase_share["shadow_point"] = round(phase_share["shadow_queries"] - sd, 4)
     value = queries * args.steps / el / 1e6
     # algorithmic bytes of one render launch (per rank, averaged over ranks)
     alg_bytes = (wq * RAY_BYTES + nodes * NODE_BYTES + tris * TRI_BYTES + whits * NORMAL_BYTES +
@@ -298,7 +307,7 @@ def main():
     traffic = traffic_hi = None
     traffic_src = None
     if world == 1 and args.traffic_json is None and args.cull_slack is None and \
-            args.camera_slack is None:
+            args.camera_slack is None and args.policy is None:
         # default run: the newest committed rocprofv3 PMC pass of this
         # workload (profiles/r*_<workload>/, tools/gpu_profile.sh); a PMC
         # pass cannot run inside the bench, so the line says where it came from

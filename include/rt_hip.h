@@ -73,6 +73,7 @@ typedef struct rt_stats {
    * the camera candidate tests, the secondary closest-hit walks and the
    * shadow queries (summed over waves) */
   unsigned long long cycles_camera, cycles_cand, cycles_secondary, cycles_shadow;
+  unsigned long long cycles_shadow_directional;  /* the directional-light share of cycles_shadow */
 } rt_stats;
 
 /* Sizes of the device-side scene image, for the roofline accounting. */
@@ -185,9 +186,11 @@ int rt_cand_survey(const rt_scene *scene, float eps_ulps, double bound_scale, in
 /* Test hook: after an rt_hip_render of (frame, rank, nranks) with exact
  * camera rays, re-derive its candidate lists on the host from the same code
  * and compare.  out = {listed prims, entries, footprint mismatches, tiles
- * whose list differs, prims on the global list}. */
+ * whose list differs, prims on the global list, fast-path filter violations
+ * (a prim not listed whose footprint reaches this rank), prims the fast
+ * path's rank/frame filter dropped}. */
 int rt_hip_cand_verify(rt_hip_ctx *ctx, const rt_frame *frame, int rank, int nranks,
-                       unsigned long long out[5]);
+                       unsigned long long out[7]);
 
 /* d_gathered = nranks consecutive tile buffers (rank-major, as an RCCL gather
  * delivers them); writes the PPM-order image (W*H*3 floats) to d_rgb. */

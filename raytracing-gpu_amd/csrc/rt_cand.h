@@ -61,7 +61,7 @@ extern "C" int rt_cand_survey_host(const CandParams* p, const float* tri, const 
 extern "C" int rt_cand_verify_host(const CandParams* p, const float* tri, const float* node,
                                    const uint32_t* prim_leaf, const uint32_t* list, uint32_t nlist,
                                    const void* fp_dev, const uint32_t* start, const uint32_t* cand,
-                                   uint32_t ntiles, unsigned long long out[5]);
+                                   uint32_t ntiles, unsigned long long out[7]);
 // prim_leaf[prim] = a leaf node holding a record of prim (scene build time)
 extern "C" hipError_t rt_cand_prim_leaf(const float4* node, uint32_t nnode, const float4* tri,
                                         uint32_t* prim_leaf, hipStream_t s);

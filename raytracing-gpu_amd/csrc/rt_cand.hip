@@ -263,11 +263,82 @@ RTC_FN int classify(const CandParams& p, const float* r, const float* leafbox, F
   return FOOTPRINT;
 }
 
+// Tiles g in [lo, hi] (global indices) with g % n == r.
+__host__ __device__ inline uint32_t rank_tiles(uint32_t lo, uint32_t hi, uint32_t n, uint32_t r) {
+  // tiles g = r + m n with g in [lo, hi]: m in [ceil((lo - r) / n), floor((hi - r) / n)]
+  const long long mlo = lo <= r ? 0 : ((long long)lo - r + n - 1) / n;
+  const long long mhi = hi < r ? -1 : ((long long)hi - r) / n;
+  return mhi >= mlo ? (uint32_t)(mhi - mlo + 1) : 0u;
+}
+
+// Can a footprint inside the ball (q, rb) -- every candidate crossing point
+// of the triangle lies in it -- reach a tile of this rank?  The ball's
+// bounding box projects (through the eye, on one side of the eye plane) into
+// the image rectangle spanned by its corners' projections; widened by the
+// float deviation of camera lines (classify's dimg) plus 2 pixels, it gives
+// the pixel rows and columns the footprint can touch, clipped to the frame.
+// false = none of this rank's tiles (off-frame, or between the rank's tiles
+// of an interleaved split); true whenever unsure.
+RTC_FN bool rank_may_touch(const CandParams& p, const double q[3], double rb) {
+  const double dq[3] = {q[0] - p.pos[0], q[1] - p.pos[1], q[2] - p.pos[2]};
+  const double R = sqrt(dq[0] * dq[0] + dq[1] * dq[1] + dq[2] * dq[2]);
+  if (!(R > 2.0 * rb + 1e-6)) return true;
+  double kmn = 1e300, kmx = -1e300, lmn = 1e300, lmx = -1e300;
+  int side = 0;
+  for (int c = 0; c < 8; c++) {
+    double Y[3];
+    for (int a = 0; a < 3; a++) Y[a] = dq[a] + (((c >> a) & 1) ? rb : -rb);
+    const double yn = Y[0] * p.n[0] + Y[1] * p.n[1] + Y[2] * p.n[2];
+    const int sd = yn > 1e-6 * (R + rb) ? 1 : (yn < -1e-6 * (R + rb) ? -1 : 0);
+    if (sd == 0 || (side != 0 && sd != side)) return true;
+    side = sd;
+    const double lam = p.plane / yn;
+    double w[3];
+    for (int a = 0; a < 3; a++) w[a] = p.pos[a] + lam * Y[a] - p.C[a];
+    const double b1 = w[0] * p.u[0] + w[1] * p.u[1] + w[2] * p.u[2];
+    const double b2 = w[0] * p.v[0] + w[1] * p.v[1] + w[2] * p.v[2];
+    const double k = p.ginv[0] * b1 + p.ginv[1] * b2, l = p.ginv[1] * b1 + p.ginv[2] * b2;
+    kmn = fmin(kmn, k);
+    kmx = fmax(kmx, k);
+    lmn = fmin(lmn, l);
+    lmx = fmax(lmx, l);
+  }
+  const double m = 2.0 + 1.5 * p.gscale * (p.dline * (1.0 + p.lmax / (R - 2.0 * rb)) + p.dorig);
+  kmn -= m;
+  kmx += m;
+  lmn -= m;
+  lmx += m;
+  // samples of pixel (r, c): k in [W/2 - c, W/2 - c + 1/2], l likewise (raster_rows)
+  const double hw_ = (double)(p.W / 2), hh = (double)(p.H / 2);
+  const int r0 = (int)fmin(fmax(0.0, ceil(hh - lmx)), (double)p.H);
+  const int r1 = (int)fmax(fmin((double)(p.H - 1), floor(hh - lmn + 0.5)), -1.0);
+  const int c0 = (int)fmin(fmax(0.0, ceil(hw_ - kmx)), (double)p.W);
+  const int c1 = (int)fmax(fmin((double)(p.W - 1), floor(hw_ - kmn + 0.5)), -1.0);
+  if (r0 > r1 || c0 > c1) return false;  // off the frame
+  const uint32_t n = (uint32_t)p.nranks, rk = (uint32_t)p.rank;
+  if (n == 1) return true;
+  const int tx0 = c0 >> 3, tx1 = c1 >> 3, ty0 = r0 >> 3, ty1 = r1 >> 3;
+  if ((uint32_t)p.tiles_x % n == 0) {  // rank = tile column mod n in every row
+    const uint32_t span = (uint32_t)(tx1 - tx0);
+    return span + 1 >= n || (rk + n - (uint32_t)tx0 % n) % n <= span;
+  }
+  if (ty1 - ty0 >= 8) return true;
+  for (int ty = ty0; ty <= ty1; ty++) {
+    const uint32_t base = (uint32_t)ty * (uint32_t)p.tiles_x;
+    if (rank_tiles(base + (uint32_t)tx0, base + (uint32_t)tx1, n, rk)) return true;
+  }
+  return false;
+}
+
+enum { Q_SAFE = 0, Q_LIST = 1, Q_AWAY = 2 };
+
 // Fast, conservative float version of classify()'s SAFE test (no leaf box):
 // every quantity is a positive magnitude computed in a few float operations,
 // bounded with explicit margins, so a true result is a proof on its own.
-// Most triangles of a frame take this exit.
-__device__ __forceinline__ bool quick_safe(const CandParams& p, const float* r) {
+// Most triangles of a frame take this exit.  A triangle it cannot prove safe
+// whose error region provably stays off this rank's tiles (rank_may_touch)
+// is Q_AWAY: its footprint would be empty here, so it is not classified.
+RTC_FN int quick_class(const CandParams& p, const float* r) {
   const float fe = 5.9604645e-8f;
   const float e1x = r[3], e1y = r[4], e1z = r[5], e2x = r[6], e2y = r[7], e2z = r[8];
   const float l1 = sqrtf(e1x * e1x + e1y * e1y + e1z * e1z) * 1.00001f;
@@ -276,11 +347,11 @@ __device__ __forceinline__ bool quick_safe(const CandParams& p, const float* r) 
   const float nl = sqrtf(nx * nx + ny * ny + nz * nz);
   // |n| and its direction carry an absolute error <= 4 eps |e1| |e2|
   const float nerr = 4.0f * fe * l1 * l2;
-  if (!(nl > 64.0f * nerr)) return false;
+  if (!(nl > 64.0f * nerr)) return Q_LIST;
   const float nlo = nl - nerr;
   float e_a = (float)p.c_a * fe * l1 * l2 * 1.0001f;
   const float amin = 9.99999975e-08f;
-  if (amin < 2.0f * e_a) return false;
+  if (amin < 2.0f * e_a) return Q_LIST;
   const float px = (float)p.pos[0] - r[0], py = (float)p.pos[1] - r[1], pz = (float)p.pos[2] - r[2];
   const float pvl = sqrtf(px * px + py * py + pz * pz) * 1.00001f + 1e-6f;
   const float deye = fabsf(nx * px + ny * py + nz * pz) / nl;
@@ -312,17 +383,17 @@ __device__ __forceinline__ bool quick_safe(const CandParams& p, const float* r) 
   }
   vmax = vmax * 1.00002f + 1e-6f;
   float num = deye_lb - (float)p.dline - kmax_ch - 1e-5f * (deye + kmax_ch);
-  if (!(num > 0.0f)) return false;
+  if (!(num > 0.0f)) return Q_LIST;
   float cl = num / (vmax + (float)p.dline) * 0.9999f;
   float h = H(cl, a, rho);
   // componentwise second round (see classify): the candidate lines cross
   // T_D, inside the ball (centroid, max vertex distance + h)
+  const float cx = (e1x + e2x) / 3.0f, cy = (e1y + e2y) / 3.0f, cz = (e1z + e2z) / 3.0f;  // - v0
+  float rv = sqrtf(cx * cx + cy * cy + cz * cz);  // max vertex distance from the centroid
+  rv = fmaxf(rv, sqrtf((e1x - cx) * (e1x - cx) + (e1y - cy) * (e1y - cy) + (e1z - cz) * (e1z - cz)));
+  rv = fmaxf(rv, sqrtf((e2x - cx) * (e2x - cx) + (e2y - cy) * (e2y - cy) + (e2z - cz) * (e2z - cz)));
   {
-    const float cx = (e1x + e2x) / 3.0f, cy = (e1y + e2y) / 3.0f, cz = (e1z + e2z) / 3.0f;  // - v0
-    float rq = sqrtf(cx * cx + cy * cy + cz * cz);
-    rq = fmaxf(rq, sqrtf((e1x - cx) * (e1x - cx) + (e1y - cy) * (e1y - cy) + (e1z - cz) * (e1z - cz)));
-    rq = fmaxf(rq, sqrtf((e2x - cx) * (e2x - cx) + (e2y - cy) * (e2y - cy) + (e2z - cz) * (e2z - cz)));
-    rq = (rq + h) * 1.0001f + 1e-6f + (float)p.dline;
+    float rq = (rv + h) * 1.0001f + 1e-6f + (float)p.dline;
     const float qx = cx - px, qy = cy - py, qz = cz - pz;  // centroid - pos
     const float R = sqrtf(qx * qx + qy * qy + qz * qz) * 0.99999f;
     if (R > 2.0f * rq) {
@@ -354,7 +425,12 @@ __device__ __forceinline__ bool quick_safe(const CandParams& p, const float* r) 
   const float rmax = vmax + h;
   const float derr = (e_eq / (a * (1.0f - rho)) + (rmax + (float)p.lmax) * (rho + 4.0f * fe) / (1.0f - rho) +
                       4.0f * fe * ((float)p.omax + rmax + (float)p.lmax)) * 1.0001f;
-  return h <= (float)p.eps_avail * 0.9999f && derr <= 2.0f * (float)p.eps_avail * 0.9999f;
+  if (h <= (float)p.eps_avail * 0.9999f && derr <= 2.0f * (float)p.eps_avail * 0.9999f) return Q_SAFE;
+  // T_D lies in the ball (centroid, rv + h): every corner of T_D is within
+  // H(cl) of its vertex.  The centroid in double from the record's floats.
+  const double q[3] = {(double)r[0] + (double)cx, (double)r[1] + (double)cy, (double)r[2] + (double)cz};
+  const double rb = ((double)rv + (double)h) * 1.001 + 1e-5 + 1e-6 * (fabs(q[0]) + fabs(q[1]) + fabs(q[2]));
+  return rank_may_touch(p, q, rb) ? Q_LIST : Q_AWAY;
 }
 
 // Tiles of this rank whose camera samples can be candidates for the
@@ -465,14 +541,6 @@ __host__ __device__ void raster_row(const CandParams& p, const Footprint& fp, in
     if (!(tx >= a0 && tx <= a1)) put(tx);
 }
 
-// Tiles g in [lo, hi] (global indices) with g % n == r.
-__host__ __device__ inline uint32_t rank_tiles(uint32_t lo, uint32_t hi, uint32_t n, uint32_t r) {
-  // tiles g = r + m n with g in [lo, hi]: m in [ceil((lo - r) / n), floor((hi - r) / n)]
-  const long long mlo = lo <= r ? 0 : ((long long)lo - r + n - 1) / n;
-  const long long mhi = hi < r ? -1 : ((long long)hi - r) / n;
-  return mhi >= mlo ? (uint32_t)(mhi - mlo + 1) : 0u;
-}
-
 // Number of tiles raster_row emits for row ty, without visiting them.
 __host__ __device__ inline uint32_t count_row(const CandParams& p, const Footprint& fp, int ty, int r0,
                                               int r1) {
@@ -524,7 +592,7 @@ constexpr int kBigWaves = 4096;
 __global__ __launch_bounds__(256) void quick_kernel(CandParams p) {
   const uint32_t prim = blockIdx.x * blockDim.x + threadIdx.x;
   if (prim >= p.nprim) return;
-  p.visits[prim] = quick_safe(p, (const float*)(p.tri + 3 * (size_t)prim)) ? 0u : 1u;
+  p.visits[prim] = quick_class(p, (const float*)(p.tri + 3 * (size_t)prim)) == Q_LIST ? 1u : 0u;
 }
 
 __global__ __launch_bounds__(256) void scatter_kernel(CandParams p) {
@@ -788,12 +856,13 @@ extern "C" int rt_cand_survey_host(const CandParams* p, const float* tri, const 
 // same f64 bits; the safe ones have no tiles), every kept footprint compared
 // bit for bit, and every tile's list equal, as a multiset, to the tiles the
 // host raster gives the listed footprints.  out: [0] listed prims, [1] entries,
-// [2] footprint mismatches, [3] tile-list mismatches (tiles), [4] globals.
+// [2] footprint mismatches, [3] tile-list mismatches (tiles), [4] globals,
+// [5] fast-path filter violations, [6] prims the rank/frame filter dropped.
 extern "C" int rt_cand_verify_host(const CandParams* p, const float* tri, const float* node,
                                    const uint32_t* prim_leaf, const uint32_t* list, uint32_t nlist,
                                    const void* fp_dev, const uint32_t* start, const uint32_t* cand,
-                                   uint32_t ntiles, unsigned long long out[5]) {
-  for (int k = 0; k < 5; k++) out[k] = 0;
+                                   uint32_t ntiles, unsigned long long out[7]) {
+  for (int k = 0; k < 7; k++) out[k] = 0;
   out[0] = nlist;
   out[1] = start[ntiles];
   const rtc::Footprint* fpd = (const rtc::Footprint*)fp_dev;
@@ -822,6 +891,29 @@ extern "C" int rt_cand_verify_host(const CandParams* p, const float* tri, const 
     if (same && fp.tri_ok) same = d.dimg == fp.dimg;
     for (int k = 0; k < 3 && same && fp.tri_ok; k++) same = d.k[k] == fp.k[k] && d.l[k] == fp.l[k];
     if (!same) out[2]++;
+  }
+  // prims the fast path did not list: proven safe, or their footprint has no
+  // tile of this rank (the rank/frame filter must never drop a needed one)
+  {
+    std::vector<unsigned char> listed(p->nprim + 1, 0);
+    for (uint32_t j = 0; j < nlist; j++) listed[list[j]] = 1;
+    for (uint32_t prim = 0; prim < p->nprim; prim++) {
+      const int qc = rtc::quick_class(*p, tri + 12 * (size_t)prim);
+      if (listed[prim]) {
+        if (qc != rtc::Q_LIST) out[5]++;
+        continue;
+      }
+      if (qc == rtc::Q_SAFE) continue;
+      if (qc == rtc::Q_LIST) {  // the device should have listed it
+        out[5]++;
+        continue;
+      }
+      rtc::Footprint fp;
+      const float* lb = prim_leaf ? node + 8 * (size_t)prim_leaf[prim] : nullptr;
+      const int c = rtc::classify(*p, tri + 12 * (size_t)prim, lb, fp);
+      if (c == rtc::GLOBAL || (c == rtc::FOOTPRINT && rtc::raster_count(*p, fp) != 0)) out[5]++;
+      out[6]++;
+    }
   }
   for (uint32_t t = 0; t < ntiles; t++) {
     std::vector<uint32_t> got(cand + start[t], cand + start[t + 1]);

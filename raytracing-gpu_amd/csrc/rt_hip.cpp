@@ -410,7 +410,7 @@ extern "C" int rt_cand_survey(const rt_scene* scene, float eps_ulps, double boun
 }
 
 extern "C" int rt_hip_cand_verify(rt_hip_ctx* c, const rt_frame* f, int rank, int nranks,
-                                  unsigned long long out[5]) {
+                                  unsigned long long out[7]) {
   if (!c || !f || !out) return rt_set_error(RT_EINVAL, "null argument");
   if (!c->d_cand_start || !c->d_cand || !c->d_cand_list)
     return rt_set_error(RT_EINVAL, "no candidate lists (render a frame with exact camera rays first)");
@@ -839,6 +839,7 @@ extern "C" int rt_hip_stats(rt_hip_ctx* c, rt_stats* out) {
   out->cycles_cand = h[13];
   out->cycles_secondary = h[14];
   out->cycles_shadow = h[15];
+  out->cycles_shadow_directional = h[16];
   out->cand_prims = c->cand_prims;
   out->cand_entries = c->cand_entries;
   out->cand_global = c->cand_global;

@@ -850,7 +850,11 @@ __device__ col apply_light(const KParams& p, bool hit, const float* m, f3 P, f3 
     } else if (type == 1 || type == 2) {
       const uint64_t c0 = COUNT ? __builtin_readcyclecounter() : 0ull;
       bool sh = shadow_q<ACCEL, COUNT, POL>(p, P, shadow_dir(type, lv, P), type, hit, s, w, wc);
-      if (COUNT) wc.cy_shadow += (uint32_t)(__builtin_readcyclecounter() - c0);
+      if (COUNT) {
+        const uint32_t dc = (uint32_t)(__builtin_readcyclecounter() - c0);
+        wc.cy_shadow += dc;
+        if (type == 1) wc.cy_shadow_dir += dc;
+      }
       if (hit && !sh) acc = color_add(acc, light_lit(type, lc, lv, m, P, N));
     }
   }
@@ -1116,7 +1120,8 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES) void render_kernel(KParams p) {
   uint32_t v[RT_NSTATS] = {wc.closest, wc.shadow,   wc.pixels,      wc.nodes,
                            wc.tris,    wc.overflow, wc.zero_normal, wc.hits,
                            wc.cl_nodes, wc.cl_tris, wc.sh_nodes,   wc.sh_tris,
-                           wc.cy_cam,   wc.cy_cand, wc.cy_sec,     wc.cy_shadow};
+                           wc.cy_cam,   wc.cy_cand, wc.cy_sec,     wc.cy_shadow,
+                           wc.cy_shadow_dir};
 #pragma unroll
   for (int k = 0; k < RT_NSTATS; k++)
     if (lane == 0 && v[k]) atomicAdd(p.stats + k, (unsigned long long)v[k]);

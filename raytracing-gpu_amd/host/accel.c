@@ -727,6 +727,102 @@ int rt_accel_validate(const rt_scene *s, int accel)
   return rc;
 }
 
+/* index of a record of prim `prim` in leaf `n` (it holds one) */
+static size_t leaf_rec_of(const rt_flat_scene *f, uint32_t n, uint32_t prim)
+{
+  const float *nd = f->node + RT_NODE_FLOATS * (size_t)n;
+  uint32_t first, info;
+  memcpy(&first, &nd[3], 4);
+  memcpy(&info, &nd[7], 4);
+  for (uint32_t k = 0; k < RT_LEAF_COUNT(info); k++)
+  {
+    uint32_t q;
+    memcpy(&q, &f->tri[RT_TRI_FLOATS * (size_t)(first + k) + 9], 4);
+    if (q == prim)
+      return first + k;
+  }
+  return first;
+}
+
+/* Coverage: every point of a triangle must lie in the box of some leaf that
+ * holds it -- otherwise a ray through that point could skip the triangle (a
+ * cell wrongly dropped by a builder's plane test or clipping would pass the
+ * per-leaf overlap checks).  Checked on a barycentric grid of 28 points per
+ * triangle (vertices, edges, interior), each against the prim's own leaves,
+ * with the builders' rounding slack. */
+static int validate_coverage(const rt_flat_scene *f, float scene_ext)
+{
+  size_t *cnt = calloc(f->ntri + 1, sizeof *cnt);
+  uint32_t *leaf_of = malloc((f->nrec ? f->nrec : 1) * sizeof *leaf_of);
+  if (!cnt || !leaf_of)
+  {
+    free(cnt);
+    free(leaf_of);
+    return rt_set_error(RT_ENOMEM, "validate coverage");
+  }
+  /* CSR prim -> leaves holding a record of it */
+  for (int pass = 0; pass < 2; pass++)
+  {
+    for (size_t n = 0; n < f->nnode; n++)
+    {
+      const float *nd = f->node + RT_NODE_FLOATS * n;
+      uint32_t first, info;
+      memcpy(&first, &nd[3], 4);
+      memcpy(&info, &nd[7], 4);
+      if (!(info & RT_NODE_LEAF))
+        continue;
+      for (uint32_t k = 0; k < RT_LEAF_COUNT(info); k++)
+      {
+        uint32_t prim;
+        memcpy(&prim, &f->tri[RT_TRI_FLOATS * (size_t)(first + k) + 9], 4);
+        if (pass == 0)
+          cnt[prim + 1]++;
+        else
+          leaf_of[cnt[prim]++] = (uint32_t)n;
+      }
+    }
+    if (pass == 0)
+      for (size_t p = 0; p < f->ntri; p++)
+        cnt[p + 1] += cnt[p];
+    else
+      for (size_t p = f->ntri; p > 0; p--) /* the fill advanced cnt[p] to the next prim's start */
+        cnt[p] = cnt[p - 1];
+    if (pass == 1)
+      cnt[0] = 0;
+  }
+  int rc = RT_OK;
+  const int N = 6;
+  for (size_t p = 0; p < f->ntri && !rc; p++)
+  {
+    /* the prim-order record: a leaf record of prim p carries the same floats */
+    const float *r = f->tri + RT_TRI_FLOATS * (size_t)leaf_rec_of(f, leaf_of[cnt[p]], (uint32_t)p);
+    for (int i = 0; i <= N && !rc; i++)
+      for (int j = 0; i + j <= N && !rc; j++)
+      {
+        double u = (double)i / N, v = (double)j / N, x[3];
+        for (int a = 0; a < 3; a++)
+          x[a] = (double)r[a] + u * (double)r[3 + a] + v * (double)r[6 + a];
+        int in = 0;
+        for (size_t q = cnt[p]; q < cnt[p + 1] && !in; q++)
+        {
+          const float *nd = f->node + RT_NODE_FLOATS * (size_t)leaf_of[q];
+          in = 1;
+          for (int a = 0; a < 3 && in; a++)
+          {
+            double sl = 1e-5 * fabs(x[a]) + 2e-6 * scene_ext + 1e-6;
+            in = x[a] >= (double)nd[a] - sl && x[a] <= (double)nd[4 + a] + sl;
+          }
+        }
+        if (!in)
+          rc = rt_set_error(RT_EINVAL, "prim %zu: point (%g, %g, %g) of the triangle lies in none "
+                            "of its %zu leaves' boxes", p, x[0], x[1], x[2], cnt[p + 1] - cnt[p]);
+      }
+  }
+  free(cnt);
+  free(leaf_of);
+  return rc;
+}
+
 /* Invariants of a flattened scene image (host-built, or downloaded from a
  * device build by rt_hip_accel_validate). */
 int rt_flat_validate(const rt_flat_scene *fp)
@@ -805,5 +901,7 @@ int rt_flat_validate(const rt_flat_scene *fp)
     if (!seen[p])
       rc = rt_set_error(RT_EINVAL, "prim %zu in no leaf", p);
   free(seen);
+  if (!rc)
+    rc = validate_coverage(&f, scene_ext);
   return rc;
 }

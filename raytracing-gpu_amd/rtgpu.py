@@ -91,7 +91,8 @@ class Stats(C.Structure):
                 ("closest_node_lanes", C.c_ulonglong), ("closest_tri_lanes", C.c_ulonglong),
                 ("shadow_node_lanes", C.c_ulonglong), ("shadow_tri_lanes", C.c_ulonglong),
                 ("cycles_camera", C.c_ulonglong), ("cycles_cand", C.c_ulonglong),
-                ("cycles_secondary", C.c_ulonglong), ("cycles_shadow", C.c_ulonglong)]
+                ("cycles_secondary", C.c_ulonglong), ("cycles_shadow", C.c_ulonglong),
+                ("cycles_shadow_directional", C.c_ulonglong)]
 
     def as_dict(self):
         return {k: int(getattr(self, k)) for k, _ in self._fields_}
@@ -413,10 +414,10 @@ class Context:
     def cand_verify(self, frame, rank=0, nranks=1):
         """Host re-derivation of the last render's candidate lists:
         {listed, entries, fp_mismatch, tile_mismatch, global}."""
-        out = (C.c_ulonglong * 5)()
+        out = (C.c_ulonglong * 7)()
         _check(lib().rt_hip_cand_verify(self.h, C.byref(frame), rank, nranks, out), "cand_verify")
-        return dict(zip(("listed", "entries", "fp_mismatch", "tile_mismatch", "global"),
-                        (int(x) for x in out)))
+        return dict(zip(("listed", "entries", "fp_mismatch", "tile_mismatch", "global",
+                         "filter_violation", "filtered"), (int(x) for x in out)))
 
     def set_camera_slack(self, ulps):
         _check(lib().rt_hip_set_camera_slack(self.h, float(ulps)), "camera_slack")

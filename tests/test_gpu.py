@@ -320,6 +320,7 @@ def test_candidate_lists_match_host(gpu, accel, nranks):
         v = ctx.cand_verify(f, rank, nranks)
         assert v["listed"] > 0 and v["entries"] > 0, v
         assert v["fp_mismatch"] == 0 and v["tile_mismatch"] == 0, str(v)
+        assert v["filter_violation"] == 0 and v["filtered"] > 0, str(v)
 
 
 def test_zero_normal_is_an_error(gpu, tmp_path):
