@@ -17,8 +17,13 @@
 #define RT_SPILL_STACK 112
 // reflection terms of a path kept in LDS (deeper ones: KParams::terms)
 #define RT_LDS_TERMS 4
-// occupancy target of the render kernels' launch bounds (waves per SIMD)
-#define RT_MIN_WAVES 4
+// occupancy target of the render kernels' launch bounds (waves per SIMD).
+// The kernels need 123 VGPRs and 9.7 KB of LDS, so they still run 4 waves
+// per SIMD; a target of 3 only changes the scheduler's trade-offs (measured,
+// C5 render kernel: 13.86 ms at 4, 13.70 at 3 and at 2; profiles/r02m_waves/).
+#ifndef RT_MIN_WAVES
+#define RT_MIN_WAVES 3
+#endif
 // traversal policies (one kernel instantiation each, rt_render.hip); the
 // others exist for tests and A/B measurements
 #define RT_POLICY_DEFAULT 0     // staged packet closest hit for coherent queries, per-lane shadows

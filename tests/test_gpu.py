@@ -364,6 +364,20 @@ def test_compat_matches_oracle(gpu, scene_dir, scene, accel):
     assert (st["closest"], st["shadow"]) == (cnt["closest"], cnt["shadow"])
 
 
+def test_compat_large_frame_sampled(gpu):
+    """gpu/rt compatibility mode on the device-built octree at 1280x720
+    (3840x2160 rays) of a 147k-triangle synthetic scene: 96 sampled output
+    pixels (each the downscale of its 9 rays) byte-identical to the oracle."""
+    import oracle as orc
+    s = gpu.Scene.synthetic(4, 4, 9776, seed=0x5EED, width=1280, height=720)
+    img, st = gpu.Context(s, "octree_gpu").render_compat(s.camera)
+    assert st["pixels"] == 9 * 1280 * 720
+    rng = np.random.default_rng(5)
+    pix = np.stack([rng.integers(0, 720, 96), rng.integers(0, 1280, 96)], axis=1)
+    ref, _ = orc.render_gpu(s.ptr, 1280, 720, pixels=pix, threads=8)
+    assert np.array_equal(img[pix[:, 0], pix[:, 1]], ref)
+
+
 def test_rt_gpu_cli_png(gpu, scene_dir, tmp_path):
     """lib/rt_gpu = gpu/rt's command line: same usage error, and the PNG it
     writes decodes to the oracle's gpu-mode image."""
