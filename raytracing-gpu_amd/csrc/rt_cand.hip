@@ -280,30 +280,44 @@ __host__ __device__ inline uint32_t rank_tiles(uint32_t lo, uint32_t hi, uint32_
 // false = none of this rank's tiles (off-frame, or between the rank's tiles
 // of an interleaved split); true whenever unsure.
 RTC_FN bool rank_may_touch(const CandParams& p, const double q[3], double rb) {
-  const double dq[3] = {q[0] - p.pos[0], q[1] - p.pos[1], q[2] - p.pos[2]};
-  const double R = sqrt(dq[0] * dq[0] + dq[1] * dq[1] + dq[2] * dq[2]);
-  if (!(R > 2.0 * rb + 1e-6)) return true;
-  double kmn = 1e300, kmx = -1e300, lmn = 1e300, lmx = -1e300;
+  // in float (the triangles that reach here are a third of the scene): the
+  // corners must lie well in front of the eye (|Y . n| >= |Y| / 20, i.e.
+  // within ~87 degrees of the view axis; anything else is kept), so the
+  // projection's relative rounding stays below 1e-5 and its absolute error
+  // below a pixel -- covered by the 3-pixel margin
+  const float dq0 = (float)(q[0] - p.pos[0]), dq1 = (float)(q[1] - p.pos[1]),
+              dq2 = (float)(q[2] - p.pos[2]);
+  const float rbf = (float)rb;
+  const float R = sqrtf(dq0 * dq0 + dq1 * dq1 + dq2 * dq2);
+  if (!(R > 2.0f * rbf + 1e-6f)) return true;
+  const float n0 = (float)p.n[0], n1 = (float)p.n[1], n2 = (float)p.n[2];
+  const float u0 = (float)p.u[0], u1 = (float)p.u[1], u2 = (float)p.u[2];
+  const float v0 = (float)p.v[0], v1 = (float)p.v[1], v2 = (float)p.v[2];
+  const float pc0 = (float)(p.pos[0] - p.C[0]), pc1 = (float)(p.pos[1] - p.C[1]),
+              pc2 = (float)(p.pos[2] - p.C[2]);
+  const float plane = (float)p.plane, g0 = (float)p.ginv[0], g1 = (float)p.ginv[1],
+              g2 = (float)p.ginv[2];
+  const float ymin = 0.05f * (R + 1.8f * rbf);
+  float kmn = 1e30f, kmx = -1e30f, lmn = 1e30f, lmx = -1e30f;
   int side = 0;
   for (int c = 0; c < 8; c++) {
-    double Y[3];
-    for (int a = 0; a < 3; a++) Y[a] = dq[a] + (((c >> a) & 1) ? rb : -rb);
-    const double yn = Y[0] * p.n[0] + Y[1] * p.n[1] + Y[2] * p.n[2];
-    const int sd = yn > 1e-6 * (R + rb) ? 1 : (yn < -1e-6 * (R + rb) ? -1 : 0);
+    const float Y0 = dq0 + ((c & 1) ? rbf : -rbf), Y1 = dq1 + ((c & 2) ? rbf : -rbf),
+                Y2 = dq2 + ((c & 4) ? rbf : -rbf);
+    const float yn = Y0 * n0 + Y1 * n1 + Y2 * n2;
+    const int sd = yn > ymin ? 1 : (yn < -ymin ? -1 : 0);
     if (sd == 0 || (side != 0 && sd != side)) return true;
     side = sd;
-    const double lam = p.plane / yn;
-    double w[3];
-    for (int a = 0; a < 3; a++) w[a] = p.pos[a] + lam * Y[a] - p.C[a];
-    const double b1 = w[0] * p.u[0] + w[1] * p.u[1] + w[2] * p.u[2];
-    const double b2 = w[0] * p.v[0] + w[1] * p.v[1] + w[2] * p.v[2];
-    const double k = p.ginv[0] * b1 + p.ginv[1] * b2, l = p.ginv[1] * b1 + p.ginv[2] * b2;
-    kmn = fmin(kmn, k);
-    kmx = fmax(kmx, k);
-    lmn = fmin(lmn, l);
-    lmx = fmax(lmx, l);
+    const float lam = plane / yn;
+    const float w0 = pc0 + lam * Y0, w1 = pc1 + lam * Y1, w2 = pc2 + lam * Y2;
+    const float b1 = w0 * u0 + w1 * u1 + w2 * u2, b2 = w0 * v0 + w1 * v1 + w2 * v2;
+    const float k = g0 * b1 + g1 * b2, l = g1 * b1 + g2 * b2;
+    kmn = fminf(kmn, k);
+    kmx = fmaxf(kmx, k);
+    lmn = fminf(lmn, l);
+    lmx = fmaxf(lmx, l);
   }
-  const double m = 2.0 + 1.5 * p.gscale * (p.dline * (1.0 + p.lmax / (R - 2.0 * rb)) + p.dorig);
+  const double m = 3.0 + 1.5 * p.gscale * (p.dline * (1.0 + p.lmax / ((double)R - 2.0 * rb)) + p.dorig) +
+                   1e-5 * (fabs((double)kmn) + fabs((double)kmx) + fabs((double)lmn) + fabs((double)lmx));
   kmn -= m;
   kmx += m;
   lmn -= m;
