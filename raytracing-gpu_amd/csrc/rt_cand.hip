@@ -128,10 +128,13 @@ RTC_FN int classify(const CandParams& p, const float* r, const float* leafbox, F
   auto alb = [&](double c) { return fmax(kAMin, kDMin * nl * c - e_a); };
   double P[3][3];
   // T_D(c) corners; returns how far they reach beyond the triangle
+  // (two divisions instead of five: the products differ from the quotients
+  // by an ulp or two, far inside the bound's own slack -- its constants are
+  // rounded up by 1.3 %, tools/mt_bound.py)
   auto expand = [&](double c, double& rho_o, double& a_o) {
-    const double a = alb(c), rho = e_a / a;
-    const double du = e_sh / (a * (1.0 - rho)), dv = e_dq / (a * (1.0 - rho));
-    const double dw = (4.0 * kEps + (e_sh + e_dq) / a + rho) / (1.0 - rho);
+    const double a = alb(c), ia = 1.0 / a, rho = e_a * ia, i1r = 1.0 / (1.0 - rho);
+    const double du = e_sh * ia * i1r, dv = e_dq * ia * i1r;
+    const double dw = (4.0 * kEps + (e_sh + e_dq) * ia + rho) * i1r;
     for (int k = 0; k < 3; k++) {
       P[0][k] = v0[k] - du * e1[k] - dv * e2[k];
       P[1][k] = v0[k] + (1.0 + dw + dv) * e1[k] - dv * e2[k];
