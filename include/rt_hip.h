@@ -192,6 +192,10 @@ int rt_cand_survey(const rt_scene *scene, float eps_ulps, double bound_scale, in
 int rt_hip_cand_verify(rt_hip_ctx *ctx, const rt_frame *frame, int rank, int nranks,
                        unsigned long long out[7]);
 
+/* Diagnostic: candidate-list entries of each of the first n rank-local tiles
+ * of the last render (n <= that rank's tile count). */
+int rt_hip_cand_tile_entries(rt_hip_ctx *ctx, unsigned int *out, size_t n);
+
 /* d_gathered = nranks consecutive tile buffers (rank-major, as an RCCL gather
  * delivers them); writes the PPM-order image (W*H*3 floats) to d_rgb. */
 int rt_hip_assemble(rt_hip_ctx *ctx, const rt_frame *frame, const float *d_gathered, int nranks,

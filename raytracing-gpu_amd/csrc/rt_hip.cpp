@@ -450,6 +450,18 @@ extern "C" int rt_hip_cand_verify(rt_hip_ctx* c, const rt_frame* f, int rank, in
   return RT_OK;
 }
 
+extern "C" int rt_hip_cand_tile_entries(rt_hip_ctx* c, unsigned int* out, size_t n) {
+  if (!c || !out) return rt_set_error(RT_EINVAL, "null argument");
+  if (!c->d_cand_start) return rt_set_error(RT_EINVAL, "no candidate lists (render a frame first)");
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = c->last_stream ? c->last_stream : c->stream;
+  HIP_TRY(hipStreamSynchronize(s));
+  std::vector<uint32_t> st(n + 1);
+  HIP_TRY(hipMemcpy(st.data(), c->d_cand_start, (n + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  for (size_t t = 0; t < n; t++) out[t] = st[t + 1] - st[t];
+  return RT_OK;
+}
+
 extern "C" int rt_hip_set_timing(rt_hip_ctx* c, int enable) {
   if (!c) return rt_set_error(RT_EINVAL, "null context");
   HIP_TRY(hipSetDevice(c->device));

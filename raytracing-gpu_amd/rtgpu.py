@@ -145,6 +145,7 @@ _PROTOS = [
     ("rt_hip_set_cull_slack", C.c_int, [C.c_void_p, C.c_float]),
     ("rt_hip_set_camera_slack", C.c_int, [C.c_void_p, C.c_float]),
     ("rt_hip_cand_verify", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
+    ("rt_hip_cand_tile_entries", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
     ("rt_hip_set_exact_camera", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_set_policy", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_tile_cycles", C.c_int, [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_size_t]),
@@ -418,6 +419,13 @@ class Context:
         _check(lib().rt_hip_cand_verify(self.h, C.byref(frame), rank, nranks, out), "cand_verify")
         return dict(zip(("listed", "entries", "fp_mismatch", "tile_mismatch", "global",
                          "filter_violation", "filtered"), (int(x) for x in out)))
+
+    def cand_tile_entries(self, ntiles):
+        """Candidate-list entries per rank-local tile of the last render."""
+        out = np.zeros(ntiles, np.uint32)
+        _check(lib().rt_hip_cand_tile_entries(self.h, out.ctypes.data_as(C.c_void_p), ntiles),
+               "cand_tile_entries")
+        return out
 
     def set_camera_slack(self, ulps):
         _check(lib().rt_hip_set_camera_slack(self.h, float(ulps)), "camera_slack")

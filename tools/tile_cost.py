@@ -46,6 +46,10 @@ def main():
     tx, ty = (a.W + 7) // 8, (a.H + 7) // 8
     items = ctx.tile_cycles(4 * tx * ty).astype(np.float64)  # item 4t + s = (tile t, sample s)
     c = items.reshape(-1, 4).sum(axis=1)
+    try:
+        ent = ctx.cand_tile_entries(tx * ty).astype(np.float64)
+    except rtgpu.RtError:
+        ent = None
     order = np.argsort(-c)
     tot = c.sum()
     res = {
@@ -58,6 +62,12 @@ def main():
         "max_item": items.max(),
         "bound_tail_over_balanced": items.max() / (tot / 4096.0),
         "worst_tiles_rc": [[int(i // tx), int(i % tx)] for i in order[:10]],
+        "worst_items_cycles": [float(x) for x in np.sort(items)[::-1][:10]],
+        # candidate entries of the worst tiles vs all tiles, and the correlation
+        # of a tile's cost with its entry count
+        "worst_tiles_entries": [float(ent[i]) for i in order[:10]] if ent is not None else None,
+        "entries_mean_max": [float(ent.mean()), float(ent.max())] if ent is not None else None,
+        "corr_cost_entries": float(np.corrcoef(c, ent)[0, 1]) if ent is not None else None,
         "stats": st,
     }
     print(json.dumps(res, default=float))
