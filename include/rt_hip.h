@@ -160,6 +160,10 @@ int rt_hip_frame_times(rt_hip_ctx *ctx, int n, float *lists_ms, float *render_ms
  * of the rank): the load-balance picture of a frame. */
 int rt_hip_tile_cycles(rt_hip_ctx *ctx, unsigned long long *out, size_t n);
 int rt_hip_set_count_work(rt_hip_ctx *ctx, int enable);
+/* The same items' phase clocks: phase 0 = the item's total (= rt_hip_tile_cycles),
+ * 1 camera walk, 2 camera candidate tests, 3 secondary walks, 4 shadow
+ * queries, 5 directional-light shadow queries. */
+int rt_hip_tile_phase_cycles(rt_hip_ctx *ctx, int phase, unsigned long long *out, size_t n);
 /* Exact camera rays (default 1): per-frame candidate lists of the triangles
  * whose float Moller-Trumbore error region the octree slack does not cover
  * (csrc/rt_cand.hip).  0 = octree walk only (A/B timing; cpu/rt parity is

@@ -500,6 +500,19 @@ extern "C" int rt_hip_tile_cycles(rt_hip_ctx* c, unsigned long long* out, size_t
   return RT_OK;
 }
 
+extern "C" int rt_hip_tile_phase_cycles(rt_hip_ctx* c, int phase, unsigned long long* out, size_t n) {
+  if (!c || !out || phase < 0 || phase > 5) return rt_set_error(RT_EINVAL, "bad argument");
+  if (!c->d_tile_cycles || n > c->tile_cycles_n)
+    return rt_set_error(RT_EINVAL, "%zu item clocks asked, %zu recorded (rt_hip_set_count_work)", n,
+                        c->tile_cycles_n);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = c->last_stream ? c->last_stream : c->stream;
+  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(hipMemcpy(out, c->d_tile_cycles + (size_t)phase * c->tile_cycles_n, n * sizeof *out,
+                    hipMemcpyDeviceToHost));
+  return RT_OK;
+}
+
 extern "C" int rt_hip_set_count_work(rt_hip_ctx* c, int enable) {
   if (!c) return rt_set_error(RT_EINVAL, "null context");
   c->count_work = enable ? 1 : 0;
@@ -793,7 +806,7 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
       (void)hipFree(c->d_tile_cycles);
       c->d_tile_cycles = nullptr;
       c->tile_cycles_cap = 0;
-      HIP_TRY(hipMalloc((void**)&c->d_tile_cycles, items * sizeof(unsigned long long)));
+      HIP_TRY(hipMalloc((void**)&c->d_tile_cycles, 6 * items * sizeof(unsigned long long)));
       c->tile_cycles_cap = items;
     }
     c->tile_cycles_n = items;

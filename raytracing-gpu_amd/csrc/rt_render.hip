@@ -748,7 +748,7 @@ __device__ bool staged_any(const KParams& p, const Ray& r, bool act, WaveCtx& w,
 // shadow queries walk per lane, except directional-light shadows (parallel
 // rays, cpu/light.c:53) under RT_POLICY_DIR_STAGED.
 static constexpr int kPacketMin = 8;
-static constexpr int kPacketMaxDepth = 1;
+static constexpr int kPacketMaxDepth = 1;  // 0 measured: the same (C5 13.73 vs 13.73 ms, r02n)
 
 // Closest-hit query; converged call, act = lane has a query.
 template <int ACCEL, bool COUNT, int POL>
@@ -1092,6 +1092,7 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES) void render_kernel(KParams p) {
     }
     const uint32_t u = 4u * (8u * (q >> 2) + x) + (q & 3u);  // item index 4t + s
     const unsigned long long c0 = COUNT ? __builtin_readcyclecounter() : 0ull;
+    const uint32_t ph0[5] = {wc.cy_cam, wc.cy_cand, wc.cy_sec, wc.cy_shadow, wc.cy_shadow_dir};
     const uint32_t t = u >> 2;
     const int smp = (int)(u & 3u);
     const uint32_t g = t * (uint32_t)p.nranks + (uint32_t)p.rank;  // global tile index
@@ -1114,7 +1115,16 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES) void render_kernel(KParams p) {
     so[0] = sc.r;
     so[64] = sc.g;
     so[128] = sc.b;
-    if (COUNT && p.tile_cycles && lane == 0) p.tile_cycles[u] = __builtin_readcyclecounter() - c0;
+    if (COUNT && p.tile_cycles && lane == 0) {
+      // [0] the item's clocks, [1..5] its phase clocks (camera walk, camera
+      // candidates, secondary walks, shadows, directional shadows), planes
+      // of 4 * ntiles_local items
+      const size_t items = 4 * (size_t)p.ntiles_local;
+      const uint32_t ph1[5] = {wc.cy_cam, wc.cy_cand, wc.cy_sec, wc.cy_shadow, wc.cy_shadow_dir};
+      p.tile_cycles[u] = __builtin_readcyclecounter() - c0;
+#pragma unroll
+      for (int k = 0; k < 5; k++) p.tile_cycles[u + (size_t)(k + 1) * items] = ph1[k] - ph0[k];
+    }
   }
   // the counters are wave totals already: one atomic per counter per wave
   uint32_t v[RT_NSTATS] = {wc.closest, wc.shadow,   wc.pixels,      wc.nodes,

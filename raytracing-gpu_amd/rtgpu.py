@@ -149,6 +149,8 @@ _PROTOS = [
     ("rt_hip_set_exact_camera", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_set_policy", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_tile_cycles", C.c_int, [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_size_t]),
+    ("rt_hip_tile_phase_cycles", C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_ulonglong),
+                                           C.c_size_t]),
     ("rt_hip_set_timing", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_frame_times", C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_float),
                                      C.POINTER(C.c_float)]),
@@ -399,6 +401,14 @@ class Context:
         out = np.zeros(n, dtype=np.uint64)
         _check(lib().rt_hip_tile_cycles(self.h, out.ctypes.data_as(C.POINTER(C.c_ulonglong)), n),
                "tile_cycles")
+        return out
+
+    def tile_phase_cycles(self, phase, n):
+        """Per-item phase clocks (rt_hip_tile_phase_cycles; numpy uint64)."""
+        out = np.zeros(n, dtype=np.uint64)
+        _check(lib().rt_hip_tile_phase_cycles(self.h, phase,
+                                              out.ctypes.data_as(C.POINTER(C.c_ulonglong)), n),
+               "tile_phase_cycles")
         return out
 
     def set_policy(self, policy):

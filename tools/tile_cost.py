@@ -46,6 +46,9 @@ def main():
     tx, ty = (a.W + 7) // 8, (a.H + 7) // 8
     items = ctx.tile_cycles(4 * tx * ty).astype(np.float64)  # item 4t + s = (tile t, sample s)
     c = items.reshape(-1, 4).sum(axis=1)
+    ph = {name: ctx.tile_phase_cycles(k, 4 * tx * ty).astype(np.float64)
+          for k, name in enumerate(("total", "camera_walk", "candidates", "secondary", "shadow",
+                                    "shadow_dir")) if k}
     try:
         ent = ctx.cand_tile_entries(tx * ty).astype(np.float64)
     except rtgpu.RtError:
@@ -63,6 +66,9 @@ def main():
         "bound_tail_over_balanced": items.max() / (tot / 4096.0),
         "worst_tiles_rc": [[int(i // tx), int(i % tx)] for i in order[:10]],
         "worst_items_cycles": [float(x) for x in np.sort(items)[::-1][:10]],
+        # phase clocks of the 10 most expensive items and the mean item
+        "worst_items_phases": [{k: float(ph[k][i]) for k in ph} for i in np.argsort(-items)[:10]],
+        "mean_item_phases": {k: float(ph[k].mean()) for k in ph},
         # candidate entries of the worst tiles vs all tiles, and the correlation
         # of a tile's cost with its entry count
         "worst_tiles_entries": [float(ent[i]) for i in order[:10]] if ent is not None else None,
