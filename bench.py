@@ -408,6 +408,8 @@ def main():
                     "closest_tris_per_query": round(cl_tris / wcl, 3) if wcl else None,
                     "shadow_nodes_per_query": round(sh_nodes / wsh, 3) if wsh else None,
                     "shadow_tris_per_query": round(sh_tris / wsh, 3) if wsh else None,
+                    # per-lane stack pushes that went past the LDS entries to HBM
+                    "stack_spill_pushes": int(work["stack_spills"]),
                     "bytes_per_launch": int((wq * RAY_BYTES + (cl_nodes + sh_nodes) * NODE_BYTES +
                                              (cl_tris + sh_tris) * TRI_BYTES +
                                              whits * NORMAL_BYTES + pixels * PIXEL_BYTES) / world),

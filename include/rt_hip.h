@@ -74,6 +74,7 @@ typedef struct rt_stats {
    * shadow queries (summed over waves) */
   unsigned long long cycles_camera, cycles_cand, cycles_secondary, cycles_shadow;
   unsigned long long cycles_shadow_directional;  /* the directional-light share of cycles_shadow */
+  unsigned long long stack_spills;  /* per-lane stack pushes beyond the LDS entries (instrumented pass) */
 } rt_stats;
 
 /* Sizes of the device-side scene image, for the roofline accounting. */

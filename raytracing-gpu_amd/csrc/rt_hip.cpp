@@ -865,6 +865,7 @@ extern "C" int rt_hip_stats(rt_hip_ctx* c, rt_stats* out) {
   out->cycles_secondary = h[14];
   out->cycles_shadow = h[15];
   out->cycles_shadow_directional = h[16];
+  out->stack_spills = h[17];
   out->cand_prims = c->cand_prims;
   out->cand_entries = c->cand_entries;
   out->cand_global = c->cand_global;

@@ -12,7 +12,7 @@
 #define RT_MAT_FLOATS_D 12
 #define RT_LIGHT_FLOATS_D 8
 #define RT_MAX_DEPTH 32
-#define RT_NSTATS 17
+#define RT_NSTATS 18
 // per-lane global overflow area of the traversal stack (entries beyond LDS)
 #define RT_SPILL_STACK 112
 // reflection terms of a path kept in LDS (deeper ones: KParams::terms)
@@ -43,6 +43,7 @@ struct WorkCount {
   // queries (wall clock of the wave, so shares of its time)
   uint32_t cy_cam, cy_cand, cy_sec, cy_shadow;
   uint32_t cy_shadow_dir;  // the directional-light part of cy_shadow
+  uint32_t stack_spills;   // per-lane stack pushes past the LDS entries (COUNT pass)
 };
 
 struct KParams {

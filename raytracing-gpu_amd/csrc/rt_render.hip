@@ -162,7 +162,9 @@ static constexpr int kSpillStack = RT_SPILL_STACK;
 struct Stack {
   uint32_t* idx;  // LDS, kLdsStack x 64
   float* tt;      // LDS, kLdsStack x 64
-  uint2* spill;   // this lane's kSpillStack entries
+  uint2* spill;   // this lane's first spill entry; entry k at spill[k * stride]
+  uint32_t stride;  // lanes of the launch: spill entries are [entry][lane], so the
+                    // lanes of a wave at the same depth touch adjacent words
   int lane;
   int sp;
 };
@@ -172,6 +174,7 @@ struct Stack {
 struct LaneCount {
   uint32_t nodes, tris, overflow;
   uint32_t lnodes, ltris;  // this lane's own visits / tests (COUNT pass)
+  uint32_t spills;         // pushes beyond the LDS part of the stack (COUNT pass)
 };
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
@@ -214,6 +217,7 @@ __device__ __forceinline__ void absorb(WorkCount& wc, const LaneCount& lc, bool 
     }
   }
   wc.overflow += wave_sum(lc.overflow);
+  if (COUNT) wc.stack_spills += wave_sum(lc.spills);
 }
 
 __device__ __forceinline__ void push(Stack& s, uint32_t i, float t, LaneCount& wc) {
@@ -221,7 +225,8 @@ __device__ __forceinline__ void push(Stack& s, uint32_t i, float t, LaneCount& w
     s.idx[s.sp * 64 + s.lane] = i;
     s.tt[s.sp * 64 + s.lane] = t;
   } else if (s.sp < kLdsStack + kSpillStack) {
-    s.spill[s.sp - kLdsStack] = make_uint2(i, __float_as_uint(t));
+    s.spill[(size_t)(s.sp - kLdsStack) * s.stride] = make_uint2(i, __float_as_uint(t));
+    wc.spills++;
   } else {
     wc.overflow++;  // reported as RT_EDEPTH by rt_hip_stats: never silent
     return;
@@ -235,7 +240,7 @@ __device__ __forceinline__ void pop(Stack& s, uint32_t& i, float& t) {
     i = s.idx[s.sp * 64 + s.lane];
     t = s.tt[s.sp * 64 + s.lane];
   } else {
-    uint2 e = s.spill[s.sp - kLdsStack];
+    uint2 e = s.spill[(size_t)(s.sp - kLdsStack) * s.stride];
     i = e.x;
     t = __uint_as_float(e.y);
   }
@@ -764,7 +769,7 @@ __device__ __forceinline__ void closest_q(const KParams& p, const Ray& r, bool a
   if (staged) {
     staged_closest<COUNT>(p, r, act, b, w, wc);
   } else {
-    LaneCount lc = {0, 0, 0, 0, 0};
+    LaneCount lc = {0, 0, 0, 0, 0, 0};
     if (act) oct_closest<COUNT>(p, r, b, s, lc);
     absorb<COUNT>(wc, lc, false);
   }
@@ -782,7 +787,7 @@ __device__ __forceinline__ bool shadow_q(const KParams& p, f3 o, f3 d, uint32_t 
   bool staged = POL == RT_POLICY_STAGED ||
                 (POL == RT_POLICY_DIR_STAGED && type == 1 && __popcll(am) >= kPacketMin);
   if (staged) return staged_any<COUNT>(p, r, act, w, wc);
-  LaneCount lc = {0, 0, 0, 0, 0};
+  LaneCount lc = {0, 0, 0, 0, 0, 0};
   bool hit = act && oct_any<COUNT>(p, r, s, lc);
   absorb<COUNT>(wc, lc, true);
   return hit;
@@ -1050,7 +1055,8 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES) void render_kernel(KParams p) {
   Stack stk;
   stk.idx = (uint32_t*)s_stack;
   stk.tt = (float*)s_stack + kLdsStack * 64;
-  stk.spill = p.spill + gl * kSpillStack;
+  stk.spill = p.spill + gl;
+  stk.stride = gridDim.x * 64u;
   stk.lane = lane;
   stk.sp = 0;
   WaveCtx w;
@@ -1131,7 +1137,7 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES) void render_kernel(KParams p) {
                            wc.tris,    wc.overflow, wc.zero_normal, wc.hits,
                            wc.cl_nodes, wc.cl_tris, wc.sh_nodes,   wc.sh_tris,
                            wc.cy_cam,   wc.cy_cand, wc.cy_sec,     wc.cy_shadow,
-                           wc.cy_shadow_dir};
+                           wc.cy_shadow_dir, wc.stack_spills};
 #pragma unroll
   for (int k = 0; k < RT_NSTATS; k++)
     if (lane == 0 && v[k]) atomicAdd(p.stats + k, (unsigned long long)v[k]);
@@ -1264,7 +1270,8 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES) void compat_kernel(KParams p) {
   Stack stk;
   stk.idx = (uint32_t*)s_stack;
   stk.tt = (float*)s_stack + kLdsStack * 64;
-  stk.spill = p.spill + gl * kSpillStack;
+  stk.spill = p.spill + gl;
+  stk.stride = gridDim.x * 64u;
   stk.lane = lane;
   stk.sp = 0;
   WaveCtx w;

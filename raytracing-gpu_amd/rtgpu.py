@@ -92,7 +92,7 @@ class Stats(C.Structure):
                 ("shadow_node_lanes", C.c_ulonglong), ("shadow_tri_lanes", C.c_ulonglong),
                 ("cycles_camera", C.c_ulonglong), ("cycles_cand", C.c_ulonglong),
                 ("cycles_secondary", C.c_ulonglong), ("cycles_shadow", C.c_ulonglong),
-                ("cycles_shadow_directional", C.c_ulonglong)]
+                ("cycles_shadow_directional", C.c_ulonglong), ("stack_spills", C.c_ulonglong)]
 
     def as_dict(self):
         return {k: int(getattr(self, k)) for k, _ in self._fields_}
