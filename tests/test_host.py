@@ -96,6 +96,30 @@ def test_parse_errors(built, tmp_path):
     assert e.value.code == -2
 
 
+def test_parse_error_texts_and_strict_vertex_count(built, tmp_path):
+    """Error texts as the reference prints them (cpu/parser.c:111 "Error during
+    the parsing %s", cpu/parse_obj.c:80 "Error during parsing %s"), and the
+    deliberate strictness on objects whose v/vn lines do not match the
+    declared count (the reference's behaviour there is undefined: it pops a
+    NULL stack head, cpu/stack.c:36-39, or leaves triangles unallocated,
+    cpu/parse_obj.c:83-89) -- rejected with a parse error, never rendered."""
+    import rtgpu
+    cam = "camera 8 8 0 0 -4 1 0 0 0 -1 0 70\n"
+    cases = [
+        (cam + "bogus 1 2 3\n", "Error during the parsing bogus"),
+        (cam + "object 3\nKa 1 1 1\nfoo 1\n", "Error during parsing foo"),
+        (cam + "object 6\nv 0 0 0\nv 1 0 0\nv 0 1 0\nvn 0 0 1\nvn 0 0 1\nvn 0 0 1\n",
+         "object declares 6 vertices"),
+        (cam + "object 3\nv 0 0 0\nv 1 0 0\nv 0 1 0\nvn 0 0 1\n", "object declares 3 vertices"),
+    ]
+    for k, (text, msg) in enumerate(cases):
+        p = tmp_path / f"bad{k}.svati"
+        p.write_text(text)
+        with pytest.raises(rtgpu.RtError) as e:
+            rtgpu.Scene.load_svati(str(p))
+        assert e.value.code == -3 and msg in str(e.value), (k, str(e.value))
+
+
 @pytest.mark.parametrize("case", CASES, ids=[case_id(c) for c in CASES])
 def test_ppm_writer_byte_identical(case, built, tmp_path):
     """cpu/printer.c:3-18 + cpu/raytracer.c:128-134 from the golden framebuffer."""
