@@ -206,6 +206,7 @@ def main():
     wl = dict(WORKLOADS[args.workload])
     if args.accel:
         wl["accel"] = args.accel
+        wl["desc"] = wl["desc"] + f" [accel overridden: {args.accel}]"
     W, H = wl["W"], wl["H"]
 
     with tempfile.TemporaryDirectory() as td:
@@ -307,7 +308,7 @@ def main():
     traffic = traffic_hi = None
     traffic_src = None
     if world == 1 and args.traffic_json is None and args.cull_slack is None and \
-            args.camera_slack is None and args.policy is None:
+            args.camera_slack is None and args.policy is None and args.accel is None:
         # default run: the newest committed rocprofv3 PMC pass of this
         # workload (profiles/r*_<workload>/, tools/gpu_profile.sh); a PMC
         # pass cannot run inside the bench, so the line says where it came from
