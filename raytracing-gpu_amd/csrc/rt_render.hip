@@ -594,6 +594,108 @@ __device__ bool flat_any_w(const KParams& p, const Ray& r, bool act, WaveCtx& w,
   return hit;
 }
 
+// Brute force, TRIANGLE-parallel: for a wave with few active lanes (deep
+// reflection bounces, shadow rays of the lanes that hit, sky pixels), the
+// lanes take turns: the active lane's ray is broadcast and the 64 lanes test
+// 64 different triangles at a time, then the lexicographic (new_dist, prim)
+// minimum is reduced across the wave -- the same decisions in another order
+// (the key makes the winner order-independent).  Ray-parallel streaming pays
+// the whole triangle list per wave however few lanes still query.
+__device__ __forceinline__ Ray ray_of_lane(const Ray& r, int l) {
+  Ray q;
+  q.o = f3{__shfl(r.o.x, l), __shfl(r.o.y, l), __shfl(r.o.z, l)};
+  q.d = f3{__shfl(r.d.x, l), __shfl(r.d.y, l), __shfl(r.d.z, l)};
+  q.dlen = __shfl(r.dlen, l);
+  q.eps = 0.0f;
+  q.oh = q.o;
+  q.ol = q.o;
+  return q;
+}
+
+template <bool COUNT>
+__device__ void flat_closest_tp(const KParams& p, const Ray& r, bool act, Best& b, WorkCount& wc) {
+  const uint32_t n = p.nrec;
+  const int lane = (int)(threadIdx.x & 63);
+  uint64_t am = __ballot(act);
+  if (COUNT) {
+    wc.tris += n * (uint32_t)__popcll(am);
+    wc.cl_tris += n * (uint32_t)__popcll(am);
+  }
+  while (am) {
+    const int l = __ffsll((unsigned long long)am) - 1;
+    am &= am - 1;
+    const Ray q = ray_of_lane(r, l);
+    Best mb;
+    mb.dist = __builtin_inff();
+    mb.t_cut = __builtin_inff();
+    mb.prim = 0xffffffffu;
+    mb.obj = 0;
+    mb.u = mb.v = 0.0f;
+    mb.t = 0.0f;
+    for (uint32_t base = 0; base < n; base += 64) {
+      const uint32_t i = base + (uint32_t)lane;
+      if (i < n) {
+        const float4* t = p.tri + 3 * (size_t)i;
+        consider(q, t[0], t[1], t[2], mb);
+      }
+    }
+    // wave minimum of (dist, prim); the winner's obj, u, v, t travel with it
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const float od = __shfl_xor(mb.dist, off);
+      const uint32_t op = __shfl_xor(mb.prim, off), oo = __shfl_xor(mb.obj, off);
+      const float ou = __shfl_xor(mb.u, off), ov = __shfl_xor(mb.v, off), ot = __shfl_xor(mb.t, off);
+      if (od < mb.dist || (od == mb.dist && op < mb.prim)) {
+        mb.dist = od;
+        mb.prim = op;
+        mb.obj = oo;
+        mb.u = ou;
+        mb.v = ov;
+        mb.t = ot;
+      }
+    }
+    if (lane == l) {
+      b.dist = mb.dist;
+      b.prim = mb.prim;
+      b.obj = mb.obj;
+      b.u = mb.u;
+      b.v = mb.v;
+      b.t = mb.t;
+    }
+  }
+}
+
+template <bool COUNT>
+__device__ bool flat_any_tp(const KParams& p, const Ray& r, bool act, WorkCount& wc) {
+  const uint32_t n = p.nrec;
+  const int lane = (int)(threadIdx.x & 63);
+  uint64_t am = __ballot(act);
+  bool res = false;
+  while (am) {
+    const int l = __ffsll((unsigned long long)am) - 1;
+    am &= am - 1;
+    const Ray q = ray_of_lane(r, l);
+    bool hit = false;
+    uint32_t base = 0;
+    for (; base < n && !hit; base += 64) {  // hit is wave-uniform (ballot)
+      const uint32_t i = base + (uint32_t)lane;
+      bool h = false;
+      if (i < n) {
+        const float4* t = p.tri + 3 * (size_t)i;
+        h = any_hit_rec(q, t[0], t[1], t[2]);
+      }
+      hit = __ballot(h) != 0;
+    }
+    if (COUNT) {
+      const uint32_t tested = base < n ? base : n;
+      wc.tris += tested;
+      wc.sh_tris += tested;
+    }
+    if (lane == l) res = hit;
+  }
+  return res;
+}
+
 // Interior node whose child boxes are staged: test them, push the ones any
 // lane wants (with the mask of the lanes that want each) far-to-near in
 // octant order, so the nearest child ends on top of the stack.
@@ -755,12 +857,27 @@ __device__ bool staged_any(const KParams& p, const Ray& r, bool act, WaveCtx& w,
 static constexpr int kPacketMin = 8;
 static constexpr int kPacketMaxDepth = 1;  // 0 measured: the same (C5 13.73 vs 13.73 ms, r02n)
 
+// Brute force: triangle-parallel when the list is long enough to fill the
+// lanes and at most kTpMaxLanes lanes query (ray-parallel streaming costs the
+// same list per wave whatever the active count; triangle-parallel costs it
+// once per active lane, spread over 64 lanes).  Measured on C2 (spheres,
+// 4,812 triangles, 1080p, flat): never 262 ms, <= 32 lanes 160, <= 48 160,
+// <= 56 159, always 250; shadows always triangle-parallel 170
+// (profiles/r02q_flat_tp/).
+static constexpr int kTpMaxLanes = 48;
+__device__ __forceinline__ bool use_tp(const KParams& p, bool act) {
+  return p.nrec >= 256u && __popcll(__ballot(act)) <= kTpMaxLanes;
+}
+
 // Closest-hit query; converged call, act = lane has a query.
 template <int ACCEL, bool COUNT, int POL>
 __device__ __forceinline__ void closest_q(const KParams& p, const Ray& r, bool act, int depth, Best& b,
                                           Stack& s, WaveCtx& w, WorkCount& wc) {
   if (ACCEL == RT_ACCEL_FLAT_D) {
-    flat_closest_w<COUNT>(p, r, act, b, w, wc);
+    if (use_tp(p, act))
+      flat_closest_tp<COUNT>(p, r, act, b, wc);
+    else
+      flat_closest_w<COUNT>(p, r, act, b, w, wc);
     return;
   }
   bool staged = POL == RT_POLICY_STAGED ||
@@ -783,7 +900,8 @@ __device__ __forceinline__ bool shadow_q(const KParams& p, f3 o, f3 d, uint32_t 
   uint64_t am = __ballot(act);
   wc.shadow += (uint32_t)__popcll(am);
   Ray r = make_ray(p, o, d, p.eps_rel);
-  if (ACCEL == RT_ACCEL_FLAT_D) return flat_any_w<COUNT>(p, r, act, w, wc);
+  if (ACCEL == RT_ACCEL_FLAT_D)
+    return use_tp(p, act) ? flat_any_tp<COUNT>(p, r, act, wc) : flat_any_w<COUNT>(p, r, act, w, wc);
   bool staged = POL == RT_POLICY_STAGED ||
                 (POL == RT_POLICY_DIR_STAGED && type == 1 && __popcll(am) >= kPacketMin);
   if (staged) return staged_any<COUNT>(p, r, act, w, wc);
