@@ -13,6 +13,7 @@ import ctypes as C
 import json
 import os
 import sys
+import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "raytracing-gpu_amd"))
@@ -38,15 +39,17 @@ def main():
             ctx.render(f, rank, n, d.value)  # warm-up
             ctx.stats()
             ctx.set_timing(True)
+            t0 = time.perf_counter()
             for _ in range(a.steps):
                 ctx.render(f, rank, n, d.value)
             ft = ctx.frame_times(a.steps)
+            wall = (time.perf_counter() - t0) * 1e3 / a.steps
             st = ctx.stats()
             ctx.set_timing(False)
             lists = sum(x for x, _ in ft) / len(ft)
             kern = sum(y for _, y in ft) / len(ft)
             row = {"nranks": n, "rank": rank, "lists_ms": round(lists, 3), "render_ms": round(kern, 3),
-                   "frame_ms": round(lists + kern, 3), "cand_entries": st["cand_entries"],
+                   "frame_ms": round(lists + kern, 3), "wall_ms_per_frame": round(wall, 3), "cand_entries": st["cand_entries"],
                    "queries": st["closest"] + st["shadow"]}
             print(json.dumps(row), flush=True)
             res.append(row)
