@@ -43,6 +43,10 @@ TRI_BYTES = 48         # triangle record (host/rt_internal.h)
 RAY_BYTES = 24         # origin + direction of a query
 NORMAL_BYTES = 36      # 3 vertex normals of a closest-hit winner
 PIXEL_BYTES = 12       # f32 RGB written per pixel
+HIT_RECORD_BYTES = 36  # hit record (P, N, coef, object: 2 float4) + its path link
+MATERIAL_BYTES = 48    # material of the hit object
+TERM_BYTES = 16        # a record's reflection term (float4)
+NODE_MU_BYTES = 8      # a node's shadow slack multipliers (csrc/rt_shadow.hip)
 N_SIMD = 1024          # 256 CUs x 4 SIMDs (MI355X_MICROARCH.md)
 N_XCD = 8
 
@@ -193,7 +197,7 @@ def main():
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary (tools/pmc_traffic.py) to report as roofline.traffic")
     ap.add_argument("--valu-json", default=None,
-                    help="PMC summary (tools/pmc_pass.sh, SQ VALU counters) to report as valu")
+                    help="PMC summary (tools/gpu_profile.sh pmc_sq.json, SQ counters) to report as sq")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -237,8 +241,14 @@ def main():
 
     # instrumented pass (untimed): algorithmic work per frame for the roofline
     ctx.set_count_work(True)
-    ctx.render(frame, rank, world, tiles.data_ptr(), sh)
-    work = ctx.stats()
+    for attempt in range(2):
+        ctx.render(frame, rank, world, tiles.data_ptr(), sh)
+        try:
+            work = ctx.stats()
+            break
+        except rtgpu.RtError as e:  # RT_EHITBUF: the buffer grew to the frame's need
+            if e.code != -10 or attempt:
+                raise
     ctx.set_count_work(False)
 
     def step():
@@ -253,19 +263,27 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    st = ctx.stats()
-    assert st["depth_overflow"] == 0
+    try:
+        st = ctx.stats()
+    except rtgpu.RtError as e:  # the first frame sized the hit-record buffer: once more
+        if e.code != -10:
+            raise
+        step()
+        torch.cuda.synchronize()
+        st = ctx.stats()
+    assert st["depth_overflow"] == 0 and st["shadow_unproven"] == 0
     counts = torch.tensor([st["closest"], st["shadow"], st["hits"], st["pixels"],
                            work["node_visits"], work["tri_tests"], work["hits"],
                            work["closest"] + work["shadow"],
                            work["closest_node_lanes"], work["closest_tri_lanes"],
                            work["shadow_node_lanes"], work["shadow_tri_lanes"],
-                           work["closest"], work["shadow"], st["cand_entries"]],
+                           work["closest"], work["shadow"], st["cand_entries"],
+                           work["shadow_node_visits"], work["shadow_tri_tests"]],
                           dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(counts)
     (closest, shadow, hits, pixels, nodes, tris, whits, wq, cl_nodes, cl_tris, sh_nodes, sh_tris,
-     wcl, wsh, cand_entries) = [float(x) for x in counts.tolist()]
+     wcl, wsh, cand_entries, sh_wnodes, sh_wtris) = [float(x) for x in counts.tolist()]
 
     # HIP events around the candidate lists and the render kernel of every
     # timed step, on the stream they run on (rt_hip_set_timing)
@@ -281,71 +299,108 @@ def main():
         dist.barrier()
     el = time.perf_counter() - t0
     ft = ctx.frame_times(min(args.steps, 1024))
+    kt = ctx.kernel_times(min(args.steps, 1024))
     ctx.set_timing(False)
+    trace_ms = sum(a for a, _, _ in kt) / len(kt)
+    shade_ms = sum(b for _, b, _ in kt) / len(kt)
+    fold_ms = sum(c for _, _, c in kt) / len(kt)
     lists_ms = sum(a for a, _ in ft) / len(ft)
     kern_ms = sum(b for _, b in ft) / len(ft)
-    tt = torch.tensor([el, kern_ms, lists_ms], dtype=torch.float64, device=dev)
+    tt = torch.tensor([el, kern_ms, lists_ms, trace_ms, shade_ms, fold_ms], dtype=torch.float64,
+                      device=dev)
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    el, kern_ms, lists_ms = tt.tolist()
+    el, kern_ms, lists_ms, trace_ms, shade_ms, fold_ms = tt.tolist()
 
     queries = closest + shadow
-    cyc = [float(work[k]) for k in ("cycles_camera", "cycles_cand", "cycles_secondary",
-                                    "cycles_shadow")]
+    cyc = [float(work[k]) for k in ("cycles_camera", "cycles_cand", "cycles_secondary")]
+    # instrumented pass: shares of the trace kernel's wave clocks per phase
     phase_share = ({k: round(v / sum(cyc), 4) for k, v in
-                    zip(("camera_walk", "camera_candidates", "secondary_walks", "shadow_queries"), cyc)}
+                    zip(("camera_walk", "camera_candidates", "secondary_walks"), cyc)}
                    if sum(cyc) > 0 else None)
-    if phase_share:  # the shadow share split by light type (cpu/light.c:49 vs :70)
-        sd = float(work["cycles_shadow_directional"]) / sum(cyc)
-        phase_share["shadow_directional"] = round(sd, 4)
-        phase_share["shadow_point"] = round(phase_share["shadow_queries"] - sd, 4)
     value = queries * args.steps / el / 1e6
-    # algorithmic bytes of one render launch (per rank, averaged over ranks)
-    alg_bytes = (wq * RAY_BYTES + nodes * NODE_BYTES + tris * TRI_BYTES + whits * NORMAL_BYTES +
-                 pixels * PIXEL_BYTES)
-    per_launch = alg_bytes / world
-    achieved = per_launch / (kern_ms * 1e-3) / 1e9
+    # Algorithmic bytes per launch of each kernel (DESIGN.md §4 "Roofline"),
+    # per rank: the records a wave pulls from the memory system (a record
+    # several lanes load with one instruction counts once) plus the rays' and
+    # hit records' own state.
+    kb = {
+        # closest-hit queries: ray, wave-distinct node / triangle fetches,
+        # the winner's normals, one hit record (2 float4 + prev) per hit,
+        # each lane's deepest-record index per item
+        "trace": (wcl * RAY_BYTES + nodes * NODE_BYTES + tris * TRI_BYTES +
+                  whits * (NORMAL_BYTES + HIT_RECORD_BYTES) + pixels * 4 * 4),
+        # per hit record: the record, its material, one term written; per
+        # shadow query: the ray and the walk's node (+ multipliers) and
+        # triangle fetches
+        "shade": (whits * (HIT_RECORD_BYTES + MATERIAL_BYTES + TERM_BYTES) + wsh * RAY_BYTES +
+                  sh_wnodes * (NODE_BYTES + NODE_MU_BYTES) + sh_wtris * TRI_BYTES),
+        # per pixel: 4 deepest indices, the chain's terms and links, the output
+        "fold": pixels * (4 * 4 + PIXEL_BYTES) + whits * (TERM_BYTES + 4),
+    }
+    kms = {"trace": trace_ms, "shade": shade_ms, "fold": fold_ms}
+    dom = max(("trace", "shade"), key=lambda k: kms[k])  # the dominant kernel
+    per_launch = kb[dom] / world
+    achieved = per_launch / (kms[dom] * 1e-3) / 1e9
     traffic = traffic_hi = None
     traffic_src = None
     if world == 1 and args.traffic_json is None and args.cull_slack is None and \
             args.camera_slack is None and args.policy is None and args.accel is None:
-        # default run: the newest committed rocprofv3 PMC pass of this
+        # default run: the newest committed rocprofv3 PMC passes of this
         # workload (profiles/r*_<workload>/, tools/gpu_profile.sh); a PMC
         # pass cannot run inside the bench, so the line says where it came from
         args.traffic_json = latest_profile(args.workload, "traffic.json")
         if args.valu_json is None:
-            args.valu_json = latest_profile(args.workload, "pmc_valu.json")
+            args.valu_json = latest_profile(args.workload, "pmc_sq.json")
+    kern_pmc = {}
     if args.traffic_json and os.path.exists(args.traffic_json):
         with open(args.traffic_json) as f:
             tj = json.load(f)
-        # FETCH_SIZE is exact for scattered 64 B requests and half the bytes
-        # of wide coalesced reads (MI355X_MICROARCH.md "HBM"); the kernel
-        # mixes both, so the raw count is a lower bound and x2 an upper one
-        if "fetch_size_kib_raw" in tj:
-            wb = tj.get("write_bytes_per_launch", 0.0)
-            traffic = tj["fetch_size_kib_raw"] * 1024 + wb
-            traffic_hi = tj["fetch_size_kib_raw"] * 2048 + wb
-        traffic_src = os.path.relpath(args.traffic_json, REPO)
-    valu = None
+        # per-kernel format (tools/pmc_traffic.py): FETCH_SIZE is exact for
+        # scattered 64 B requests and half the bytes of wide coalesced reads
+        # (MI355X_MICROARCH.md "HBM"): x1 lower bound, x2 upper
+        for k in ("trace", "shade", "fold"):
+            e = tj.get(k + "_kernel")
+            if e and "fetch_size_kib_raw" in e:
+                wb = e.get("write_bytes_per_launch", 0.0)
+                kern_pmc[k] = {"hbm_bytes": e["fetch_size_kib_raw"] * 1024 + wb,
+                               "hbm_bytes_upper": e["fetch_size_kib_raw"] * 2048 + wb}
+        if dom in kern_pmc:
+            traffic = kern_pmc[dom]["hbm_bytes"]
+            traffic_hi = kern_pmc[dom]["hbm_bytes_upper"]
+            traffic_src = os.path.relpath(args.traffic_json, REPO)
+    sq = {}
     if args.valu_json and os.path.exists(args.valu_json):
-        # the resource this kernel actually saturates: VALU
-        # issue.  SQ_* cycle counters count quad-cycles; GRBM_GUI_ACTIVE sums
-        # the 8 XCDs' busy clocks (MI355X_MICROARCH.md, DVFS give-back).
+        # SQ counters per kernel (tools/pmc_pass.sh, two passes merged by
+        # tools/gpu_profile.sh).  SQ_* cycle counters count quad-cycles
+        # (MI355X_MICROARCH.md); GRBM_GUI_ACTIVE sums the 8 XCDs' busy clocks.
         with open(args.valu_json) as f:
-            pm = json.load(f)
-        quad = pm["GRBM_GUI_ACTIVE"] / N_XCD / 4.0
-        valu = {
-            "busy_frac": round(pm["SQ_ACTIVE_INST_VALU"] / (N_SIMD * quad), 4),
-            "lane_util": round(pm["SQ_THREAD_CYCLES_VALU"] / (64.0 * pm["SQ_ACTIVE_INST_VALU"]), 4),
-            "valu_insts_per_launch": pm["SQ_INSTS_VALU"],
-            "clock_ghz": round(pm["GRBM_GUI_ACTIVE"] / N_XCD / (kern_ms * 1e-3) / 1e9, 3),
-            "source": os.path.relpath(args.valu_json, REPO),
-        }
-        if "SQ_WAVE_CYCLES" in pm:
-            # resident waves per SIMD, averaged over the kernel's duration
-            valu["waves_per_simd"] = round(pm["SQ_WAVE_CYCLES"] / (N_SIMD * quad), 3)
-        if "SQ_WAVES" in pm:
-            valu["waves_launched"] = pm["SQ_WAVES"]
+            pj = json.load(f)
+        for k in ("trace", "shade"):
+            pm = pj.get(k + "_kernel")
+            if not pm or "SQ_WAVE_CYCLES" not in pm:
+                continue
+            cycles = pm["GRBM_GUI_ACTIVE"] / N_XCD           # shader clocks of the dispatch
+            wc = pm["SQ_WAVE_CYCLES"]                           # quad-cycles, summed over waves
+            e = {
+                # a wave64 VALU instruction holds a 32-lane SIMD for >= 2 clocks
+                "valu_pipe_occupancy": round(pm["SQ_INSTS_VALU"] * 2 / (N_SIMD * cycles), 4),
+                "valu_lane_util": round(pm["SQ_THREAD_CYCLES_VALU"] / (64.0 * pm["SQ_ACTIVE_INST_VALU"]), 4),
+                "valu_insts_per_launch": pm["SQ_INSTS_VALU"],
+                "waves_per_simd": round(wc / (N_SIMD * cycles / 4.0), 3),
+                "clock_ghz": round(cycles / (kms[k] * 1e-3) / 1e9, 3),
+                # where a resident wave's clocks go (disjoint; sums to ~1)
+                "stall": {"issuing": round(pm["SQ_ACTIVE_INST_ANY"] / wc, 4),
+                          "wait_dependency": round(pm["SQ_WAIT_ANY"] / wc, 4),
+                          "wait_issue": round(pm["SQ_WAIT_INST_ANY"] / wc, 4)},
+                "valu_active_per_wave": round(pm["SQ_ACTIVE_INST_VALU"] / wc, 4),
+            }
+            for c in ("SQ_INSTS_VMEM_RD", "SQ_INSTS_LDS", "SQ_INSTS_SMEM", "SQ_INSTS_SALU"):
+                if c in pm:
+                    e[c.lower()[3:] + "_per_launch"] = pm[c]
+            if "SQ_ACTIVE_INST_LDS" in pm:
+                e["lds_active_per_wave"] = round(pm["SQ_ACTIVE_INST_LDS"] / wc, 4)
+            sq[k] = e
+        sq["source"] = os.path.relpath(args.valu_json, REPO)
 
     if rank == 0:
         cpu = None
@@ -381,45 +436,56 @@ def main():
                                       "closest_hits": int(hits), "pixels": int(pixels)},
             },
             "roofline": {
-                # priced against HBM; what the kernel
-                # actually saturates is VALU issue (valu.busy_frac)
+                # priced against HBM; the dominant kernel of
+                # the render (trace: camera + reflection paths; shade: shadow
+                # queries + Phong) -- see "kernels" for all three
                 "bound": "hbm",
-                "limiter": ("valu" if valu and valu["busy_frac"] > achieved / HBM_PEAK_GBS
-                            else None),
+                "kernel": f"{dom}_kernel<{'FLAT' if wl['accel'] == 'flat' else 'OCTREE'}>",
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
                 "traffic": traffic,
                 "traffic_upper": traffic_hi,
+                "hbm_measured_GBs": (round(traffic / (kms[dom] * 1e-3) / 1e9, 2)
+                                     if traffic is not None else None),
                 "traffic_source": (f"committed profile {traffic_src} (not measured in this run)"
                                    if traffic is not None else None),
-                "kernel": "render_kernel<FLAT>" if wl["accel"] == "flat" else "render_kernel<OCTREE>",
-                "kernel_ms": round(kern_ms, 3),
-                "candidate_lists_ms": round(lists_ms, 3),
+                "kernel_ms": round(kms[dom], 3),
                 "algorithmic_bytes_per_launch": int(per_launch),
-                "per_query_bytes": round(alg_bytes / wq, 1) if wq else None,
-                # wave-distinct record fetches (a record several lanes load with
-                # one instruction counts once) per query ...
-                "node_fetches_per_query": round(nodes / wq, 3) if wq else None,
-                "tri_fetches_per_query": round(tris / wq, 3) if wq else None,
+                "kernels": {k: {"ms": round(kms[k], 3),
+                                "algorithmic_bytes_per_launch": int(kb[k] / world),
+                                "achieved_GBs": round(kb[k] / world / (kms[k] * 1e-3) / 1e9, 2),
+                                "hbm_bytes_per_launch": (kern_pmc[k]["hbm_bytes"]
+                                                         if k in kern_pmc else None),
+                                "hbm_measured_GBs": (round(kern_pmc[k]["hbm_bytes"] /
+                                                           (kms[k] * 1e-3) / 1e9, 2)
+                                                     if k in kern_pmc else None)}
+                            for k in ("trace", "shade", "fold")},
+                "render_ms": round(kern_ms, 3),
+                "candidate_lists_ms": round(lists_ms, 3),
+                # wave-distinct record fetches per query (a record several lanes
+                # load with one instruction counts once) ...
+                "closest_fetches_per_query": {"nodes": round(nodes / wcl, 3) if wcl else None,
+                                              "tris": round(tris / wcl, 3) if wcl else None},
+                "shadow_fetches_per_query": {"nodes": round(sh_wnodes / wsh, 3) if wsh else None,
+                                             "tris": round(sh_wtris / wsh, 3) if wsh else None},
                 # ... and the per-lane work behind them (SURVEY.md §8(d) N_node, N_tri)
                 "per_lane": {
                     "closest_nodes_per_query": round(cl_nodes / wcl, 3) if wcl else None,
                     "closest_tris_per_query": round(cl_tris / wcl, 3) if wcl else None,
                     "shadow_nodes_per_query": round(sh_nodes / wsh, 3) if wsh else None,
                     "shadow_tris_per_query": round(sh_tris / wsh, 3) if wsh else None,
-                    # per-lane stack pushes that went past the LDS entries to HBM
                     "stack_spill_pushes": int(work["stack_spills"]),
-                    "bytes_per_launch": int((wq * RAY_BYTES + (cl_nodes + sh_nodes) * NODE_BYTES +
-                                             (cl_tris + sh_tris) * TRI_BYTES +
-                                             whits * NORMAL_BYTES + pixels * PIXEL_BYTES) / world),
                 },
                 "candidate_entries": int(cand_entries),
-                # instrumented pass: share of the waves' clocks per phase
-                "phase_share": phase_share,
+                "shadow_global_prims": info.get("shadow_global"),
+                "shadow_mu_max": info.get("shadow_mu_max"),
+                # instrumented pass: shares of the trace kernel's wave clocks
+                "trace_phase_share": phase_share,
             },
-            "valu": valu,
+            # SQ counters of the committed PMC passes, per kernel
+            "sq": sq or None,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -50,12 +50,13 @@ enum { RT_ACCEL_FLAT = 0, RT_ACCEL_OCTREE = 1, RT_ACCEL_OCTREE_GPU = 2 };
 /* Per-render counters.  closest = closest-hit queries
  * (collide() calls: camera + reflection rays), shadow = shadow queries
  * (collide_dist() calls), camera = 4*pixels rendered.  node_visits and
- * tri_tests are only filled by the instrumented kernel (rt_hip_set_count_work)
- * and give the algorithmic bytes of the roofline. */
+ * tri_tests (closest-hit queries) and shadow_node_visits / shadow_tri_tests
+ * are only filled by the instrumented kernels (rt_hip_set_count_work) and
+ * give the algorithmic bytes of the roofline. */
 typedef struct rt_stats {
   unsigned long long closest, shadow, camera;
   unsigned long long node_visits, tri_tests;
-  unsigned long long depth_overflow;   /* paths deeper than the term buffer (must be 0) */
+  unsigned long long depth_overflow;   /* paths past RT_MAX_BOUNCES or a stack overflow (must be 0) */
   unsigned long long zero_normal;      /* winners with an exactly-zero interpolated normal */
   unsigned long long pixels;
   unsigned long long hits;             /* closest-hit queries that hit geometry */
@@ -75,6 +76,16 @@ typedef struct rt_stats {
   unsigned long long cycles_camera, cycles_cand, cycles_secondary, cycles_shadow;
   unsigned long long cycles_shadow_directional;  /* the directional-light share of cycles_shadow */
   unsigned long long stack_spills;  /* per-lane stack pushes beyond the LDS entries (instrumented pass) */
+  unsigned long long shadow_zero_risk;  /* shadow rays whose first hit lies on an object that can
+                                         * interpolate a zero normal (must be 0, RT_EZERONORMAL) */
+  unsigned long long hit_records;   /* closest hits recorded for shading (trace -> shade) */
+  /* instrumented pass: wave-distinct node / triangle record fetches of the
+   * shadow queries (shade kernel); node_visits / tri_tests are then those of
+   * the closest-hit queries (trace kernel) */
+  unsigned long long shadow_node_visits, shadow_tri_tests;
+  /* point-light shadow rays whose origin lies beyond the extent the exact
+   * shadow walk assumes (csrc/rt_shadow.hip; must be 0, RT_EINEXACT) */
+  unsigned long long shadow_unproven;
 } rt_stats;
 
 /* Sizes of the device-side scene image, for the roofline accounting. */
@@ -89,6 +100,11 @@ typedef struct rt_accel_info {
   unsigned long long device_bytes;     /* total device memory of the scene image */
   double build_seconds;                /* build time (flatten + octree, host or device) */
   unsigned long long max_leaf;         /* largest leaf (triangle records)        */
+  /* exact shadow rays (octree, csrc/rt_shadow.hip): triangles every
+   * unshadowed shadow ray tests outside the walk, and the largest per-node
+   * multiplier of the shadow walk's culling slack */
+  unsigned long long shadow_global;
+  double shadow_mu_max;
 } rt_accel_info;
 
 /* Host-only: build the acceleration structure rt_hip_create would build and
@@ -124,9 +140,14 @@ int rt_hip_accel_info(const rt_hip_ctx *ctx, rt_accel_info *out);
 int rt_hip_accel_validate(const rt_hip_ctx *ctx);
 void rt_hip_destroy(rt_hip_ctx *ctx);
 
-/* Image tiling: 8x8-pixel tiles in PPM order, tile t belongs to rank t % nranks.
- * A rank's tile buffer holds rt_hip_tiles_per_rank() tiles, each 64 pixels
- * x 3 floats (pixel p of a tile = row p/8, col p%8 inside the tile). */
+/* Image tiling: 8x8-pixel tiles grouped in blocks of tb x tb tiles, tb = 4
+ * (32x32 pixels) when nranks > 1 and 1 (scanline tile order) for one rank;
+ * block b (scanline order over ceil(tiles_x/tb) x ceil(tiles_y/tb) blocks)
+ * belongs to rank b % nranks.  A rank's tile buffer holds its blocks
+ * in order, tb*tb tiles each in row-major order, each tile 64 pixels x 3 floats
+ * (pixel p of a tile = row p/8, col p%8 inside the tile); slots past the
+ * frame's edge are padding (0).  rt_hip_tiles_per_rank() = the largest
+ * rank's tile count (rank 0's), the size of every rank's buffer in a gather. */
 int rt_hip_tiles_per_rank(int width, int height, int nranks);
 size_t rt_hip_tile_buffer_floats(int width, int height, int nranks);
 
@@ -149,21 +170,26 @@ int rt_hip_set_cull_slack(rt_hip_ctx *ctx, float ulps);
  * to carry; exactness holds for every value. */
 int rt_hip_set_camera_slack(rt_hip_ctx *ctx, float ulps);
 /* Phase timing: with enable, every rt_hip_render records HIP events on its
- * stream before the camera candidate lists, before the render kernel and
- * after it (a ring of the last 1024 frames; enabling clears it).
+ * stream before the camera candidate lists, before and after each of its
+ * three kernels (a ring of the last 1024 frames; enabling clears it).
  * rt_hip_frame_times waits for the last n timed frames and returns their two
  * spans in milliseconds, oldest first (lists_ms ~0 without lists). */
 int rt_hip_set_timing(rt_hip_ctx *ctx, int enable);
 int rt_hip_frame_times(rt_hip_ctx *ctx, int n, float *lists_ms, float *render_ms);
+/* The render span of the same frames split by kernel: trace (closest-hit
+ * paths -> hit records), shade (shadow queries + Phong terms per record),
+ * fold (terms -> tile buffer). */
+int rt_hip_frame_kernel_times(rt_hip_ctx *ctx, int n, float *trace_ms, float *shade_ms,
+                              float *fold_ms);
 /* Instrumented build: also count node visits and triangle tests (slower). */
 /* Shader clocks of every work item -- (tile t, sample s) at index 4t + s,
  * rank-local tile order -- of the last instrumented render (n <= 4 x tiles
  * of the rank): the load-balance picture of a frame. */
 int rt_hip_tile_cycles(rt_hip_ctx *ctx, unsigned long long *out, size_t n);
 int rt_hip_set_count_work(rt_hip_ctx *ctx, int enable);
-/* The same items' phase clocks: phase 0 = the item's total (= rt_hip_tile_cycles),
- * 1 camera walk, 2 camera candidate tests, 3 secondary walks, 4 shadow
- * queries, 5 directional-light shadow queries. */
+/* The same items' phase clocks (trace kernel): phase 0 = the item's total
+ * (= rt_hip_tile_cycles), 1 camera walk, 2 camera candidate tests, 3
+ * secondary walks.  Shadow queries run in the shade kernel, per hit record. */
 int rt_hip_tile_phase_cycles(rt_hip_ctx *ctx, int phase, unsigned long long *out, size_t n);
 /* Exact camera rays (default 1): per-frame candidate lists of the triangles
  * whose float Moller-Trumbore error region the octree slack does not cover
@@ -196,6 +222,14 @@ int rt_cand_survey(const rt_scene *scene, float eps_ulps, double bound_scale, in
  * path's rank/frame filter dropped}. */
 int rt_hip_cand_verify(rt_hip_ctx *ctx, const rt_frame *frame, int rank, int nranks,
                        unsigned long long out[7]);
+
+/* Test hook: after an rt_hip_render, shade every stride-th hit record of
+ * each region again through the context's walk and by brute force over every
+ * triangle (cpu/hit.c:93-109), and compare each record's shadow outcome per
+ * light.  out = {records compared, shadow queries compared, records whose
+ * outcomes differ, queries the walk found lit and brute force shadowed}.
+ * The render's image and stats are untouched. */
+int rt_hip_verify_shadows(rt_hip_ctx *ctx, unsigned stride, unsigned long long out[4]);
 
 /* Diagnostic: candidate-list entries of each of the first n rank-local tiles
  * of the last render (n <= that rank's tile count). */

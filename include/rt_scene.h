@@ -28,10 +28,20 @@ enum {
   RT_ENOMEM = -4,    /* host allocation failed                           */
   RT_EHIP = -5,      /* HIP runtime error (device alloc, launch, copy)   */
   RT_ENODEV = -6,    /* no usable gfx950 device                          */
-  RT_EDEPTH = -7,    /* a path exceeded the reflection-depth buffer      */
+  RT_EDEPTH = -7,    /* a path needed more than RT_MAX_BOUNCES closest-hit queries
+                      * (cpu/rt recursion without end: Nr >= 1 mirrors), or a
+                      * traversal stack overflowed                       */
   RT_ERCCL = -8,     /* RCCL collective failed                           */
-  RT_EZERONORMAL = -9 /* a closest hit had an exactly zero interpolated normal:
-                       * cpu/hit.c:79 skips that object, which is not reproduced */
+  RT_EZERONORMAL = -9, /* a closest hit had an exactly zero interpolated normal, or
+                       * a shadow ray hit an object that can have one: cpu/hit.c:79,99
+                       * skips such an object, which is not reproduced     */
+  RT_EHITBUF = -10,  /* the frame made more hits than the hit-record buffer held:
+                      * the image is incomplete; the buffer has been grown to the
+                      * frame's need, render the frame again              */
+  RT_EINEXACT = -11  /* rendered with a tuning knob that gives up the cpu/rt parity
+                      * guarantee (rt_hip_set_exact_camera(0), a camera bound scale
+                      * < 1, a culling slack below the default): image written,
+                      * parity not guaranteed                             */
 };
 
 const char *rt_strerror(int code);

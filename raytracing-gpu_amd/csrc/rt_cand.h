@@ -36,6 +36,7 @@ struct CandParams {
   double c_dot, c_a;      // error-bound constants (tools/mt_bound.py C_DOT, C_A)
   double kmin, kmax, lmin, lmax_;  // sample coordinates of the frame
   int W, H, tiles_x, tiles_y, rank, nranks, ntiles_local;
+  int blocks_x, tb;       // tile blocks per block row, block side (csrc/rt_tiles.h: ranks own whole blocks)
   uint32_t* list;         // nprim: prims the float fast path cannot prove safe (pass 0)
   rtc::Footprint* fp;     // nprim: footprint of list entry j (pass 1, read by passes 2 and big)
   uint32_t* visits;       // nprim + 1: pass 0 flags, then tile entries of list entry j (pass 1)

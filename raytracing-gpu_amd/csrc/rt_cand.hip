@@ -32,6 +32,7 @@
 #include <rocprim/rocprim.hpp>
 
 #include "rt_cand.h"
+#include "rt_tiles.h"
 
 namespace rtc {
 
@@ -266,12 +267,11 @@ RTC_FN int classify(const CandParams& p, const float* r, const float* leafbox, F
   return FOOTPRINT;
 }
 
-// Tiles g in [lo, hi] (global indices) with g % n == r.
-__host__ __device__ inline uint32_t rank_tiles(uint32_t lo, uint32_t hi, uint32_t n, uint32_t r) {
-  // tiles g = r + m n with g in [lo, hi]: m in [ceil((lo - r) / n), floor((hi - r) / n)]
-  const long long mlo = lo <= r ? 0 : ((long long)lo - r + n - 1) / n;
-  const long long mhi = hi < r ? -1 : ((long long)hi - r) / n;
-  return mhi >= mlo ? (uint32_t)(mhi - mlo + 1) : 0u;
+// This rank's tiles in tile row ty, columns [x0, x1] (csrc/rt_tiles.h).
+__host__ __device__ inline uint32_t rank_tiles(const CandParams& p, int ty, int x0, int x1) {
+  if (x0 > x1) return 0u;
+  return rt_rank_row_tiles(ty, x0, x1, (uint32_t)p.nranks, (uint32_t)p.rank, (uint32_t)p.blocks_x,
+                           (uint32_t)p.tb, nullptr);
 }
 
 // Can a footprint inside the ball (q, rb) -- every candidate crossing point
@@ -334,15 +334,19 @@ RTC_FN bool rank_may_touch(const CandParams& p, const double q[3], double rb) {
   if (r0 > r1 || c0 > c1) return false;  // off the frame
   const uint32_t n = (uint32_t)p.nranks, rk = (uint32_t)p.rank;
   if (n == 1) return true;
-  const int tx0 = c0 >> 3, tx1 = c1 >> 3, ty0 = r0 >> 3, ty1 = r1 >> 3;
-  if ((uint32_t)p.tiles_x % n == 0) {  // rank = tile column mod n in every row
-    const uint32_t span = (uint32_t)(tx1 - tx0);
-    return span + 1 >= n || (rk + n - (uint32_t)tx0 % n) % n <= span;
-  }
-  if (ty1 - ty0 >= 8) return true;
-  for (int ty = ty0; ty <= ty1; ty++) {
-    const uint32_t base = (uint32_t)ty * (uint32_t)p.tiles_x;
-    if (rank_tiles(base + (uint32_t)tx0, base + (uint32_t)tx1, n, rk)) return true;
+  // whole tb x tb-tile blocks per rank, block b -> rank b mod n
+  // (csrc/rt_tiles.h): a block column range of >= n blocks meets every rank
+  // in every block row; otherwise one check per block row (the residues of
+  // the rows repeat with period n)
+  const int bx0 = (c0 >> 3) / p.tb, bx1 = (c1 >> 3) / p.tb;
+  const int by0 = (r0 >> 3) / p.tb, by1 = (r1 >> 3) / p.tb;
+  if ((uint32_t)(bx1 - bx0 + 1) >= n) return true;
+  const int rows = by1 - by0 + 1 < (int)n ? by1 - by0 + 1 : (int)n;
+  for (int k = 0; k < rows; k++) {
+    const uint32_t by = (uint32_t)(by0 + k);
+    const uint32_t res = (rk + n - (uint32_t)(((uint64_t)by * (uint32_t)p.blocks_x) % n)) % n;
+    const uint32_t f = (uint32_t)bx0 <= res ? res : (uint32_t)bx0 + (res + n - (uint32_t)bx0 % n) % n;
+    if (f <= (uint32_t)bx1) return true;
   }
   return false;
 }
@@ -550,8 +554,9 @@ __host__ __device__ void raster_row(const CandParams& p, const Footprint& fp, in
   int a0, a1, b0, b1;
   row_tiles(p, fp, ty, r0, r1, a0, a1, b0, b1);
   auto put = [&](int tx) {
-    const uint32_t g = (uint32_t)ty * (uint32_t)p.tiles_x + (uint32_t)tx;
-    if ((int)(g % (uint32_t)p.nranks) == p.rank) emit(g / (uint32_t)p.nranks);
+    uint32_t rk;
+    const uint32_t t = rt_tile_local(tx, ty, (uint32_t)p.nranks, (uint32_t)p.blocks_x, (uint32_t)p.tb, &rk);
+    if ((int)rk == p.rank) emit(t);
   };
   for (int tx = a0; tx <= a1; tx++) put(tx);
   for (int tx = b0; tx <= b1; tx++)
@@ -563,9 +568,7 @@ __host__ __device__ inline uint32_t count_row(const CandParams& p, const Footpri
                                               int r1) {
   int a0, a1, b0, b1;
   row_tiles(p, fp, ty, r0, r1, a0, a1, b0, b1);
-  const uint32_t base = (uint32_t)ty * (uint32_t)p.tiles_x, n = (uint32_t)p.nranks,
-                 r = (uint32_t)p.rank;
-  auto cnt = [&](int x0, int x1) { return x0 <= x1 ? rank_tiles(base + x0, base + x1, n, r) : 0u; };
+  auto cnt = [&](int x0, int x1) { return rank_tiles(p, ty, x0, x1); };
   uint32_t c = cnt(a0, a1) + cnt(b0, b1);
   if (a0 <= a1 && b0 <= b1) c -= cnt(a0 > b0 ? a0 : b0, a1 < b1 ? a1 : b1);  // overlap counted once
   return c;
@@ -692,20 +695,27 @@ __global__ __launch_bounds__(64) void big_count_kernel(CandParams p) {
   }
 }
 
-// The rank's tiles of one tile-row column interval [x0, x1] (base = first
-// global tile of the row): global tiles g0 + m n, local indices q0 + m with
-// q0 = g0 / n -- one division per interval, none per tile.  Returns the
-// count written at keys/vals[o ..].
-__device__ __forceinline__ uint32_t emit_interval(const CandParams& p, uint32_t base, int x0, int x1,
+// The rank's tiles of one tile-row column interval [x0, x1] of tile row ty:
+// the rank's blocks bx = f, f + n, ... of the row (csrc/rt_tiles.h), each
+// contributing its columns inside the interval at consecutive local indices
+// -- one division per block, none per tile.  Returns the count written at
+// keys/vals[o ..].
+__device__ __forceinline__ uint32_t emit_interval(const CandParams& p, int ty, int x0, int x1,
                                                   uint32_t o, uint32_t prim) {
   if (x0 > x1) return 0;
   const uint32_t n = (uint32_t)p.nranks, r = (uint32_t)p.rank;
-  const uint32_t lo = base + (uint32_t)x0, hi = base + (uint32_t)x1;
-  const uint32_t cnt = rank_tiles(lo, hi, n, r);
-  const uint32_t q0 = (lo + (r + n - lo % n) % n) / n;
-  for (uint32_t m = 0; m < cnt; m++) {
-    p.keys[o + m] = q0 + m;
-    p.vals[o + m] = prim;
+  int f;
+  const int tb = p.tb;
+  const uint32_t cnt = rt_rank_row_tiles(ty, x0, x1, n, r, (uint32_t)p.blocks_x, (uint32_t)tb, &f);
+  const uint32_t by = (uint32_t)(ty / tb), row = (uint32_t)(ty % tb) * (uint32_t)tb;
+  uint32_t k = 0;
+  for (int bx = f; k < cnt; bx += (int)n) {
+    const int a = x0 > bx * tb ? x0 : bx * tb, b = x1 < bx * tb + tb - 1 ? x1 : bx * tb + tb - 1;
+    const uint32_t base = ((by * (uint32_t)p.blocks_x + (uint32_t)bx) / n) * (uint32_t)(tb * tb) + row;
+    for (int tx = a; tx <= b; tx++, k++) {
+      p.keys[o + k] = base + (uint32_t)(tx - bx * tb);
+      p.vals[o + k] = prim;
+    }
   }
   return cnt;
 }
@@ -716,13 +726,12 @@ __device__ __forceinline__ uint32_t emit_row(const CandParams& p, const Footprin
                                              int r1, uint32_t o, uint32_t prim) {
   int a0, a1, b0, b1;
   row_tiles(p, fp, ty, r0, r1, a0, a1, b0, b1);
-  const uint32_t base = (uint32_t)ty * (uint32_t)p.tiles_x;
-  uint32_t k = emit_interval(p, base, a0, a1, o, prim);
+  uint32_t k = emit_interval(p, ty, a0, a1, o, prim);
   if (a0 > a1) {
-    k += emit_interval(p, base, b0, b1, o + k, prim);
+    k += emit_interval(p, ty, b0, b1, o + k, prim);
   } else {
-    k += emit_interval(p, base, b0, b1 < a0 - 1 ? b1 : a0 - 1, o + k, prim);
-    k += emit_interval(p, base, b0 > a1 + 1 ? b0 : a1 + 1, b1, o + k, prim);
+    k += emit_interval(p, ty, b0, b1 < a0 - 1 ? b1 : a0 - 1, o + k, prim);
+    k += emit_interval(p, ty, b0 > a1 + 1 ? b0 : a1 + 1, b1, o + k, prim);
   }
   return k;
 }
@@ -920,7 +929,15 @@ extern "C" int rt_cand_verify_host(const CandParams* p, const float* tri, const 
         if (qc != rtc::Q_LIST) out[5]++;
         continue;
       }
-      if (qc == rtc::Q_SAFE) continue;
+      if (qc == rtc::Q_SAFE) {
+        // the float fast path's proof checked against the f64 one: a prim it
+        // calls safe must have no tile here by classify() either
+        rtc::Footprint fp;
+        const float* lb = prim_leaf ? node + 8 * (size_t)prim_leaf[prim] : nullptr;
+        const int c = rtc::classify(*p, tri + 12 * (size_t)prim, lb, fp);
+        if (c == rtc::GLOBAL || (c == rtc::FOOTPRINT && rtc::raster_count(*p, fp) != 0)) out[5]++;
+        continue;
+      }
       if (qc == rtc::Q_LIST) {  // the device should have listed it
         out[5]++;
         continue;

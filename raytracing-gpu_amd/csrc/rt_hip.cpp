@@ -19,6 +19,8 @@
 #include "rt_build.h"
 #include "rt_cand.h"
 #include "rt_kernels.h"
+#include "rt_shadow.h"
+#include "rt_tiles.h"
 
 extern "C" {
 #include "../host/rt_cull.h"
@@ -66,10 +68,28 @@ struct rt_hip_ctx {
   float eps_ulps = RT_EPS_ULPS_DEFAULT;
   float cam_eps_ulps = RT_CAM_EPS_ULPS_DEFAULT;
   int policy = RT_POLICY_DEFAULT;  // traversal policy (tests / A/B only: rt_hip_set_policy)
-  float* d_terms = nullptr;        // deep reflection terms (KParams::terms)
   unsigned long long* d_tile_cycles = nullptr;  // COUNT pass: per-item clocks
-  float* d_samples = nullptr;                   // per-item sample colours (KParams::samples)
-  size_t samples_cap = 0;                       // tiles
+  // wavefront split (rt_render.hip): hit records of RT_HIT_REGIONS regions
+  float4* d_hit = nullptr;          // 2 float4 per record
+  uint32_t* d_hit_prev = nullptr;   // per record
+  float4* d_hit_term = nullptr;     // per record
+  uint32_t* d_hit_count = nullptr;  // RT_HIT_REGIONS append counters + as many shade chunk counters
+  size_t hit_cap = 0;               // records per region
+  size_t hit_need = 0;              // per region: what the last overflowing frame needed
+  uint32_t* d_last = nullptr;       // per (item, lane): a path's deepest record
+  size_t last_cap = 0;              // items
+  int grid_of[2][4][2] = {};        // persistent grids [trace][policy][count_work]
+  int cus = 0;                      // compute units of the device
+  std::vector<uint32_t> light_type; // per light (rt_hip_verify_shadows)
+  KParams last_p{};                 // the last render's parameters (rt_hip_verify_shadows)
+  // exact shadow rays (csrc/rt_shadow.hip), built for the slack sh_ulps
+  float2* d_prim_mu = nullptr;
+  float2* d_node_mu = nullptr;
+  uint32_t* d_sh_global = nullptr;
+  uint32_t n_sh_global = 0;
+  float sh_ulps = -1.0f;
+  float sh_omax = 0.0f;
+  float sh_mu_max = 1.0f;
   size_t tile_cycles_cap = 0, tile_cycles_n = 0;
   // exact camera rays (csrc/rt_cand.hip)
   int exact_camera = 1;
@@ -100,7 +120,7 @@ struct rt_hip_ctx {
   // candidate lists, before the render kernel and after it, on the render's
   // stream; a ring of the last RT_TIMED_FRAMES frames
   int timing = 0;
-  hipEvent_t ev[RT_TIMED_FRAMES][3] = {};
+  hipEvent_t ev[RT_TIMED_FRAMES][5] = {};  // lists | trace | shade | fold |
   unsigned long long frames = 0;  // timed frames recorded
 };
 
@@ -110,10 +130,21 @@ static int cand_params(const rt_frame* f, const float scene_c[3], float scene_r,
 static int tiles_x_of(int W) { return (W + 7) / 8; }
 static int tiles_y_of(int H) { return (H + 7) / 8; }
 
+// tile blocks of a frame split nranks ways (csrc/rt_tiles.h)
+static uint32_t nblocks_of(int W, int H, int nranks) {
+  const int tb = rt_block_side(nranks);
+  return (uint32_t)rt_blocks_x(tiles_x_of(W), tb) * (uint32_t)rt_blocks_y(tiles_y_of(H), tb);
+}
+
+// tiles rank `rank` renders (whole blocks, edge padding included)
+static int rank_tile_count(int W, int H, int rank, int nranks) {
+  const int tb = rt_block_side(nranks);
+  return (int)(rt_rank_blocks(nblocks_of(W, H, nranks), (uint32_t)nranks, (uint32_t)rank) * tb * tb);
+}
+
 extern "C" int rt_hip_tiles_per_rank(int width, int height, int nranks) {
   if (width <= 0 || height <= 0 || nranks <= 0) return 0;
-  long nt = (long)tiles_x_of(width) * tiles_y_of(height);
-  return (int)((nt + nranks - 1) / nranks);
+  return rank_tile_count(width, height, 0, nranks);  // rank 0 holds the most blocks
 }
 
 extern "C" size_t rt_hip_tile_buffer_floats(int width, int height, int nranks) {
@@ -151,9 +182,15 @@ extern "C" void rt_hip_destroy(rt_hip_ctx* c) {
   (void)hipFree(c->d_counter);
   (void)hipFree(c->d_stats);
   (void)hipFree(c->d_spill);
-  (void)hipFree(c->d_terms);
   (void)hipFree(c->d_tile_cycles);
-  (void)hipFree(c->d_samples);
+  (void)hipFree(c->d_hit);
+  (void)hipFree(c->d_hit_prev);
+  (void)hipFree(c->d_hit_term);
+  (void)hipFree(c->d_hit_count);
+  (void)hipFree(c->d_last);
+  (void)hipFree(c->d_prim_mu);
+  (void)hipFree(c->d_node_mu);
+  (void)hipFree(c->d_sh_global);
   if (c->d_tri_prim != c->d_tri) (void)hipFree(c->d_tri_prim);
   (void)hipFree(c->d_cand_list);
   (void)hipFree(c->d_cand_fp);
@@ -177,6 +214,64 @@ extern "C" void rt_hip_destroy(rt_hip_ctx* c) {
       if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
+}
+
+// Per-node slack multipliers of the shadow walk for the context's culling
+// slack (csrc/rt_shadow.hip): once per scene and slack, on the context's
+// stream, synchronous (setup; it reads back the global list's length).
+static int shadow_prepare(rt_hip_ctx* c, hipStream_t s) {
+  if (c->accel != RT_ACCEL_OCTREE || !c->d_node) return RT_OK;
+  if (c->d_node_mu && c->sh_ulps == c->eps_ulps) return RT_OK;
+  const size_t np = c->nprim, nn = c->info.nodes;
+  if (!c->d_node_mu) {
+    HIP_TRY(hipMalloc((void**)&c->d_prim_mu, (np + 1) * sizeof(float2)));
+    HIP_TRY(hipMalloc((void**)&c->d_sh_global, (np + 1) * sizeof(uint32_t)));
+    HIP_TRY(hipMalloc((void**)&c->d_node_mu, (nn + 1) * sizeof(float2)));
+  }
+  uint32_t* d_n = nullptr;
+  HIP_TRY(hipMalloc((void**)&d_n, sizeof(uint32_t)));
+  ShadowParams sp;
+  std::memset(&sp, 0, sizeof sp);
+  sp.tri = c->d_tri_prim;
+  sp.nprim = c->nprim;
+  sp.light = c->d_light;
+  sp.nlight = c->nlight;
+  sp.node = c->d_node;
+  sp.nnode = (uint32_t)nn;
+  sp.rec = c->d_tri;
+  for (int a = 0; a < 3; a++) sp.c[a] = c->scene_c[a];
+  sp.R = c->scene_r;
+  // the walk computes eps(o) in float (host/rt_cull.h); the multipliers keep
+  // a relative margin of 1e-6 and the +1 of the original slack on top
+  sp.eps_rel = (double)(c->eps_ulps * 5.9604645e-8f);
+  const double cmag = std::fmax(std::fabs(c->scene_c[0]), std::fmax(std::fabs(c->scene_c[1]),
+                                                                  std::fabs(c->scene_c[2])));
+  sp.plane_eps = (double)RT_CULL_PLANE * (cmag + c->scene_r) + 1e-6;
+  // point lights: shadow rays leave hit points, which lie on the scene's
+  // triangles up to the float error of their hit; origins beyond twice the
+  // scene's extent are counted (rt_stats.shadow_unproven), never assumed
+  sp.omax_assumed = 2.0 * c->scene_r + 1.0;
+  sp.reach_cap = c->scene_r + 1.0;
+  sp.prim_mu = c->d_prim_mu;
+  sp.node_mu = c->d_node_mu;
+  sp.global = c->d_sh_global;
+  sp.nglobal = d_n;
+  uint32_t n = 0;
+  std::vector<float2> nm(1);
+  hipError_t he = hipMemsetAsync(d_n, 0, sizeof(uint32_t), s);
+  if (he == hipSuccess) he = rt_shadow_build(&sp, (int)c->info.max_depth + 2, s);
+  if (he == hipSuccess) he = hipMemcpyAsync(&n, d_n, sizeof n, hipMemcpyDeviceToHost, s);
+  if (he == hipSuccess) he = hipMemcpyAsync(nm.data(), c->d_node_mu, sizeof(float2), hipMemcpyDeviceToHost, s);
+  if (he == hipSuccess) he = hipStreamSynchronize(s);
+  (void)hipFree(d_n);
+  if (he != hipSuccess) return rt_set_error(RT_EHIP, "shadow multipliers: %s", hipGetErrorString(he));
+  c->n_sh_global = n;
+  c->sh_omax = (float)(sp.omax_assumed * (1.0 - 1e-6));
+  c->sh_mu_max = nm[0].x;  // the root's: the max over the scene
+  c->sh_ulps = c->eps_ulps;
+  c->info.shadow_global = n;
+  c->info.shadow_mu_max = nm[0].x;
+  return RT_OK;
 }
 
 extern "C" int rt_hip_create(int device, const rt_scene* scene, int accel, rt_hip_ctx** out) {
@@ -220,6 +315,7 @@ extern "C" int rt_hip_create(int device, const rt_scene* scene, int accel, rt_hi
   if (!rc && fs.nnode) rc = upload(&c->d_node, fs.node, bytes_node);
   if (!rc) rc = upload(&c->d_counter, nullptr, 8 * 128);  // 8 item-stream counters (rt_render.hip)
   if (!rc) rc = upload(&c->d_stats, nullptr, RT_NSTATS * sizeof(unsigned long long));
+  if (!rc) rc = upload(&c->d_hit_count, nullptr, 2 * RT_HIT_REGIONS * 32 * sizeof(uint32_t));
   if (!rc && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
     rc = rt_set_error(RT_EHIP, "hipStreamCreate");
   rt_device_tree tree{};
@@ -281,18 +377,36 @@ extern "C" int rt_hip_create(int device, const rt_scene* scene, int accel, rt_hi
     rt_hip_destroy(c);
     return rc;
   }
-  // persistent grid: enough one-wave workgroups to fill every SIMD
+  // persistent grids: as many one-wave workgroups as each kernel's
+  // registers and LDS let a CU hold (rt_render_grid); the compat kernel
+  // keeps 16 per CU
   c->grid = prop.multiProcessorCount * 16;
+  c->cus = prop.multiProcessorCount;
+  for (size_t li = 0; li < scene->light_count; li++) c->light_type.push_back((uint32_t)scene->lights[li].type);
+  int gmax = c->grid;
+  const int dacc = c->accel == RT_ACCEL_FLAT ? RT_ACCEL_FLAT_D : RT_ACCEL_OCTREE_D;
+  for (int tr = 0; tr < 2; tr++)
+    for (int pol = 0; pol < 4; pol++)
+      for (int cw = 0; cw < 2; cw++) {
+        int g = 0;
+        hipError_t he = rt_render_grid(tr, dacc, cw, pol, prop.multiProcessorCount, &g);
+        if (he != hipSuccess) {
+          rt_hip_destroy(c);
+          return rt_set_error(RT_EHIP, "occupancy query: %s", hipGetErrorString(he));
+        }
+        c->grid_of[tr][pol][cw] = g;
+        gmax = g > gmax ? g : gmax;
+      }
+  // per-lane traversal stack spill area, [entry][lane] for the largest grid
   if (c->accel == RT_ACCEL_OCTREE &&
-      hipMalloc((void**)&c->d_spill, (size_t)c->grid * 64 * RT_SPILL_STACK * sizeof(uint2)) !=
-          hipSuccess) {
+      hipMalloc((void**)&c->d_spill, (size_t)gmax * 64 * RT_SPILL_STACK * sizeof(uint2)) != hipSuccess) {
     rt_hip_destroy(c);
     return rt_set_error(RT_EHIP, "hipMalloc traversal spill stack");
   }
-  if (hipMalloc((void**)&c->d_terms, (size_t)c->grid * 64 * 3 * (RT_MAX_DEPTH - RT_LDS_TERMS) *
-                                         sizeof(float)) != hipSuccess) {
+  rc = shadow_prepare(c, c->stream);
+  if (rc) {
     rt_hip_destroy(c);
-    return rt_set_error(RT_EHIP, "hipMalloc reflection terms");
+    return rc;
   }
   *out = c;
   return RT_OK;
@@ -453,6 +567,8 @@ extern "C" int rt_hip_cand_verify(rt_hip_ctx* c, const rt_frame* f, int rank, in
 extern "C" int rt_hip_cand_tile_entries(rt_hip_ctx* c, unsigned int* out, size_t n) {
   if (!c || !out) return rt_set_error(RT_EINVAL, "null argument");
   if (!c->d_cand_start) return rt_set_error(RT_EINVAL, "no candidate lists (render a frame first)");
+  if (n > (size_t)c->last_p.ntiles_local)
+    return rt_set_error(RT_EINVAL, "%zu tiles asked, the last render had %d", n, c->last_p.ntiles_local);
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = c->last_stream ? c->last_stream : c->stream;
   HIP_TRY(hipStreamSynchronize(s));
@@ -481,9 +597,26 @@ extern "C" int rt_hip_frame_times(rt_hip_ctx* c, int n, float* lists_ms, float* 
   HIP_TRY(hipSetDevice(c->device));
   for (int i = 0; i < n; i++) {
     hipEvent_t* e = c->ev[(c->frames - (unsigned long long)n + (unsigned long long)i) % RT_TIMED_FRAMES];
-    HIP_TRY(hipEventSynchronize(e[2]));
+    HIP_TRY(hipEventSynchronize(e[4]));
     HIP_TRY(hipEventElapsedTime(lists_ms + i, e[0], e[1]));
-    HIP_TRY(hipEventElapsedTime(render_ms + i, e[1], e[2]));
+    HIP_TRY(hipEventElapsedTime(render_ms + i, e[1], e[4]));
+  }
+  return RT_OK;
+}
+
+extern "C" int rt_hip_frame_kernel_times(rt_hip_ctx* c, int n, float* trace_ms, float* shade_ms,
+                                         float* fold_ms) {
+  if (!c || !trace_ms || !shade_ms || !fold_ms) return rt_set_error(RT_EINVAL, "null argument");
+  if (n <= 0 || n > RT_TIMED_FRAMES || (unsigned long long)n > c->frames)
+    return rt_set_error(RT_EINVAL, "%d timed frames asked, %llu recorded (ring of %d)", n,
+                        c->frames, RT_TIMED_FRAMES);
+  HIP_TRY(hipSetDevice(c->device));
+  for (int i = 0; i < n; i++) {
+    hipEvent_t* e = c->ev[(c->frames - (unsigned long long)n + (unsigned long long)i) % RT_TIMED_FRAMES];
+    HIP_TRY(hipEventSynchronize(e[4]));
+    HIP_TRY(hipEventElapsedTime(trace_ms + i, e[1], e[2]));
+    HIP_TRY(hipEventElapsedTime(shade_ms + i, e[2], e[3]));
+    HIP_TRY(hipEventElapsedTime(fold_ms + i, e[3], e[4]));
   }
   return RT_OK;
 }
@@ -501,7 +634,7 @@ extern "C" int rt_hip_tile_cycles(rt_hip_ctx* c, unsigned long long* out, size_t
 }
 
 extern "C" int rt_hip_tile_phase_cycles(rt_hip_ctx* c, int phase, unsigned long long* out, size_t n) {
-  if (!c || !out || phase < 0 || phase > 5) return rt_set_error(RT_EINVAL, "bad argument");
+  if (!c || !out || phase < 0 || phase > 3) return rt_set_error(RT_EINVAL, "bad argument");
   if (!c->d_tile_cycles || n > c->tile_cycles_n)
     return rt_set_error(RT_EINVAL, "%zu item clocks asked, %zu recorded (rt_hip_set_count_work)", n,
                         c->tile_cycles_n);
@@ -625,8 +758,9 @@ static int cand_params(const rt_frame* f, const float scene_c[3], float scene_r,
   cp.tiles_y = tiles_y_of(H);
   cp.rank = rank;
   cp.nranks = nranks;
-  const int ntot = cp.tiles_x * cp.tiles_y;
-  cp.ntiles_local = (ntot - rank + nranks - 1) / nranks;
+  cp.tb = rt_block_side(nranks);
+  cp.blocks_x = rt_blocks_x(cp.tiles_x, cp.tb);
+  cp.ntiles_local = rank_tile_count(W, H, rank, nranks);
   return RT_OK;
 }
 
@@ -751,6 +885,38 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
   return RT_OK;
 }
 
+// Hit-record buffers for a rank of ntiles tiles: first sized for 2 hits per
+// camera ray (the reference scenes make 0.5-1.3; C5 0.48), then for what an
+// overflowing frame needed (rt_hip_stats -> RT_EHITBUF); `last` for every
+// (item, lane).
+static int hit_buffers(rt_hip_ctx* c, size_t ntiles) {
+  const size_t items = 4 * ntiles;
+  if (items > c->last_cap) {
+    (void)hipFree(c->d_last);
+    c->d_last = nullptr;
+    c->last_cap = 0;
+    HIP_TRY(hipMalloc((void**)&c->d_last, items * 64 * sizeof(uint32_t)));
+    c->last_cap = items;
+  }
+  size_t want = (2 * items * 64 + RT_HIT_REGIONS - 1) / RT_HIT_REGIONS + 1024;
+  if (c->hit_need > want) want = c->hit_need;
+  if (want > (1ull << 29) - 1) want = (1ull << 29) - 1;  // slot field of a record index
+  if (want <= c->hit_cap && c->d_hit) return RT_OK;
+  (void)hipFree(c->d_hit);
+  (void)hipFree(c->d_hit_prev);
+  (void)hipFree(c->d_hit_term);
+  c->d_hit = nullptr;
+  c->d_hit_prev = nullptr;
+  c->d_hit_term = nullptr;
+  c->hit_cap = 0;
+  const size_t n = want * RT_HIT_REGIONS;
+  HIP_TRY(hipMalloc((void**)&c->d_hit, n * 2 * sizeof(float4)));
+  HIP_TRY(hipMalloc((void**)&c->d_hit_prev, n * sizeof(uint32_t)));
+  HIP_TRY(hipMalloc((void**)&c->d_hit_term, n * sizeof(float4)));
+  c->hit_cap = want;  // only once every buffer exists
+  return RT_OK;
+}
+
 extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nranks,
                              float* d_tiles, void* stream) {
   if (!c || !f || !d_tiles) return rt_set_error(RT_EINVAL, "null argument");
@@ -778,7 +944,7 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
   p.ntiles_total = tiles_x_of(f->width) * tiles_y_of(f->height);
   p.rank = rank;
   p.nranks = nranks;
-  p.ntiles_local = (p.ntiles_total - rank + nranks - 1) / nranks;
+  p.ntiles_local = rank_tile_count(f->width, f->height, rank, nranks);
   p.out = d_tiles;
   p.tile_counter = c->d_counter;
   p.stats = c->d_stats;
@@ -791,15 +957,17 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
   // (DESIGN.md "Conservative culling")
   p.eps_rel = c->eps_ulps * 5.9604645e-8f;
   p.eps_rel_cam = c->cam_eps_ulps * 5.9604645e-8f;
-  p.terms = c->d_terms;
-  if ((size_t)p.ntiles_local > c->samples_cap) {
-    (void)hipFree(c->d_samples);
-    c->d_samples = nullptr;
-    c->samples_cap = 0;
-    HIP_TRY(hipMalloc((void**)&c->d_samples, (size_t)p.ntiles_local * 4 * 192 * sizeof(float)));
-    c->samples_cap = (size_t)p.ntiles_local;
+  {
+    int rc = hit_buffers(c, (size_t)p.ntiles_local);
+    if (rc) return rc;
   }
-  p.samples = c->d_samples;
+  p.hit = c->d_hit;
+  p.hit_prev = c->d_hit_prev;
+  p.hit_term = c->d_hit_term;
+  p.hit_count = c->d_hit_count;
+  p.shade_counter = c->d_hit_count + RT_HIT_REGIONS * 32;
+  p.hit_cap = (uint32_t)c->hit_cap;
+  p.last = c->d_last;
   if (c->count_work) {  // per-item clocks of the instrumented pass (rt_hip_tile_cycles)
     const size_t items = 4 * (size_t)p.ntiles_local;
     if (items > c->tile_cycles_cap) {
@@ -812,6 +980,14 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
     c->tile_cycles_n = items;
     p.tile_cycles = c->d_tile_cycles;
   }
+  {
+    int rc = shadow_prepare(c, s);  // no-op unless the culling slack changed
+    if (rc) return rc;
+  }
+  p.node_mu = c->d_node_mu;
+  p.sh_global = c->d_sh_global;
+  p.n_sh_global = c->n_sh_global;
+  p.sh_omax = c->sh_omax;
   c->cand_prims = c->cand_entries = c->cand_global = 0;
   hipEvent_t* ev = c->ev[c->frames % RT_TIMED_FRAMES];
   if (c->timing) HIP_TRY(hipEventRecord(ev[0], s));
@@ -819,33 +995,131 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
     int rc = cand_prepare(c, f, &p, s);
     if (rc) return rc;
   }
-  if (c->accel == RT_ACCEL_OCTREE && !c->d_node) {
-    // empty scene: nothing to traverse, the FLAT kernel with 0 records is exact
-    HIP_TRY(hipMemsetAsync(c->d_counter, 0, 8 * 128, s));  // 8 item streams, 128 B apart
-    HIP_TRY(hipMemsetAsync(c->d_stats, 0, RT_NSTATS * sizeof(unsigned long long), s));
-    if (c->timing) HIP_TRY(hipEventRecord(ev[1], s));
-    HIP_TRY(rt_launch_render(&p, RT_ACCEL_FLAT_D, c->count_work, c->policy, c->grid, s));
-  } else {
-    HIP_TRY(hipMemsetAsync(c->d_counter, 0, 8 * 128, s));  // 8 item streams, 128 B apart
-    HIP_TRY(hipMemsetAsync(c->d_stats, 0, RT_NSTATS * sizeof(unsigned long long), s));
-    if (c->timing) HIP_TRY(hipEventRecord(ev[1], s));
-    HIP_TRY(rt_launch_render(&p, c->accel, c->count_work, c->policy, c->grid, s));
-  }
+  // an empty octree scene has nothing to traverse: the FLAT kernels with 0
+  // records are exact (their grids are the FLAT instantiation's own)
+  const bool empty = c->accel == RT_ACCEL_OCTREE && !c->d_node;
+  const int dacc = (c->accel == RT_ACCEL_FLAT || empty) ? RT_ACCEL_FLAT_D : RT_ACCEL_OCTREE_D;
+  const int pol = dacc == RT_ACCEL_FLAT_D ? 0 : c->policy, cw = c->count_work ? 1 : 0;
+  const int gt = empty ? c->grid : c->grid_of[1][pol][cw], gs = empty ? c->grid : c->grid_of[0][pol][cw];
+  HIP_TRY(hipMemsetAsync(c->d_counter, 0, 8 * 128, s));  // 8 item streams, 128 B apart
+  HIP_TRY(hipMemsetAsync(c->d_stats, 0, RT_NSTATS * sizeof(unsigned long long), s));
+  HIP_TRY(hipMemsetAsync(c->d_hit_count, 0, 2 * RT_HIT_REGIONS * 32 * sizeof(uint32_t), s));
+  if (c->timing) HIP_TRY(hipEventRecord(ev[1], s));
+  HIP_TRY(rt_launch_trace(&p, dacc, c->count_work, pol, gt, s));
+  if (c->timing) HIP_TRY(hipEventRecord(ev[2], s));
+  HIP_TRY(rt_launch_shade(&p, dacc, c->count_work, pol, gs, s));
+  if (c->timing) HIP_TRY(hipEventRecord(ev[3], s));
+  HIP_TRY(rt_launch_fold(&p, s));
+  c->last_p = p;
   if (c->timing) {
-    HIP_TRY(hipEventRecord(ev[2], s));
+    HIP_TRY(hipEventRecord(ev[4], s));
     c->frames++;
   }
   c->last_stream = s;
   return RT_OK;
 }
 
+// Shadow verification (tests, tools): the last render's hit records shaded
+// again, every stride-th record of each region, once through the context's
+// walk (octree) and once by brute force over every triangle (the FLAT any-hit
+// of cpu/hit.c:93-109 over the prim-order records), and the two unshadowed-
+// light masks compared record by record.  The render's image, terms and stats
+// are left as they were.  out = {records compared, shadow queries compared,
+// records whose masks differ, queries the walk called lit and brute force
+// shadowed}.
+extern "C" int rt_hip_verify_shadows(rt_hip_ctx* c, unsigned stride, unsigned long long out[4]) {
+  if (!c || !out) return rt_set_error(RT_EINVAL, "null argument");
+  if (!c->d_hit || !c->last_p.hit) return rt_set_error(RT_EINVAL, "no hit records (render a frame first)");
+  if (c->nlight > 32) return rt_set_error(RT_EINVAL, "shadow verification covers at most 32 lights");
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = c->last_stream ? c->last_stream : c->stream;
+  HIP_TRY(hipStreamSynchronize(s));
+  const size_t n = c->hit_cap * RT_HIT_REGIONS;
+  uint32_t *lit[2] = {nullptr, nullptr}, *ctr = nullptr;
+  float4* term = nullptr;
+  unsigned long long* st = nullptr;
+  int rc = RT_OK;
+  uint32_t hc[RT_HIT_REGIONS * 32];
+  std::vector<uint32_t> la, lb;
+  unsigned long long nsh = 0;
+  for (uint32_t li = 0; li < c->nlight; li++) nsh += c->light_type[li] == 1 || c->light_type[li] == 2;
+  if (hipMalloc((void**)&lit[0], n * sizeof(uint32_t)) != hipSuccess ||
+      hipMalloc((void**)&lit[1], n * sizeof(uint32_t)) != hipSuccess ||
+      hipMalloc((void**)&term, n * sizeof(float4)) != hipSuccess ||
+      hipMalloc((void**)&ctr, RT_HIT_REGIONS * 32 * sizeof(uint32_t)) != hipSuccess ||
+      hipMalloc((void**)&st, RT_NSTATS * sizeof(unsigned long long)) != hipSuccess) {
+    rc = rt_set_error(RT_EHIP, "hipMalloc shadow verification buffers");
+    goto done;
+  }
+  for (int pass = 0; pass < 2 && !rc; pass++) {
+    KParams p = c->last_p;
+    p.hit_term = term;
+    p.hit_lit = lit[pass];
+    p.shade_stride = stride ? stride : 1;
+    p.shade_counter = ctr;
+    p.stats = st;
+    int dacc = c->accel == RT_ACCEL_FLAT || !c->d_node ? RT_ACCEL_FLAT_D : RT_ACCEL_OCTREE_D;
+    int g = c->grid_of[0][0][0];
+    if (pass == 1) {  // brute force over the prim-order records
+      p.tri = c->d_tri_prim;
+      p.nrec = c->nprim;
+      p.node = nullptr;
+      dacc = RT_ACCEL_FLAT_D;
+      if (rt_render_grid(0, RT_ACCEL_FLAT_D, 0, 0, c->cus, &g) != hipSuccess) g = c->grid;
+    }
+    if (hipMemsetAsync(lit[pass], 0xff, n * sizeof(uint32_t), s) != hipSuccess ||
+        hipMemsetAsync(ctr, 0, RT_HIT_REGIONS * 32 * sizeof(uint32_t), s) != hipSuccess ||
+        rt_launch_shade(&p, dacc, 0, dacc == RT_ACCEL_FLAT_D ? 0 : c->policy, g, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      rc = rt_set_error(RT_EHIP, "shadow verification pass %d: %s", pass,
+                        hipGetErrorString(hipGetLastError()));
+  }
+  if (rc) goto done;
+  la.resize(n);
+  lb.resize(n);
+  if (hipMemcpy(la.data(), lit[0], n * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(lb.data(), lit[1], n * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(hc, c->d_hit_count, sizeof hc, hipMemcpyDeviceToHost) != hipSuccess) {
+    rc = rt_set_error(RT_EHIP, "shadow verification read-back");
+    goto done;
+  }
+  std::memset(out, 0, 4 * sizeof *out);
+  for (int x = 0; x < RT_HIT_REGIONS; x++) {
+    const size_t cnt = hc[32 * x] < c->hit_cap ? hc[32 * x] : c->hit_cap;
+    for (size_t k = 0; k < cnt; k += (stride ? stride : 1)) {
+      const size_t a = (size_t)x * c->hit_cap + k;
+      out[0]++;
+      if (la[a] != lb[a]) {
+        out[2]++;
+        out[3] += (unsigned long long)__builtin_popcount(la[a] & ~lb[a]);
+      }
+    }
+  }
+  out[1] = out[0] * nsh;
+done:
+  (void)hipFree(lit[0]);
+  (void)hipFree(lit[1]);
+  (void)hipFree(term);
+  (void)hipFree(ctr);
+  (void)hipFree(st);
+  return rc;
+}
+
 extern "C" int rt_hip_stats(rt_hip_ctx* c, rt_stats* out) {
   if (!c || !out) return rt_set_error(RT_EINVAL, "null argument");
   HIP_TRY(hipSetDevice(c->device));
   unsigned long long h[RT_NSTATS];
+  uint32_t hc[RT_HIT_REGIONS * 32];
   hipStream_t s = c->last_stream ? c->last_stream : c->stream;
   HIP_TRY(hipMemcpyAsync(h, c->d_stats, sizeof h, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(hc, c->d_hit_count, sizeof hc, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  size_t need = 0;
+  unsigned long long records = 0;
+  for (int x = 0; x < RT_HIT_REGIONS; x++) {
+    need = hc[32 * x] > need ? hc[32 * x] : need;
+    records += hc[32 * x];
+  }
   std::memset(out, 0, sizeof *out);
   out->closest = h[0];
   out->shadow = h[1];
@@ -866,11 +1140,21 @@ extern "C" int rt_hip_stats(rt_hip_ctx* c, rt_stats* out) {
   out->cycles_shadow = h[15];
   out->cycles_shadow_directional = h[16];
   out->stack_spills = h[17];
+  out->shadow_zero_risk = h[18];
+  out->shadow_node_visits = h[19];
+  out->shadow_tri_tests = h[20];
+  out->shadow_unproven = h[21];
+  out->hit_records = records;
   out->cand_prims = c->cand_prims;
   out->cand_entries = c->cand_entries;
   out->cand_global = c->cand_global;
+  if (need > c->hit_cap) {  // the frame is incomplete: grow for the next render
+    c->hit_need = need + need / 4 + 1024;
+    return rt_set_error(RT_EHITBUF, "%llu hit records, %zu per region held (grown to %zu: render again)",
+                        records, c->hit_cap, c->hit_need);
+  }
   if (out->depth_overflow)
-    return rt_set_error(RT_EDEPTH, "%llu paths overflowed the depth/stack buffers",
+    return rt_set_error(RT_EDEPTH, "%llu paths overflowed the bounce limit or a traversal stack",
                         out->depth_overflow);
   // never silent: the image may differ from cpu/rt's there
   if (out->zero_normal)
@@ -878,6 +1162,16 @@ extern "C" int rt_hip_stats(rt_hip_ctx* c, rt_stats* out) {
                         "%llu closest hits had an exactly zero interpolated normal (cpu/hit.c:79 "
                         "would skip those objects)",
                         out->zero_normal);
+  if (out->shadow_zero_risk)
+    return rt_set_error(RT_EZERONORMAL,
+                        "%llu shadow rays hit an object whose interpolated normal can vanish "
+                        "(cpu/hit.c:99 may skip it; early any-hit exit not proven exact)",
+                        out->shadow_zero_risk);
+  if (out->shadow_unproven)
+    return rt_set_error(RT_EINEXACT,
+                        "%llu point-light shadow rays left from beyond the extent the shadow "
+                        "walk's exactness bound assumes (csrc/rt_shadow.hip)",
+                        out->shadow_unproven);
   return RT_OK;
 }
 
@@ -905,13 +1199,17 @@ extern "C" int rt_hip_render_image(rt_hip_ctx* c, const rt_frame* f, float* h_rg
     (void)hipFree(d_tiles);
     return rt_set_error(RT_EHIP, "hipMalloc image");
   }
-  int rc = rt_hip_render(c, f, 0, 1, d_tiles, nullptr);
-  if (!rc) rc = rt_hip_assemble(c, f, d_tiles, 1, d_rgb, nullptr);
-  if (!rc && hipMemcpyAsync(h_rgb, d_rgb, npx * 3 * sizeof(float), hipMemcpyDeviceToHost,
-                            c->stream) != hipSuccess)
-    rc = rt_set_error(RT_EHIP, "D2H image");
   rt_stats tmp;
-  if (!rc) rc = rt_hip_stats(c, st ? st : &tmp);
+  int rc = RT_OK;
+  for (int attempt = 0; attempt < 2; attempt++) {  // once more after the hit buffer grew
+    rc = rt_hip_render(c, f, 0, 1, d_tiles, nullptr);
+    if (!rc) rc = rt_hip_assemble(c, f, d_tiles, 1, d_rgb, nullptr);
+    if (!rc && hipMemcpyAsync(h_rgb, d_rgb, npx * 3 * sizeof(float), hipMemcpyDeviceToHost,
+                              c->stream) != hipSuccess)
+      rc = rt_set_error(RT_EHIP, "D2H image");
+    if (!rc) rc = rt_hip_stats(c, st ? st : &tmp);
+    if (rc != RT_EHITBUF) break;
+  }
   (void)hipFree(d_tiles);
   (void)hipFree(d_rgb);
   return rc;
@@ -973,10 +1271,21 @@ extern "C" int rt_hip_render_compat(rt_hip_ctx* c, const rt_camera* cam, unsigne
   p.spill = c->d_spill;
   p.eps_rel = c->eps_ulps * 5.9604645e-8f;
   p.eps_rel_cam = c->cam_eps_ulps * 5.9604645e-8f;
-  p.terms = c->d_terms;
   const int accel = (c->accel == RT_ACCEL_FLAT || !c->d_node) ? RT_ACCEL_FLAT_D : RT_ACCEL_OCTREE_D;
+  rc = shadow_prepare(c, s);
+  if (rc) {
+    (void)hipFree(d_hi);
+    (void)hipFree(d_lo);
+    return rc;
+  }
+  p.node_mu = c->d_node_mu;
+  p.sh_global = c->d_sh_global;
+  p.n_sh_global = c->n_sh_global;
+  p.sh_omax = c->sh_omax;
+  p.tri_prim = c->d_tri_prim;
   if (hipMemsetAsync(c->d_counter, 0, 8 * 128, s) != hipSuccess ||
       hipMemsetAsync(c->d_stats, 0, RT_NSTATS * sizeof(unsigned long long), s) != hipSuccess ||
+      hipMemsetAsync(c->d_hit_count, 0, 2 * RT_HIT_REGIONS * 32 * sizeof(uint32_t), s) != hipSuccess ||
       rt_launch_compat(&p, accel, c->grid, s) != hipSuccess ||
       rt_launch_downscale(d_hi, d_lo, cam->width, cam->height, s) != hipSuccess ||
       hipMemcpyAsync(h_rgba, d_lo, nlo * sizeof(uint32_t), hipMemcpyDeviceToHost, s) != hipSuccess)
@@ -1127,7 +1436,15 @@ extern "C" int rt_raytrace_multi(const char* input, const char* output, int ngpu
     (void)hipDeviceSynchronize();
   }
   t0 = std::chrono::steady_clock::now();
-  rc = per_gpu(ngpus, [&](int g) { return rt_hip_render(ctx[g], &f, g, ngpus, d_tiles[g], nullptr); });
+  rc = per_gpu(ngpus, [&](int g) {
+    int r = rt_hip_render(ctx[g], &f, g, ngpus, d_tiles[g], nullptr);
+    rt_stats st;
+    if (!r && (r = rt_hip_stats(ctx[g], &st)) == RT_EHITBUF)  // the buffer grew: once more
+      r = rt_hip_render(ctx[g], &f, g, ngpus, d_tiles[g], nullptr);
+    else if (r == RT_EDEPTH || r == RT_EZERONORMAL)
+      r = RT_OK;  // reported by the stats pass below
+    return r;
+  });
   if (rc) goto out;
   if (ngpus > 1) {
     // one gather of every rank's tile buffer to device 0 over xGMI

@@ -11,12 +11,18 @@
 #define RT_ACCEL_OCTREE_D 1
 #define RT_MAT_FLOATS_D 12
 #define RT_LIGHT_FLOATS_D 8
-#define RT_MAX_DEPTH 32
-#define RT_NSTATS 18
+// closest-hit queries one path may make before the render reports RT_EDEPTH:
+// cpu/rt recurses while coef >= 0.01 (cpu/raytracer.c:19-34), which is
+// unbounded for mirrors of Nr >= 1; paths of Nr < 1 end long before this
+#define RT_MAX_BOUNCES 16384
+#define RT_NSTATS 22
 // per-lane global overflow area of the traversal stack (entries beyond LDS)
 #define RT_SPILL_STACK 112
-// reflection terms of a path kept in LDS (deeper ones: KParams::terms)
-#define RT_LDS_TERMS 4
+// hit records (the wavefront split, rt_render.hip): 8 regions, one per
+// item stream, each with its own append counter; a record index is
+// region | (slot << 3), RT_NO_REC = none
+#define RT_HIT_REGIONS 8
+#define RT_NO_REC 0xffffffffu
 // occupancy target of the render kernels' launch bounds (waves per SIMD).
 // The kernels need 123 VGPRs and 9.7 KB of LDS, so they still run 4 waves
 // per SIMD; a target of 3 only changes the scheduler's trade-offs (measured,
@@ -24,6 +30,21 @@
 #ifndef RT_MIN_WAVES
 #define RT_MIN_WAVES 3
 #endif
+// occupancy targets of the wavefront split's kernels (waves per SIMD):
+// trace_kernel (closest-hit walks, candidate tests) needs 104 registers left
+// alone, 96 at 5 waves (C5 trace 7.35 -> 6.34 ms, profiles/r03d/); shade_kernel
+// (shadow queries + Phong per hit record) fits 64 at 8 (7.19 -> 6.89 ms)
+#ifndef RT_TRACE_MIN_WAVES
+#define RT_TRACE_MIN_WAVES 5
+#endif
+#ifndef RT_SHADE_MIN_WAVES
+#define RT_SHADE_MIN_WAVES 8
+#endif
+// triangle record flag (q2.w bits, host/accel.c rt_flatten): the record's
+// object has a triangle whose interpolated normal can be exactly zero, so
+// cpu/hit.c:99 may skip the object in collide_dist (early any-hit exit is
+// then not known to be exact)
+#define RT_REC_ZERO_RISK 1u
 // traversal policies (one kernel instantiation each, rt_render.hip); the
 // others exist for tests and A/B measurements
 #define RT_POLICY_DEFAULT 0     // staged packet closest hit for coherent queries, per-lane shadows
@@ -44,6 +65,8 @@ struct WorkCount {
   uint32_t cy_cam, cy_cand, cy_sec, cy_shadow;
   uint32_t cy_shadow_dir;  // the directional-light part of cy_shadow
   uint32_t stack_spills;   // per-lane stack pushes past the LDS entries (COUNT pass)
+  uint32_t zero_risk;      // shadow hits on objects whose interpolated normal can vanish
+  uint32_t sh_unproven;    // point-light shadow rays from beyond the proof's assumed extent
 };
 
 struct KParams {
@@ -56,8 +79,28 @@ struct KParams {
   rt::f3 u, v, C, pos;  // camera frame (cpu/raytracer.c:82-86)
   int W, H;
   int tiles_x, ntiles_total, rank, nranks, ntiles_local;
-  float* out;                   // rank's tile buffer (written by combine_kernel)
-  float* samples;               // ntiles_local x 4 samples x 3 channels x 64 lanes: sample colours
+  float* out;                   // rank's tile buffer (written by fold_kernel)
+  // wavefront split (rt_render.hip): trace_kernel appends one hit record per
+  // closest hit, shade_kernel turns each into its reflection term, fold_kernel
+  // sums every path's terms deepest-first and a pixel's four samples
+  float4* hit;                  // RT_HIT_REGIONS x hit_cap records: P.xyz N.x | N.yz coef obj
+  uint32_t* hit_prev;           // per record: the path's previous record (RT_NO_REC)
+  float4* hit_term;             // per record: color_mul(apply_light(...), coef), rgb
+  uint32_t* hit_count;          // RT_HIT_REGIONS append counters, 32 words apart
+  uint32_t hit_cap;             // records per region
+  uint32_t* last;               // per (item, lane): the path's deepest record (RT_NO_REC)
+  uint32_t* shade_counter;      // RT_HIT_REGIONS chunk counters of shade_kernel, 32 words apart
+  // shadow verification (rt_hip_verify_shadows; NULL / 0 in renders): the
+  // shade pass writes each shaded record's unshadowed-light mask (lights
+  // 0..31) and shades only every shade_stride-th record of each region
+  uint32_t* hit_lit;
+  uint32_t shade_stride;
+  // exact shadow rays (csrc/rt_shadow.hip): per-node (mu, nu) multipliers of
+  // the shadow walk's slack, and the prims every unshadowed shadow ray tests
+  const float2* node_mu;
+  const uint32_t* sh_global;
+  uint32_t n_sh_global;
+  float sh_omax;  // point-light shadow origins with |o - c|_max beyond this are counted unproven
   uint32_t* tile_counter;       // 8 item-stream counters, 32 words apart; zeroed before launch
   unsigned long long* stats;    // RT_NSTATS counters, zeroed before launch
   uint2* spill;                 // grid*64 lanes x RT_SPILL_STACK stack entries
@@ -67,7 +110,6 @@ struct KParams {
   float eps_rel;                // culling slack, rt_cull.h rt_cull_eps()
   float eps_rel_cam;            // the same for camera rays (bounce depth 0)
   unsigned long long* tile_cycles;  // COUNT pass: shader clocks of each work item (tile, sample) (NULL: none)
-  float* terms;                 // (RT_MAX_DEPTH - RT_LDS_TERMS) x grid*64 lanes x 3: deep reflection terms
   // camera-ray candidate lists (csrc/rt_cand.hip); cand_start == NULL: none
   const uint32_t* cand_start;   // ntiles_local + 1 offsets into cand
   const uint32_t* cand;         // prims
@@ -77,9 +119,17 @@ struct KParams {
   const float* cand_skip;       // per cand entry: lower bound of new_dist - |pos - o| (depth skip)
 };
 
-// policy = RT_POLICY_* (octree only)
-extern "C" hipError_t rt_launch_render(const KParams* p, int accel, int count_work, int policy,
-                                       int grid, hipStream_t stream);
+// The three launches of one render (policy = RT_POLICY_*, octree only):
+// trace (closest hits -> hit records), shade (shadow queries + Phong per
+// record -> terms), fold (terms -> the rank's tile buffer)
+extern "C" hipError_t rt_launch_trace(const KParams* p, int accel, int count_work, int policy,
+                                      int grid, hipStream_t stream);
+extern "C" hipError_t rt_launch_shade(const KParams* p, int accel, int count_work, int policy,
+                                      int grid, hipStream_t stream);
+extern "C" hipError_t rt_launch_fold(const KParams* p, hipStream_t stream);
+// persistent grid (one-wave workgroups) of trace (trace = 1) or shade on `cus` CUs
+extern "C" hipError_t rt_render_grid(int trace, int accel, int count_work, int policy, int cus,
+                                     int* grid);
 // gpu/rt compatibility mode: p->W x p->H = the 3x upscaled frame, p->out =
 // its packed RGBA8 image; then the 3x3 downscale to W x H (PNG row order)
 extern "C" hipError_t rt_launch_compat(const KParams* p, int accel, int grid, hipStream_t stream);

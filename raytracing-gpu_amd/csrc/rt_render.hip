@@ -25,6 +25,7 @@
 #include "rt_cull.h"
 #include "rt_device.h"
 #include "rt_kernels.h"
+#include "rt_tiles.h"
 
 namespace rt {
 
@@ -34,7 +35,6 @@ static constexpr float kEps = 0.0000001f;  // cpu/hit.c:7 (float)1e-7
 // order, so LDS staging needs no s_barrier: only a compiler barrier that
 // keeps the LDS reads and writes in source order.
 __device__ __forceinline__ void wave_sync() { __asm__ volatile("" ::: "memory"); }
-static constexpr int kMaxDepth = RT_MAX_DEPTH;
 
 __device__ __forceinline__ f3 ld3(const float* p) { return f3{p[0], p[1], p[2]}; }
 
@@ -143,13 +143,21 @@ __device__ __forceinline__ void consider(const Ray& r, const float4& q0, const f
   }
 }
 
+// Any hit with new_dist > 0.01 (cpu/hit.c:93-109: collide_dist > 0 <=>
+// shadowed, cpu/light.c:24-31).  Early exit is exact for an object none of
+// whose triangles can interpolate an exactly zero normal (record flag bit 0,
+// host/accel.c): its closest hit then counts in collide_dist whatever
+// triangle the walk met first.  A hit on a flagged object sets `risk`
+// (reported as RT_EZERONORMAL, never silent).
 __device__ __forceinline__ bool any_hit_rec(const Ray& r, const float4& q0, const float4& q1,
-                                            const float4& q2) {
+                                            const float4& q2, uint32_t& risk) {
   f3 v0{q0.x, q0.y, q0.z}, e1{q0.w, q1.x, q1.y}, e2{q1.z, q1.w, q2.x};
   if (!mt_candidate(r.o, r.d, v0, e1, e2, __builtin_inff())) return false;
   float t, u, v;
   if (!mt_test(r.o, r.d, v0, e1, e2, t, u, v)) return false;
-  return (double)hit_dist(r, t) > 0.01;
+  if (!((double)hit_dist(r, t) > 0.01)) return false;
+  risk |= __float_as_uint(q2.w) & RT_REC_ZERO_RISK;
+  return true;
 }
 
 // -------------------------------------------------------------- OCTREE
@@ -173,6 +181,7 @@ struct Stack {
 // WorkCount after the walk (absorb).
 struct LaneCount {
   uint32_t nodes, tris, overflow;
+  uint32_t risk;           // any hit on an object whose normal can vanish (any_hit_rec)
   uint32_t lnodes, ltris;  // this lane's own visits / tests (COUNT pass)
   uint32_t spills;         // pushes beyond the LDS part of the stack (COUNT pass)
 };
@@ -217,6 +226,7 @@ __device__ __forceinline__ void absorb(WorkCount& wc, const LaneCount& lc, bool 
     }
   }
   wc.overflow += wave_sum(lc.overflow);
+  wc.zero_risk += (uint32_t)__popcll(__ballot(lc.risk != 0));
   if (COUNT) wc.stack_spills += wave_sum(lc.spills);
 }
 
@@ -254,6 +264,22 @@ __device__ __forceinline__ float box_enter(const Ray& r, f3 inv, float4 lo, floa
   bool hit = rt_box_hit(r.oh.x, r.oh.y, r.oh.z, r.ol.x, r.ol.y, r.ol.z, inv.x, inv.y, inv.z, lo.x,
                         lo.y, lo.z, hi.x, hi.y, hi.z, &t);
   return hit ? t : __builtin_inff();
+}
+
+// Shadow walk box test (csrc/rt_shadow.hip): the box grown by mu eps instead
+// of eps, and reaching parameters t >= -nu eps / |d| (a float accept may sit
+// slightly behind the origin).  mn = the node's (mu, nu), both >= 1.
+__device__ __forceinline__ bool box_hit_sh(const Ray& r, f3 inv, float4 lo, float4 hi, float2 mn) {
+  const float e = r.eps * mn.x;
+  float tmin;
+  const float ohx = r.o.x + e, ohy = r.o.y + e, ohz = r.o.z + e;
+  const float olx = r.o.x - e, oly = r.o.y - e, olz = r.o.z - e;
+  float tx0 = fmaf(lo.x, inv.x, -(ohx * inv.x)), tx1 = fmaf(hi.x, inv.x, -(olx * inv.x));
+  float ty0 = fmaf(lo.y, inv.y, -(ohy * inv.y)), ty1 = fmaf(hi.y, inv.y, -(oly * inv.y));
+  float tz0 = fmaf(lo.z, inv.z, -(ohz * inv.z)), tz1 = fmaf(hi.z, inv.z, -(olz * inv.z));
+  tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
+  const float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+  return tmax >= fmaxf(tmin, -(mn.y * r.eps) / r.dlen);
 }
 
 __device__ __forceinline__ bool rt_prune(float t_enter, float dlen, float best, float eps) {
@@ -323,7 +349,8 @@ __device__ __forceinline__ void push_children(const float4* __restrict__ node, c
 // octant arithmetic (any-hit needs no exact front-to-back order).  Child
 // k+1's box is in flight while child k is tested.
 template <bool COUNT>
-__device__ __forceinline__ void push_children_any(const float4* __restrict__ node, const Ray& r,
+__device__ __forceinline__ void push_children_any(const float4* __restrict__ node,
+                                                  const float2* __restrict__ mu, const Ray& r,
                                                   f3 inv, uint32_t dm, uint32_t first,
                                                   uint32_t info, Stack& s, LaneCount& wc) {
   const int cnt = (int)RT_NODE_COUNT(info);
@@ -332,16 +359,19 @@ __device__ __forceinline__ void push_children_any(const float4* __restrict__ nod
   const int step = up ? 1 : -1;
   uint32_t ci = first + (uint32_t)k;
   float4 nlo = node[2 * ci], nhi = node[2 * ci + 1];
+  float2 nmu = mu[ci];
   if (COUNT) wc.nodes += lanes_distinct(ci);
   for (int n = 0; n < cnt; n++) {
     float4 clo = nlo, chi = nhi;
+    const float2 cmu = nmu;
     if (n + 1 < cnt) {
       ci += (uint32_t)step;
       nlo = node[2 * ci];
       nhi = node[2 * ci + 1];
+      nmu = mu[ci];
       if (COUNT) wc.nodes += lanes_distinct(ci);
     }
-    if (box_enter(r, inv, clo, chi) != __builtin_inff()) push(s, __float_as_uint(clo.w), chi.w, wc);
+    if (box_hit_sh(r, inv, clo, chi, cmu)) push(s, __float_as_uint(clo.w), chi.w, wc);
   }
 }
 
@@ -364,7 +394,7 @@ __device__ __forceinline__ bool leaf_lane(const float4* __restrict__ tri, uint32
       wc.ltris++;
     }
     if (ANY) {
-      if (any_hit_rec(r, q0, q1, q2)) return true;
+      if (any_hit_rec(r, q0, q1, q2, wc.risk)) return true;
     } else {
       consider(r, q0, q1, q2, b);
     }
@@ -414,7 +444,7 @@ __device__ bool oct_any(const KParams& p, const Ray& r, Stack& s, LaneCount& wc)
   {
     float4 lo = node[0], hi = node[1];
     if (COUNT) wc.nodes += lanes_distinct(0);
-    if (box_enter(r, inv, lo, hi) != __builtin_inff()) push(s, __float_as_uint(lo.w), hi.w, wc);
+    if (box_hit_sh(r, inv, lo, hi, p.node_mu[0])) push(s, __float_as_uint(lo.w), hi.w, wc);
   }
   Best unused;
   while (s.sp > 0) {
@@ -430,7 +460,7 @@ __device__ bool oct_any(const KParams& p, const Ray& r, Stack& s, LaneCount& wc)
         return true;
       }
     } else {
-      push_children_any<COUNT>(node, r, inv, dm, first, info, s, wc);
+      push_children_any<COUNT>(node, p.node_mu, r, inv, dm, first, info, s, wc);
     }
   }
   wave_sync();
@@ -564,6 +594,7 @@ __device__ void flat_closest_w(const KParams& p, const Ray& r, bool act, Best& b
 template <bool COUNT>
 __device__ bool flat_any_w(const KParams& p, const Ray& r, bool act, WaveCtx& w, WorkCount& wc) {
   bool alive = act, hit = false;
+  uint32_t risk = 0;
   const uint32_t n = p.nrec;
   if (__ballot(alive) == 0 || n == 0) return false;
   Fetch f = fetch_issue(p.tri, 3 * (int)chunk<kFlatRecs>(n, 0), w.lane);
@@ -583,7 +614,7 @@ __device__ bool flat_any_w(const KParams& p, const Ray& r, bool act, WaveCtx& w,
       n0 = w.stage[kn];
       n1 = w.stage[kn + 1];
       n2 = w.stage[kn + 2];
-      if (alive && any_hit_rec(r, q0, q1, q2)) {
+      if (alive && any_hit_rec(r, q0, q1, q2, risk)) {
         hit = true;
         alive = false;
       }
@@ -591,6 +622,7 @@ __device__ bool flat_any_w(const KParams& p, const Ray& r, bool act, WaveCtx& w,
     }
     if (__ballot(alive) == 0) break;
   }
+  wc.zero_risk += (uint32_t)__popcll(__ballot(risk != 0));
   return hit;
 }
 
@@ -671,6 +703,7 @@ __device__ bool flat_any_tp(const KParams& p, const Ray& r, bool act, WorkCount&
   const int lane = (int)(threadIdx.x & 63);
   uint64_t am = __ballot(act);
   bool res = false;
+  uint32_t risk = 0;  // per lane: any tested triangle's flag (conservative)
   while (am) {
     const int l = __ffsll((unsigned long long)am) - 1;
     am &= am - 1;
@@ -682,7 +715,7 @@ __device__ bool flat_any_tp(const KParams& p, const Ray& r, bool act, WorkCount&
       bool h = false;
       if (i < n) {
         const float4* t = p.tri + 3 * (size_t)i;
-        h = any_hit_rec(q, t[0], t[1], t[2]);
+        h = any_hit_rec(q, t[0], t[1], t[2], risk);
       }
       hit = __ballot(h) != 0;
     }
@@ -693,6 +726,7 @@ __device__ bool flat_any_tp(const KParams& p, const Ray& r, bool act, WorkCount&
     }
     if (lane == l) res = hit;
   }
+  wc.zero_risk += (uint32_t)__popcll(__ballot(risk != 0));
   return res;
 }
 
@@ -702,7 +736,8 @@ __device__ bool flat_any_tp(const KParams& p, const Ray& r, bool act, WorkCount&
 template <bool ANY>
 __device__ __forceinline__ void stage_push_children(const Ray& r, f3 inv, uint32_t dm,
                                                     uint32_t info, bool want, float limit,
-                                                    int& sp, WaveCtx& w, WorkCount& wc) {
+                                                    int& sp, WaveCtx& w, WorkCount& wc,
+                                                    const float2* __restrict__ mu = nullptr) {
   uint32_t mask = RT_NODE_MASK(info), cnt = RT_NODE_COUNT(info);
   uint64_t lanes[8];
   uint32_t hitmask = 0;
@@ -711,8 +746,13 @@ __device__ __forceinline__ void stage_push_children(const Ray& r, f3 inv, uint32
     lanes[c] = 0;
     if ((uint32_t)c < cnt) {
       float4 clo = w.stage[2 * c], chi = w.stage[2 * c + 1];
-      float t0 = box_enter(r, inv, clo, chi);
-      bool w2 = want && t0 != __builtin_inff() && (ANY || !(t0 * r.dlen > limit));
+      bool w2;
+      if (ANY) {
+        w2 = want && box_hit_sh(r, inv, clo, chi, mu[c]);  // the shadow walk's grown boxes
+      } else {
+        float t0 = box_enter(r, inv, clo, chi);
+        w2 = want && t0 != __builtin_inff() && !(t0 * r.dlen > limit);
+      }
       lanes[c] = __ballot(w2);
       if (lanes[c] != 0) hitmask |= 1u << c;
     }
@@ -799,6 +839,7 @@ __device__ bool staged_any(const KParams& p, const Ray& r, bool act, WaveCtx& w,
   const float4* __restrict__ node = p.node;
   const float4* __restrict__ tri = p.tri;
   bool alive = act, hit = false;
+  uint32_t risk = 0;
   uint64_t am = __ballot(alive);
   if (am == 0) return false;
   f3 inv = inv_dir(r.d);
@@ -831,7 +872,7 @@ __device__ bool staged_any(const KParams& p, const Ray& r, bool act, WaveCtx& w,
         for (uint32_t k = 0; k < m; k++) {
           if (COUNT) wc.sh_tris += (uint32_t)__popcll(__ballot(want));
           float4 q0 = w.stage[3 * k], q1 = w.stage[3 * k + 1], q2 = w.stage[3 * k + 2];
-          if (want && any_hit_rec(r, q0, q1, q2)) {
+          if (want && any_hit_rec(r, q0, q1, q2, risk)) {
             hit = true;
             alive = false;
             want = false;
@@ -842,9 +883,10 @@ __device__ bool staged_any(const KParams& p, const Ray& r, bool act, WaveCtx& w,
       if (__ballot(alive) == 0) break;
     } else {
       stage_load(node + 2 * (size_t)first, 2 * (int)RT_NODE_COUNT(info), w);
-      stage_push_children<true>(r, inv, dm, info, want, 0.0f, sp, w, wc);
+      stage_push_children<true>(r, inv, dm, info, want, 0.0f, sp, w, wc, p.node_mu + first);
     }
   }
+  wc.zero_risk += (uint32_t)__popcll(__ballot(risk != 0));
   return hit;
 }
 
@@ -886,7 +928,7 @@ __device__ __forceinline__ void closest_q(const KParams& p, const Ray& r, bool a
   if (staged) {
     staged_closest<COUNT>(p, r, act, b, w, wc);
   } else {
-    LaneCount lc = {0, 0, 0, 0, 0, 0};
+    LaneCount lc = {0, 0, 0, 0, 0, 0, 0};
     if (act) oct_closest<COUNT>(p, r, b, s, lc);
     absorb<COUNT>(wc, lc, false);
   }
@@ -904,16 +946,40 @@ __device__ __forceinline__ bool shadow_q(const KParams& p, f3 o, f3 d, uint32_t 
     return use_tp(p, act) ? flat_any_tp<COUNT>(p, r, act, wc) : flat_any_w<COUNT>(p, r, act, w, wc);
   bool staged = POL == RT_POLICY_STAGED ||
                 (POL == RT_POLICY_DIR_STAGED && type == 1 && __popcll(am) >= kPacketMin);
-  if (staged) return staged_any<COUNT>(p, r, act, w, wc);
-  LaneCount lc = {0, 0, 0, 0, 0, 0};
-  bool hit = act && oct_any<COUNT>(p, r, s, lc);
-  absorb<COUNT>(wc, lc, true);
+  bool hit;
+  if (staged) {
+    hit = staged_any<COUNT>(p, r, act, w, wc);
+  } else {
+    LaneCount lc = {0, 0, 0, 0, 0, 0, 0};
+    hit = act && oct_any<COUNT>(p, r, s, lc);
+    absorb<COUNT>(wc, lc, true);
+  }
+  // the prims whose float error region no slack multiplier bounds
+  // (csrc/rt_shadow.hip): tested by every ray the walk found unshadowed
+  if (p.n_sh_global && __ballot(act && !hit)) {
+    uint32_t risk = 0;
+    for (uint32_t k = 0; k < p.n_sh_global; k++) {
+      const float4* q = p.tri_prim + 3 * (size_t)uni(p.sh_global[k]);
+      const float4 q0 = ldu(q, 0), q1 = ldu(q, 1), q2 = ldu(q, 2);
+      if (act && !hit) hit = any_hit_rec(r, q0, q1, q2, risk);
+      if (__ballot(act && !hit) == 0) break;
+    }
+    wc.zero_risk += (uint32_t)__popcll(__ballot(risk != 0));
+  }
+  // point lights: the cosine bound assumed origins within sh_omax of the scene centre
+  if (type == 2) {
+    const float m = fmaxf(fabsf(o.x - p.scene_c.x), fmaxf(fabsf(o.y - p.scene_c.y), fabsf(o.z - p.scene_c.z)));
+    wc.sh_unproven += (uint32_t)__popcll(__ballot(act && !(m <= p.sh_omax)));
+  }
   return hit;
 }
 
 // pow of cpu/light.c:20, out of line: inlined, its f64 polynomial
 // coefficients were hoisted out of the path loop and spilled to scratch.
-__device__ __noinline__ float spec_pow(double x, double e) { return (float)pow(fmax(x, 0.0), e); }
+#ifndef RT_SPEC_POW_INLINE
+#define RT_SPEC_POW_INLINE __noinline__
+#endif
+__device__ RT_SPEC_POW_INLINE float spec_pow(double x, double e) { return (float)pow(fmax(x, 0.0), e); }
 
 // cpu/light.c:7-22
 __device__ __forceinline__ col specular(col tmp, f3 inc_o, f3 inc_d, f3 P, f3 N, const float* m) {
@@ -1055,59 +1121,75 @@ __device__ __forceinline__ void cand_closest(const KParams& p, const Ray& r, boo
   }
 }
 
-// Reflection terms of one path, folded deepest-first at the end
-// (cpu/raytracer.c:19-34 returns color_add(local, reflected) from the
-// deepest call outwards).  The first kLdsTerms live in LDS, [term][channel]
-// [lane] so a wave's accesses are conflict-free (in registers they were
-// spilled around every walk: the walks need all 128 VGPRs); deeper ones --
-// rare, C5 paths end by depth 3 -- go to this lane's slots of a global
-// overflow area laid out [term][lane] so a wave's stores coalesce.
-static constexpr int kLdsTerms = RT_LDS_TERMS;
-
-struct Terms {
-  float* lds;     // s_terms + lane
-  float* over;    // p.terms + 3 * global lane
-  size_t stride;  // floats between consecutive overflow terms of a lane
-};
-
-__device__ __forceinline__ void term_put(Terms& T, int k, col c) {
-  if (k < kLdsTerms) {
-    float* q = T.lds + k * 192;
-    q[0] = c.r;
-    q[64] = c.g;
-    q[128] = c.b;
-  } else {
-    float* q = T.over + (size_t)(k - kLdsTerms) * T.stride;
-    q[0] = c.r;
-    q[1] = c.g;
-    q[2] = c.b;
-  }
+// PPM (row, col) of lane `lane` of rank-local tile t (rt_hip.h "Image
+// tiling", csrc/rt_tiles.h): 8 x 8 pixels, lane = row * 8 + col.
+__device__ __forceinline__ void tile_pixel(const KParams& p, uint32_t t, int lane, int& pr,
+                                           int& pc) {
+  int tx, ty;
+  const int tb = rt_block_side(p.nranks);
+  rt_tile_xy(t, (uint32_t)p.rank, (uint32_t)p.nranks, (uint32_t)rt_blocks_x(p.tiles_x, tb), (uint32_t)tb,
+             &tx, &ty);
+  pr = ty * 8 + (lane >> 3);
+  pc = tx * 8 + (lane & 7);
 }
 
-__device__ __forceinline__ col term_get(const Terms& T, int k) {
-  if (k < kLdsTerms) {
-    const float* q = T.lds + k * 192;
-    return col{q[0], q[64], q[128]};
-  }
-  const float* q = T.over + (size_t)(k - kLdsTerms) * T.stride;
-  return col{q[0], q[1], q[2]};
+// The wave's counters are wave totals already: one atomic per counter per
+// wave.  The wave-distinct record fetches (nodes, tris) of the shade kernel's
+// shadow queries go to their own slots, so each kernel's algorithmic bytes
+// can be priced on its own (bench.py roofline).
+__device__ __forceinline__ void flush_counts(const KParams& p, const WorkCount& wc, int lane,
+                                             bool shade = false) {
+  uint32_t v[RT_NSTATS] = {wc.closest, wc.shadow,   wc.pixels,      shade ? 0u : wc.nodes,
+                           shade ? 0u : wc.tris,    wc.overflow, wc.zero_normal, wc.hits,
+                           wc.cl_nodes, wc.cl_tris, wc.sh_nodes,   wc.sh_tris,
+                           wc.cy_cam,   wc.cy_cand, wc.cy_sec,     wc.cy_shadow,
+                           wc.cy_shadow_dir, wc.stack_spills, wc.zero_risk,
+                           shade ? wc.nodes : 0u, shade ? wc.tris : 0u, wc.sh_unproven};
+#pragma unroll
+  for (int k = 0; k < RT_NSTATS; k++)
+    if (lane == 0 && v[k]) atomicAdd(p.stats + k, (unsigned long long)v[k]);
 }
 
-// One camera sample (cpu/raytracer.c:19-34) for every lane of the wave: the
-// recursion becomes a wave-uniform bounce loop.  valid = the lane owns a pixel.
+// ---------------------------------------------------------- wavefront split
+// A render is three launches.  trace_kernel follows every camera sample's
+// path of closest hits (cpu/raytracer.c:19-34) and appends one hit record per
+// hit -- the bounce never depends on the shading: ray_bounce takes only the
+// hit (cpu/raytracer.c:28, cpu/ray.c:16-25) and the next coefficient only the
+// material (cpu/raytracer.c:29).  shade_kernel then runs the shadow queries
+// and Phong terms of every record (cpu/light.c:33-100) with the 64 lanes of a
+// wave on 64 records -- no lane idles on a sky pixel or an ended path -- in a
+// lean kernel that keeps more waves resident than the walk-heavy trace, and
+// writes the record's term color_mul(local, coef) (cpu/raytracer.c:30).
+// fold_kernel sums each path's terms deepest-first (color_add(reflection,
+// term) from the deepest call outwards) and a pixel's four samples in the
+// reference's order.  The same operations on the same values as the
+// recursion, so the same bits; a path's length is bounded only by
+// RT_MAX_BOUNCES (cpu/rt: by its stack).
+
+// Hit record, 2 float4: P.xyz N.x | N.y N.z coef bits(obj); its path's
+// previous record in hit_prev.  Record index = region | (slot << 3).
+__device__ __forceinline__ size_t rec_addr(const KParams& p, uint32_t idx) {
+  return (size_t)(idx & 7u) * p.hit_cap + (idx >> 3);
+}
+
+// One camera sample for every lane of the wave (trace_kernel): the
+// recursion as a wave-uniform bounce loop, a hit record appended per hit (one
+// atomic per wave and bounce, on the item stream's own counter x).  Returns
+// the lane's deepest record (RT_NO_REC: none).  valid = the lane owns a pixel.
 template <int ACCEL, bool COUNT, int POL>
-__device__ __forceinline__ col trace_path(const KParams& p, bool valid, f3 o, f3 d, float coef,
-                                          Stack& s, WaveCtx& w, WorkCount& wc, uint32_t tile,
-                                          Terms& T) {
-  int depth = 0;
+__device__ __forceinline__ uint32_t trace_path(const KParams& p, bool valid, f3 o, f3 d,
+                                               uint32_t x, Stack& s, WaveCtx& w, WorkCount& wc,
+                                               uint32_t tile) {
+  int depth = 0;  // wave-uniform: queries so far on this path
   bool alive = valid;
-  bool first = true;  // wave-uniform: the camera query (bounce depth 0)
+  float coef = 1.0f;
+  uint32_t prev = RT_NO_REC;
   for (;;) {
     alive = alive && !((double)coef < 0.01);  // checked before the query
     uint64_t am = __ballot(alive);
     if (am == 0) break;
     wc.closest += (uint32_t)__popcll(am);  // wave-uniform counters (SGPRs)
-    Ray r = make_ray(p, o, d, first ? p.eps_rel_cam : p.eps_rel);
+    Ray r = make_ray(p, o, d, depth == 0 ? p.eps_rel_cam : p.eps_rel);
     Best b;
     b.dist = __builtin_inff();
     b.t_cut = __builtin_inff();
@@ -1119,12 +1201,11 @@ __device__ __forceinline__ col trace_path(const KParams& p, bool valid, f3 o, f3
     closest_q<ACCEL, COUNT, POL>(p, r, alive, depth, b, s, w, wc);
     if (COUNT) {
       const uint64_t c1 = __builtin_readcyclecounter();
-      (first ? wc.cy_cam : wc.cy_sec) += (uint32_t)(c1 - c0);
+      (depth == 0 ? wc.cy_cam : wc.cy_sec) += (uint32_t)(c1 - c0);
       c0 = c1;
     }
-    if (ACCEL != RT_ACCEL_FLAT_D && first) cand_closest<COUNT>(p, r, alive, tile, b, w, wc);
+    if (ACCEL != RT_ACCEL_FLAT_D && depth == 0) cand_closest<COUNT>(p, r, alive, tile, b, w, wc);
     if (COUNT) wc.cy_cand += (uint32_t)(__builtin_readcyclecounter() - c0);
-    first = false;
     bool hit = alive && b.dist != __builtin_inff();
     f3 N = f3{0.0f, 0.0f, 0.0f};
     wc.hits += (uint32_t)__popcll(__ballot(hit));
@@ -1137,30 +1218,40 @@ __device__ __forceinline__ col trace_path(const KParams& p, bool valid, f3 o, f3
     }
     wc.zero_normal += (uint32_t)__popcll(__ballot(zero));
     hit = hit && !zero;
-    const float* m = p.mat + RT_MAT_FLOATS_D * (hit ? b.obj : 0u);
-    f3 P = hit ? hit_point(r, b.t) : o;  // the winner's hit point, same bits
-    col local = apply_light<ACCEL, COUNT, POL>(p, hit, m, P, N, s, w, wc);
-    alive = hit;
-    bool deep = hit && depth == kMaxDepth;
-    wc.overflow += (uint32_t)__popcll(__ballot(deep));
+    const uint64_t hm = __ballot(hit);
+    if (hm == 0) break;
+    uint32_t base = 0;
+    if (w.lane == 0) base = atomicAdd(p.hit_count + 32u * x, (uint32_t)__popcll(hm));
+    base = uni(base);
+    bool deep = false;
     if (hit) {
-      if (deep) {
-        alive = false;
+      const uint32_t slot = base + (uint32_t)__popcll(hm & ((1ull << w.lane) - 1ull));
+      const f3 P = hit_point(r, b.t);  // the winner's hit point, same bits
+      if (slot < p.hit_cap) {  // else: counted, and rt_hip_stats reports the overflow
+        const size_t a = (size_t)x * p.hit_cap + slot;
+        p.hit[2 * a] = make_float4(P.x, P.y, P.z, N.x);
+        p.hit[2 * a + 1] = make_float4(N.y, N.z, coef, __uint_as_float(b.obj));
+        p.hit_prev[a] = prev;
+      }
+      prev = x | (slot << 3);
+      const float ncoef = p.mat[RT_MAT_FLOATS_D * (size_t)b.obj + 10] * coef;  // obj.nr * coef
+      if (depth + 1 >= RT_MAX_BOUNCES) {
+        deep = !((double)ncoef < 0.01);  // cpu/rt would query again: never silent
       } else {
-        term_put(T, depth++, color_mul(local, coef));
         d = bounce_dir(d, N);
         o = P;
-        coef = m[10] * coef;
+        coef = ncoef;
       }
     }
+    wc.overflow += (uint32_t)__popcll(__ballot(deep));
+    alive = hit && depth + 1 < RT_MAX_BOUNCES;
+    ++depth;
   }
-  col acc = init_color(0.0f, 0.0f, 0.0f);
-  for (int k = depth - 1; k >= 0; --k) acc = color_add(acc, term_get(T, k));
-  return acc;
+  return prev;
 }
 
 template <int ACCEL, bool COUNT, int POL>
-__global__ __launch_bounds__(64, RT_MIN_WAVES) void render_kernel(KParams p) {
+__global__ __launch_bounds__(64, RT_TRACE_MIN_WAVES) void trace_kernel(KParams p) {
   const int lane = threadIdx.x & 63;
   WorkCount wc = {};
   // The per-lane stacks and the staged wave stack share one LDS area: a
@@ -1168,7 +1259,6 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES) void render_kernel(KParams p) {
   // empty stack (wave_sync() at both ends orders the accesses).
   __shared__ float4 s_stack[ACCEL == RT_ACCEL_FLAT_D ? 1 : kStackArea];
   __shared__ float4 s_stage[ACCEL == RT_ACCEL_FLAT_D ? kStageFlat : kStageOct];
-  __shared__ float s_terms[kLdsTerms * 3 * 64];
   const size_t gl = (size_t)blockIdx.x * 64 + (size_t)lane;
   Stack stk;
   stk.idx = (uint32_t*)s_stack;
@@ -1182,14 +1272,6 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES) void render_kernel(KParams p) {
   w.stkm = (uint64_t*)(s_stack + 2 * kStack2);
   w.stage = s_stage;
   w.lane = lane;
-  Terms T;
-  T.lds = s_terms + lane;
-  T.over = p.terms + 3 * gl;
-  T.stride = 3 * (size_t)gridDim.x * 64;
-  // Persistent waves pull the rank's tiles in scanline order from one atomic
-  // counter: all 8 XCDs then work on the same few tile rows, whose geometry
-  // stays in the Infinity Cache (measured, C5: 8 per-XCD bands ran 13 %
-  // slower).
   // Work item = (tile t, sample s): the four samples of a tile run on four
   // waves, so a tile of long mirror paths (C2: the worst tile cost 7.7x a
   // balanced schedule's whole frame, tools/tile_cost.py) is no longer one
@@ -1199,8 +1281,7 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES) void render_kernel(KParams p) {
   // tile's samples share one XCD's L2, all XCDs work on the same few tile
   // rows (their geometry stays in the Infinity Cache), and the item counters'
   // atomic traffic is split 8 ways; a drained stream's waves move on to the
-  // next.  Each item writes its sample colour; combine_kernel sums a pixel's
-  // four in the reference's order.
+  // next.  Each item writes its lanes' deepest hit records.
   const uint32_t nt = (uint32_t)p.ntiles_local;
   const uint32_t home = (uint32_t)blockIdx.x & 7u;
   uint32_t probe = 0;
@@ -1216,12 +1297,11 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES) void render_kernel(KParams p) {
     }
     const uint32_t u = 4u * (8u * (q >> 2) + x) + (q & 3u);  // item index 4t + s
     const unsigned long long c0 = COUNT ? __builtin_readcyclecounter() : 0ull;
-    const uint32_t ph0[5] = {wc.cy_cam, wc.cy_cand, wc.cy_sec, wc.cy_shadow, wc.cy_shadow_dir};
+    const uint32_t ph0[3] = {wc.cy_cam, wc.cy_cand, wc.cy_sec};
     const uint32_t t = u >> 2;
     const int smp = (int)(u & 3u);
-    const uint32_t g = t * (uint32_t)p.nranks + (uint32_t)p.rank;  // global tile index
-    const int ty = (int)(g / (uint32_t)p.tiles_x), tx = (int)(g % (uint32_t)p.tiles_x);
-    const int pr = ty * 8 + (lane >> 3), pc = tx * 8 + (lane & 7);
+    int pr, pc;
+    tile_pixel(p, t, lane, pr, pc);
     // PPM (row, col) -> framebuffer slot (j, i) of cpu/raytracer.c:71,128-134
     const int ii = p.W - pc, jj = p.H - pr;
     const bool valid = pr < p.H && pc < p.W && ii >= 1 && ii <= 2 * (p.W / 2) && jj >= 1 &&
@@ -1233,58 +1313,157 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES) void render_kernel(KParams p) {
     const float l = (float)j + 0.5f * (float)(smp & 1);
     f3 point = add(add(p.C, scale(p.u, k)), scale(p.v, l));
     f3 dir = normalize(sub(p.pos, point));
-    col sc = trace_path<ACCEL, COUNT, POL>(p, valid, point, dir, 1.0f, stk, w, wc, t, T);
-    // this item's sample colour, [item][channel][lane] (coalesced)
-    float* so = p.samples + (size_t)u * 192 + lane;
-    so[0] = sc.r;
-    so[64] = sc.g;
-    so[128] = sc.b;
+    p.last[(size_t)u * 64 + lane] =
+        trace_path<ACCEL, COUNT, POL>(p, valid, point, dir, x, stk, w, wc, t);
     if (COUNT && p.tile_cycles && lane == 0) {
-      // [0] the item's clocks, [1..5] its phase clocks (camera walk, camera
-      // candidates, secondary walks, shadows, directional shadows), planes
-      // of 4 * ntiles_local items
+      // [0] the item's clocks, [1..3] its phase clocks (camera walk, camera
+      // candidates, secondary walks), planes of 4 * ntiles_local items
       const size_t items = 4 * (size_t)p.ntiles_local;
-      const uint32_t ph1[5] = {wc.cy_cam, wc.cy_cand, wc.cy_sec, wc.cy_shadow, wc.cy_shadow_dir};
+      const uint32_t ph1[3] = {wc.cy_cam, wc.cy_cand, wc.cy_sec};
       p.tile_cycles[u] = __builtin_readcyclecounter() - c0;
 #pragma unroll
-      for (int k = 0; k < 5; k++) p.tile_cycles[u + (size_t)(k + 1) * items] = ph1[k] - ph0[k];
+      for (int k2 = 0; k2 < 3; k2++) p.tile_cycles[u + (size_t)(k2 + 1) * items] = ph1[k2] - ph0[k2];
     }
   }
-  // the counters are wave totals already: one atomic per counter per wave
-  uint32_t v[RT_NSTATS] = {wc.closest, wc.shadow,   wc.pixels,      wc.nodes,
-                           wc.tris,    wc.overflow, wc.zero_normal, wc.hits,
-                           wc.cl_nodes, wc.cl_tris, wc.sh_nodes,   wc.sh_tris,
-                           wc.cy_cam,   wc.cy_cand, wc.cy_sec,     wc.cy_shadow,
-                           wc.cy_shadow_dir, wc.stack_spills};
-#pragma unroll
-  for (int k = 0; k < RT_NSTATS; k++)
-    if (lane == 0 && v[k]) atomicAdd(p.stats + k, (unsigned long long)v[k]);
+  flush_counts(p, wc, lane);
 }
 
-// A pixel's four sample colours (render_kernel items 4t..4t+3) summed in the
-// reference's order: acc = color_add(acc, color_mul(s, 0.25)) for the samples
-// (i,j), (i,j+.5), (i+.5,j), (i+.5,j+.5) (cpu/raytracer.c:55-68); pixels
-// outside the framebuffer's even-sized area are 0.  One thread per pixel.
-__global__ __launch_bounds__(256) void combine_kernel(const float* __restrict__ samples,
-                                                      float* __restrict__ out, uint32_t ntiles,
-                                                      int W, int H, int tiles_x, int rank,
-                                                      int nranks) {
+// Per-lane LDS stack of the shadow walks only (shade_kernel, default
+// policy): (first, info) entries, no staged wave stack.
+static constexpr int kLaneStackArea = kLdsStack * 64 * 8 / 16;
+
+// apply_light (cpu/light.c:33-100) of hit record a, in two phases per block
+// of 32 lights: first the shadow queries (only the hit point is live across
+// the walks), then the Phong terms of the unshadowed lights, summed in the
+// file order of the lights as the reference does.
+template <int ACCEL, bool COUNT, int POL>
+__device__ __forceinline__ col shade_record(const KParams& p, bool valid, size_t a, Stack& s,
+                                            WaveCtx& w, WorkCount& wc, uint32_t& lit0) {
+  col acc = init_color(0.0f, 0.0f, 0.0f);
+  for (uint32_t l0 = 0; l0 < p.nlight; l0 += 32) {
+    const uint32_t l1 = p.nlight - l0 < 32u ? p.nlight : l0 + 32u;
+    uint32_t lit = 0;  // bit k: light l0 + k does not shadow the point
+    {
+      f3 P{0.0f, 0.0f, 0.0f};
+      if (valid) {
+        const float4 r0 = p.hit[2 * a];
+        P = f3{r0.x, r0.y, r0.z};
+      }
+      for (uint32_t li = l0; li < l1; li++) {
+        const float* L = p.light + RT_LIGHT_FLOATS_D * li;
+        const uint32_t type = __float_as_uint(L[0]);
+        if (type != 1 && type != 2) continue;
+        const f3 lv = f3{L[4], L[5], L[6]};
+        const uint64_t c0 = COUNT ? __builtin_readcyclecounter() : 0ull;
+        const bool sh = shadow_q<ACCEL, COUNT, POL>(p, P, shadow_dir(type, lv, P), type, valid, s, w, wc);
+        if (COUNT) {
+          const uint32_t dc = (uint32_t)(__builtin_readcyclecounter() - c0);
+          wc.cy_shadow += dc;
+          if (type == 1) wc.cy_shadow_dir += dc;
+        }
+        if (!sh) lit |= 1u << (li - l0);
+      }
+    }
+    if (l0 == 0) lit0 = lit;
+    if (!valid) continue;
+    const float4 r0 = p.hit[2 * a], r1 = p.hit[2 * a + 1];
+    const f3 P{r0.x, r0.y, r0.z}, N{r0.w, r1.x, r1.y};
+    const float* m = p.mat + RT_MAT_FLOATS_D * (size_t)__float_as_uint(r1.w);
+    for (uint32_t li = l0; li < l1; li++) {
+      const float* L = p.light + RT_LIGHT_FLOATS_D * li;
+      const uint32_t type = __float_as_uint(L[0]);
+      const col lc = init_color(L[1], L[2], L[3]);
+      if (type == 0)  // AMBIENT
+        acc = color_add(acc, color_mul2(lc, init_color(m[0], m[1], m[2])));
+      else if ((type == 1 || type == 2) && ((lit >> (li - l0)) & 1u))
+        acc = color_add(acc, light_lit(type, lc, f3{L[4], L[5], L[6]}, m, P, N));
+    }
+  }
+  return acc;
+}
+
+// shade_kernel: hit records in chunks of 64 from RT_HIT_REGIONS streams
+// (workgroup b drains region b mod 8, then steals), every lane one record:
+// cpu/light.c:33-100 with the shadow queries of cpu/light.c:24-31, then the
+// term color_mul(local, coef) of cpu/raytracer.c:30.
+template <int ACCEL, bool COUNT, int POL>
+__global__ __launch_bounds__(64, RT_SHADE_MIN_WAVES) void shade_kernel(KParams p) {
+  const int lane = threadIdx.x & 63;
+  WorkCount wc = {};
+  constexpr bool kStaged = POL == RT_POLICY_STAGED || POL == RT_POLICY_DIR_STAGED;
+  __shared__ float4 s_stack[ACCEL == RT_ACCEL_FLAT_D ? 1 : (kStaged ? kStackArea : kLaneStackArea)];
+  __shared__ float4 s_stage[ACCEL == RT_ACCEL_FLAT_D ? kStageFlat : (kStaged ? kStageOct : 1)];
+  const size_t gl = (size_t)blockIdx.x * 64 + (size_t)lane;
+  Stack stk;
+  stk.idx = (uint32_t*)s_stack;
+  stk.tt = (float*)s_stack + kLdsStack * 64;
+  stk.spill = p.spill + gl;
+  stk.stride = gridDim.x * 64u;
+  stk.lane = lane;
+  stk.sp = 0;
+  WaveCtx w;
+  w.stk2 = s_stack;
+  w.stkm = (uint64_t*)(s_stack + 2 * kStack2);
+  w.stage = s_stage;
+  w.lane = lane;
+  const uint32_t home = (uint32_t)blockIdx.x & 7u;
+  uint32_t probe = 0;
+  for (;;) {
+    const uint32_t x = (home + probe) & 7u;
+    const uint32_t hc = p.hit_count[32u * x];
+    const uint32_t n = hc < p.hit_cap ? hc : p.hit_cap;
+    const uint32_t stride = p.shade_stride > 1u ? p.shade_stride : 1u;  // verification only
+    const uint32_t ns = (n + stride - 1u) / stride;  // records shaded
+    uint32_t q = 0;
+    if (lane == 0) q = atomicAdd(p.shade_counter + 32u * x, 1u);
+    q = uni(q);
+    if (q >= (ns + 63u) / 64u) {
+      if (++probe == 8u) break;
+      continue;
+    }
+    const uint32_t k = q * 64u + (uint32_t)lane;
+    const bool valid = k < ns;
+    const size_t a = (size_t)x * p.hit_cap + (size_t)k * stride;
+    uint32_t lit = 0;
+    const col local = shade_record<ACCEL, COUNT, POL>(p, valid, a, stk, w, wc, lit);
+    if (valid) {
+      const col tm = color_mul(local, p.hit[2 * a + 1].z);  // coef
+      p.hit_term[a] = make_float4(tm.r, tm.g, tm.b, 0.0f);
+      if (p.hit_lit) p.hit_lit[a] = lit;
+    }
+  }
+  flush_counts(p, wc, lane, true);
+}
+
+// A pixel's four samples (trace_kernel items 4t..4t+3): each sample's path
+// terms summed deepest-first, acc = color_add(reflected, term)
+// (cpu/raytracer.c:29-30), then acc = color_add(acc, color_mul(s, 0.25)) over
+// the samples (i,j), (i,j+.5), (i+.5,j), (i+.5,j+.5) (cpu/raytracer.c:55-68);
+// pixels outside the framebuffer's even-sized area are 0.  One thread per
+// pixel of the rank's tile buffer.
+__global__ __launch_bounds__(256) void fold_kernel(KParams p) {
   const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= ntiles * 64u) return;
+  if (idx >= (uint32_t)p.ntiles_local * 64u) return;
   const uint32_t t = idx >> 6, lane = idx & 63u;
-  const uint32_t g = t * (uint32_t)nranks + (uint32_t)rank;
-  const int ty = (int)(g / (uint32_t)tiles_x), tx = (int)(g % (uint32_t)tiles_x);
-  const int pr = ty * 8 + (int)(lane >> 3), pc = tx * 8 + (int)(lane & 7);
-  const int ii = W - pc, jj = H - pr;
-  const bool valid = pr < H && pc < W && ii >= 1 && ii <= 2 * (W / 2) && jj >= 1 &&
-                     jj <= 2 * (H / 2);
+  int pr, pc;
+  tile_pixel(p, t, (int)lane, pr, pc);
+  const int ii = p.W - pc, jj = p.H - pr;
+  const bool valid = pr < p.H && pc < p.W && ii >= 1 && ii <= 2 * (p.W / 2) && jj >= 1 &&
+                     jj <= 2 * (p.H / 2);
   col acc = init_color(0.0f, 0.0f, 0.0f);
   for (int smp = 0; smp < 4; smp++) {
-    const float* si = samples + ((size_t)t * 4 + (size_t)smp) * 192 + lane;
-    acc = color_add(acc, color_mul(col{si[0], si[64], si[128]}, 0.25f));
+    col sc = init_color(0.0f, 0.0f, 0.0f);
+    uint32_t r = p.last[((size_t)t * 4 + (size_t)smp) * 64 + lane];
+    while (r != RT_NO_REC && (r >> 3) < p.hit_cap) {
+      const size_t a = rec_addr(p, r);
+      const float4 tm = p.hit_term[a];
+      sc = color_add(sc, col{tm.x, tm.y, tm.z});
+      r = p.hit_prev[a];
+    }
+    acc = color_add(acc, color_mul(sc, 0.25f));
   }
   if (!valid) acc = col{0.0f, 0.0f, 0.0f};
-  float* o = out + (size_t)idx * 3;
+  float* o = p.out + (size_t)idx * 3;
   o[0] = acc.r;
   o[1] = acc.g;
   o[2] = acc.b;
@@ -1458,11 +1637,7 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES) void compat_kernel(KParams p) {
       img[(size_t)py * (size_t)p.W + (size_t)px] = (uint32_t)color.r | ((uint32_t)color.g << 8) |
                                                    ((uint32_t)color.b << 16) | 0xff000000u;
   }
-  uint32_t v[RT_NSTATS] = {wc.closest, wc.shadow, wc.pixels, wc.nodes, wc.tris, wc.overflow,
-                           wc.zero_normal, wc.hits};
-#pragma unroll
-  for (int k = 0; k < RT_NSTATS; k++)
-    if (lane == 0 && v[k]) atomicAdd(p.stats + k, (unsigned long long)v[k]);
+  flush_counts(p, wc, lane);
 }
 
 // gpu/raytracer.cu:48-85: output pixel (row R, column c) of the W x H image
@@ -1497,8 +1672,10 @@ __global__ __launch_bounds__(256) void assemble_kernel(const float* __restrict__
   size_t npx = (size_t)W * (size_t)H;
   if (idx >= npx) return;
   int row = (int)(idx / (size_t)W), col = (int)(idx % (size_t)W);
-  int g = (row >> 3) * tiles_x + (col >> 3);
-  int rank = g % nranks, local = g / nranks;
+  uint32_t rank;
+  const int tb = rt_block_side(nranks);
+  const uint32_t local = rt_tile_local(col >> 3, row >> 3, (uint32_t)nranks,
+                                       (uint32_t)rt_blocks_x(tiles_x, tb), (uint32_t)tb, &rank);
   int lane = ((row & 7) << 3) | (col & 7);
   const float* src = tiles + (((size_t)rank * tiles_per_rank + local) * 64 + lane) * 3;
   rgb[3 * idx + 0] = src[0];
@@ -1510,51 +1687,73 @@ __global__ __launch_bounds__(256) void assemble_kernel(const float* __restrict__
 }  // namespace rt
 
 // ---------------------------------------------------------------- launchers
-// One instantiation per (accel, work counting, policy); the default policy's
-// kernel has no policy switch inside.  The work-counting pass and the test
-// policies are separate kernels, so they cannot slow the default one down.
-static hipError_t launch_combine(const KParams* p, hipStream_t stream) {
-  const uint32_t n = (uint32_t)p->ntiles_local * 64u;
-  if (n == 0) return hipGetLastError();
-  hipLaunchKernelGGL(rt::combine_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, p->samples,
-                     p->out, (uint32_t)p->ntiles_local, p->W, p->H, p->tiles_x, p->rank, p->nranks);
-  return hipGetLastError();
+// One instantiation per (kernel, accel, work counting, policy); the default
+// policy's kernels have no policy switch inside.  The work-counting pass and
+// the test policies are separate kernels, so they cannot slow the default
+// ones down.
+// The instantiation of (kernel, accel, counting, policy).  Policies only
+// differ in the walks they use: trace has no shadow queries (policy 3 =
+// default there), shade has no closest-hit queries (policy 1 = default).
+template <bool TRACE>
+static const void* kernel_of(int accel, int count_work, int policy) {
+  using namespace rt;
+  if (accel == RT_ACCEL_FLAT_D) {
+    if (TRACE)
+      return count_work ? (const void*)trace_kernel<RT_ACCEL_FLAT_D, true, 0>
+                        : (const void*)trace_kernel<RT_ACCEL_FLAT_D, false, 0>;
+    return count_work ? (const void*)shade_kernel<RT_ACCEL_FLAT_D, true, 0>
+                      : (const void*)shade_kernel<RT_ACCEL_FLAT_D, false, 0>;
+  }
+  if (TRACE) {
+    if (policy == RT_POLICY_LANE) return (const void*)trace_kernel<RT_ACCEL_OCTREE_D, false, RT_POLICY_LANE>;
+    if (policy == RT_POLICY_STAGED)
+      return (const void*)trace_kernel<RT_ACCEL_OCTREE_D, false, RT_POLICY_STAGED>;
+    return count_work ? (const void*)trace_kernel<RT_ACCEL_OCTREE_D, true, RT_POLICY_DEFAULT>
+                      : (const void*)trace_kernel<RT_ACCEL_OCTREE_D, false, RT_POLICY_DEFAULT>;
+  }
+  if (policy == RT_POLICY_STAGED) return (const void*)shade_kernel<RT_ACCEL_OCTREE_D, false, RT_POLICY_STAGED>;
+  if (policy == RT_POLICY_DIR_STAGED)
+    return (const void*)shade_kernel<RT_ACCEL_OCTREE_D, false, RT_POLICY_DIR_STAGED>;
+  return count_work ? (const void*)shade_kernel<RT_ACCEL_OCTREE_D, true, RT_POLICY_DEFAULT>
+                    : (const void*)shade_kernel<RT_ACCEL_OCTREE_D, false, RT_POLICY_DEFAULT>;
 }
 
-extern "C" hipError_t rt_launch_render(const KParams* p, int accel, int count_work, int policy,
-                                       int grid, hipStream_t stream) {
-  dim3 g(grid), b(64);
-  if (accel == RT_ACCEL_FLAT_D) {
-    if (count_work)
-      hipLaunchKernelGGL((rt::render_kernel<RT_ACCEL_FLAT_D, true, 0>), g, b, 0, stream, *p);
-    else
-      hipLaunchKernelGGL((rt::render_kernel<RT_ACCEL_FLAT_D, false, 0>), g, b, 0, stream, *p);
-    hipError_t e = hipGetLastError();
-    return e != hipSuccess ? e : launch_combine(p, stream);
-  }
-  switch (policy) {
-    case RT_POLICY_LANE:
-      hipLaunchKernelGGL((rt::render_kernel<RT_ACCEL_OCTREE_D, false, RT_POLICY_LANE>), g, b, 0,
-                         stream, *p);
-      break;
-    case RT_POLICY_STAGED:
-      hipLaunchKernelGGL((rt::render_kernel<RT_ACCEL_OCTREE_D, false, RT_POLICY_STAGED>), g, b, 0,
-                         stream, *p);
-      break;
-    case RT_POLICY_DIR_STAGED:
-      hipLaunchKernelGGL((rt::render_kernel<RT_ACCEL_OCTREE_D, false, RT_POLICY_DIR_STAGED>), g, b,
-                         0, stream, *p);
-      break;
-    default:
-      if (count_work)
-        hipLaunchKernelGGL((rt::render_kernel<RT_ACCEL_OCTREE_D, true, RT_POLICY_DEFAULT>), g, b, 0,
-                           stream, *p);
-      else
-        hipLaunchKernelGGL((rt::render_kernel<RT_ACCEL_OCTREE_D, false, RT_POLICY_DEFAULT>), g, b, 0,
-                           stream, *p);
-  }
-  hipError_t e = hipGetLastError();
-  return e != hipSuccess ? e : launch_combine(p, stream);
+// Persistent grid of a kernel: as many one-wave workgroups as the kernel's
+// registers and LDS let every CU hold (the occupancy API), so every SIMD is
+// filled and no workgroup waits for a slot.
+extern "C" hipError_t rt_render_grid(int trace, int accel, int count_work, int policy, int cus,
+                                     int* grid) {
+  const void* k = trace ? kernel_of<true>(accel, count_work, policy)
+                        : kernel_of<false>(accel, count_work, policy);
+  int per_cu = 0;
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 64, 0);
+  if (e != hipSuccess) return e;
+  if (per_cu < 1) per_cu = 1;
+  if (per_cu > 32) per_cu = 32;
+  *grid = per_cu * cus;
+  return hipSuccess;
+}
+
+static hipError_t launch_kernel(const void* k, int grid, const KParams* p, hipStream_t stream) {
+  void* args[] = {(void*)p};
+  return hipLaunchKernel(k, dim3(grid), dim3(64), args, 0, stream);
+}
+
+extern "C" hipError_t rt_launch_trace(const KParams* p, int accel, int count_work, int policy,
+                                      int grid, hipStream_t stream) {
+  return launch_kernel(kernel_of<true>(accel, count_work, policy), grid, p, stream);
+}
+
+extern "C" hipError_t rt_launch_shade(const KParams* p, int accel, int count_work, int policy,
+                                      int grid, hipStream_t stream) {
+  return launch_kernel(kernel_of<false>(accel, count_work, policy), grid, p, stream);
+}
+
+extern "C" hipError_t rt_launch_fold(const KParams* p, hipStream_t stream) {
+  const uint32_t n = (uint32_t)p->ntiles_local * 64u;
+  if (n == 0) return hipGetLastError();
+  hipLaunchKernelGGL(rt::fold_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, *p);
+  return hipGetLastError();
 }
 
 extern "C" hipError_t rt_launch_assemble(const float* tiles, float* rgb, int W, int H, int tiles_x,

@@ -517,6 +517,77 @@ static int build_octree(const oct_input *in, size_t ntri, const dbox *root, oct_
 
 /* -------------------------------------------------------------- flatten */
 
+/* Squared distance from the origin to the triangle (a, b, c), in double
+ * (closest point by Voronoi regions, Ericson, Real-Time Collision Detection
+ * 5.1.5). */
+static double origin_tri_dist2(const double a[3], const double b[3], const double c[3])
+{
+  double ab[3], ac[3], ap[3], bp[3], cp[3], q[3];
+  for (int k = 0; k < 3; k++)
+  {
+    ab[k] = b[k] - a[k];
+    ac[k] = c[k] - a[k];
+    ap[k] = -a[k];
+    bp[k] = -b[k];
+    cp[k] = -c[k];
+  }
+#define DOT3(x, y) ((x)[0] * (y)[0] + (x)[1] * (y)[1] + (x)[2] * (y)[2])
+  double d1 = DOT3(ab, ap), d2 = DOT3(ac, ap);
+  if (d1 <= 0 && d2 <= 0)
+    return DOT3(a, a);
+  double d3 = DOT3(ab, bp), d4 = DOT3(ac, bp);
+  if (d3 >= 0 && d4 <= d3)
+    return DOT3(b, b);
+  double vc = d1 * d4 - d3 * d2;
+  if (vc <= 0 && d1 >= 0 && d3 <= 0)
+  {
+    double v = d1 / (d1 - d3);
+    for (int k = 0; k < 3; k++) q[k] = a[k] + v * ab[k];
+    return DOT3(q, q);
+  }
+  double d5 = DOT3(ab, cp), d6 = DOT3(ac, cp);
+  if (d6 >= 0 && d5 <= d6)
+    return DOT3(c, c);
+  double vb = d5 * d2 - d1 * d6;
+  if (vb <= 0 && d2 >= 0 && d6 <= 0)
+  {
+    double w = d2 / (d2 - d6);
+    for (int k = 0; k < 3; k++) q[k] = a[k] + w * ac[k];
+    return DOT3(q, q);
+  }
+  double va = d3 * d6 - d5 * d4;
+  if (va <= 0 && (d4 - d3) >= 0 && (d5 - d6) >= 0)
+  {
+    double w = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+    for (int k = 0; k < 3; k++) q[k] = b[k] + w * (c[k] - b[k]);
+    return DOT3(q, q);
+  }
+  double den = 1.0 / (va + vb + vc);
+  double v = vb * den, w = vc * den;
+  for (int k = 0; k < 3; k++) q[k] = a[k] + ab[k] * v + ac[k] * w;
+  return DOT3(q, q);
+#undef DOT3
+}
+
+/* Can the reference's interpolated normal (n0'(1-u-v) + n1' u) + n2' v of
+ * this triangle (cpu/hit.c:38-40, nk' = the normalised vertex normals) be
+ * exactly zero for some accepted (u, v)?  Only if 0 lies in (or within float
+ * rounding of) the triangle the three unit normals span: each component is
+ * a sum of three products of magnitude <= 1, rounded to a few 2^-24, and u,
+ * v, 1-u-v may stray a few ulps outside [0, 1].  Distance < 1e-5 = "can". A
+ * NaN normal (normalize of a zero vn) stays NaN, never zero. */
+int rt_tri_normal_can_vanish(const float *nrm9)
+{
+  double n[3][3];
+  for (int k = 0; k < 9; k++)
+  {
+    if (isnan(nrm9[k]))
+      return 0;
+    n[k / 3][k % 3] = nrm9[k];
+  }
+  return origin_tri_dist2(n[0], n[1], n[2]) < 1e-10;
+}
+
 int rt_flatten(const rt_scene *s, int accel, rt_flat_scene *out)
 {
   memset(out, 0, sizeof *out);
@@ -583,6 +654,20 @@ int rt_flatten(const rt_scene *s, int accel, rt_flat_scene *out)
         if (pb[3 + a] > out->scene_hi[a]) out->scene_hi[a] = pb[3 + a];
       }
     }
+  }
+  /* record flag RT_REC_ZERO_RISK on every triangle of an object that holds
+   * a triangle whose interpolated normal can vanish (cpu/hit.c:79,99 skip
+   * such an object when its closest triangle interpolates exactly zero) */
+  for (size_t o = 0, p0 = 0; o < s->object_count; o++)
+  {
+    size_t n = s->objects[o].triangle_count;
+    int risk = 0;
+    for (size_t k = 0; k < n && !risk; k++)
+      risk = rt_tri_normal_can_vanish(out->nrm + 9 * (p0 + k));
+    if (risk)
+      for (size_t k = 0; k < n; k++)
+        rec[RT_TRI_FLOATS * (p0 + k) + 11] = u2f(RT_REC_ZERO_RISK_BIT);
+    p0 += n;
   }
   for (size_t i = 0; i < s->light_count; i++)
   {

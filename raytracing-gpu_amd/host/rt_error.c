@@ -17,9 +17,11 @@ const char *rt_strerror(int code)
   case RT_ENOMEM: return "out of host memory";
   case RT_EHIP: return "HIP runtime error";
   case RT_ENODEV: return "no usable gfx950 device";
-  case RT_EDEPTH: return "reflection depth buffer overflow";
+  case RT_EDEPTH: return "reflection depth or traversal stack overflow";
   case RT_ERCCL: return "RCCL error";
-  case RT_EZERONORMAL: return "zero interpolated normal (cpu/hit.c:79 not reproduced)";
+  case RT_EZERONORMAL: return "zero interpolated normal (cpu/hit.c:79,99 not reproduced)";
+  case RT_EHITBUF: return "hit-record buffer overflow (grown; render again)";
+  case RT_EINEXACT: return "inexact tuning knob active (cpu/rt parity not guaranteed)";
   default: return "unknown error";
   }
 }

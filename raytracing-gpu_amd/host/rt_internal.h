@@ -27,7 +27,9 @@ rt_vec3 rt_v_normalize(rt_vec3 a);
  * Triangle record (48 B, 3 x float4), in traversal order:
  *   q0 = v0.x v0.y v0.z e1.x
  *   q1 = e1.y e1.z e2.x e2.y
- *   q2 = e2.z  bits(prim)  bits(object)  0
+ *   q2 = e2.z  bits(prim)  bits(object)  flags
+ * flags bit 0 (RT_REC_ZERO_RISK_BIT): the object has a triangle whose
+ * interpolated normal can be exactly zero (rt_tri_normal_can_vanish).
  * prim = global triangle index in (object, LIFO triangle) order, which is the
  * tie-break key of cpu/hit.c:59,82.  e1/e2 are the
  * exact subtractions cpu/hit.c:16-17 performs.
@@ -59,7 +61,10 @@ typedef struct rt_flat_scene {
 #define RT_LIGHT_FLOATS 8
 
 
+#define RT_REC_ZERO_RISK_BIT 1u /* = RT_REC_ZERO_RISK of csrc/rt_kernels.h */
+
 int rt_flatten(const rt_scene *scene, int accel, rt_flat_scene *out);
+int rt_tri_normal_can_vanish(const float *nrm9);
 void rt_flat_free(rt_flat_scene *f);
 int rt_flat_validate(const rt_flat_scene *f);
 

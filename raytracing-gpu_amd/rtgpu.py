@@ -92,7 +92,10 @@ class Stats(C.Structure):
                 ("shadow_node_lanes", C.c_ulonglong), ("shadow_tri_lanes", C.c_ulonglong),
                 ("cycles_camera", C.c_ulonglong), ("cycles_cand", C.c_ulonglong),
                 ("cycles_secondary", C.c_ulonglong), ("cycles_shadow", C.c_ulonglong),
-                ("cycles_shadow_directional", C.c_ulonglong), ("stack_spills", C.c_ulonglong)]
+                ("cycles_shadow_directional", C.c_ulonglong), ("stack_spills", C.c_ulonglong),
+                ("shadow_zero_risk", C.c_ulonglong), ("hit_records", C.c_ulonglong),
+                ("shadow_node_visits", C.c_ulonglong), ("shadow_tri_tests", C.c_ulonglong),
+                ("shadow_unproven", C.c_ulonglong)]
 
     def as_dict(self):
         return {k: int(getattr(self, k)) for k, _ in self._fields_}
@@ -103,7 +106,8 @@ class AccelInfo(C.Structure):
                 ("nodes", C.c_ulonglong), ("leaves", C.c_ulonglong), ("max_depth", C.c_ulonglong),
                 ("tri_record_bytes", C.c_ulonglong), ("node_record_bytes", C.c_ulonglong),
                 ("device_bytes", C.c_ulonglong), ("build_seconds", C.c_double),
-                ("max_leaf", C.c_ulonglong)]
+                ("max_leaf", C.c_ulonglong), ("shadow_global", C.c_ulonglong),
+                ("shadow_mu_max", C.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -146,6 +150,7 @@ _PROTOS = [
     ("rt_hip_set_camera_slack", C.c_int, [C.c_void_p, C.c_float]),
     ("rt_hip_cand_verify", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
     ("rt_hip_cand_tile_entries", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
+    ("rt_hip_verify_shadows", C.c_int, [C.c_void_p, C.c_uint, C.POINTER(C.c_ulonglong)]),
     ("rt_hip_set_exact_camera", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_set_policy", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_tile_cycles", C.c_int, [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_size_t]),
@@ -154,6 +159,8 @@ _PROTOS = [
     ("rt_hip_set_timing", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_frame_times", C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_float),
                                      C.POINTER(C.c_float)]),
+    ("rt_hip_frame_kernel_times", C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_float),
+                                            C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     ("rt_hip_set_camera_bound_scale", C.c_int, [C.c_void_p, C.c_double]),
     ("rt_cand_survey", C.c_int, [C.POINTER(SceneStruct), C.c_float, C.c_double, C.c_int, C.c_int,
                                  C.POINTER(C.c_ulonglong)]),
@@ -396,6 +403,12 @@ class Context:
         _check(lib().rt_hip_frame_times(self.h, n, a, b), "frame_times")
         return list(zip(a, b))
 
+    def kernel_times(self, n=1):
+        """[(trace_ms, shade_ms, fold_ms)] of the last n timed renders, oldest first."""
+        a, b, c = (C.c_float * n)(), (C.c_float * n)(), (C.c_float * n)()
+        _check(lib().rt_hip_frame_kernel_times(self.h, n, a, b, c), "frame_kernel_times")
+        return list(zip(a, b, c))
+
     def tile_cycles(self, n):
         """Per-tile shader clocks of the last instrumented render (numpy uint64)."""
         out = np.zeros(n, dtype=np.uint64)
@@ -429,6 +442,14 @@ class Context:
         _check(lib().rt_hip_cand_verify(self.h, C.byref(frame), rank, nranks, out), "cand_verify")
         return dict(zip(("listed", "entries", "fp_mismatch", "tile_mismatch", "global",
                          "filter_violation", "filtered"), (int(x) for x in out)))
+
+    def verify_shadows(self, stride=1):
+        """Shadow outcomes of the last render's hit records (every stride-th
+        per region): the walk vs brute force (rt_hip_verify_shadows)."""
+        out = (C.c_ulonglong * 4)()
+        _check(lib().rt_hip_verify_shadows(self.h, stride, out), "verify_shadows")
+        return dict(zip(("records", "queries", "records_differ", "walk_lit_brute_shadowed"),
+                        (int(x) for x in out)))
 
     def cand_tile_entries(self, ntiles):
         """Candidate-list entries per rank-local tile of the last render."""
@@ -516,17 +537,67 @@ def raytrace(input_path, output_path, gpus=1, accel=None):
     return st.as_dict(), ms.value
 
 
+# ---- tile map (host mirror of csrc/rt_tiles.h) ----
+def block_side(nranks):
+    """Tiles per block side: rank r owns blocks b = r, r + nranks, ... (scanline
+    order); 4 when the frame is split, 1 (plain scanline tiles) for one rank."""
+    return 4 if nranks > 1 else 1
+
+
+def _blocks(width, height, nranks):
+    tb = block_side(nranks)
+    tx, ty = (width + 7) // 8, (height + 7) // 8
+    return tb, -(-tx // tb), -(-ty // tb)
+
+
+def rank_tile_count(width, height, rank, nranks):
+    """Tiles (whole blocks, edge padding included) rank `rank` renders."""
+    tb, bx, by = _blocks(width, height, nranks)
+    nb = bx * by
+    return ((nb - rank + nranks - 1) // nranks if nb > rank else 0) * tb * tb
+
+
+def tiles_per_rank_host(width, height, nranks):
+    return rank_tile_count(width, height, 0, nranks)
+
+
+def tile_xy(t, rank, nranks, width, height):
+    """(tx, ty) of rank-local tiles t (numpy arrays) of rank `rank`."""
+    tb, bx, _ = _blocks(width, height, nranks)
+    t = np.asarray(t)
+    b = (t // (tb * tb)) * nranks + rank
+    k = t % (tb * tb)
+    return (b % bx) * tb + k % tb, (b // bx) * tb + k // tb
+
+
+def tile_local(tx, ty, nranks, width, height):
+    """(rank, local index) of tiles (tx, ty) (numpy arrays)."""
+    tb, bx, _ = _blocks(width, height, nranks)
+    b = (np.asarray(ty) // tb) * bx + np.asarray(tx) // tb
+    return b % nranks, (b // nranks) * (tb * tb) + (np.asarray(ty) % tb) * tb + np.asarray(tx) % tb
+
+
+def tile_pixels(width, height, rank, nranks):
+    """(tiles, 64, 2) PPM (row, col) of the rank's tile-buffer slots, -1 where
+    the slot is padding (past the frame's edge)."""
+    n = rank_tile_count(width, height, rank, nranks)
+    tx, ty = tile_xy(np.arange(n), rank, nranks, width, height)
+    lane = np.arange(64)
+    r = ty[:, None] * 8 + (lane // 8)[None, :]
+    c = tx[:, None] * 8 + (lane % 8)[None, :]
+    bad = (r >= height) | (c >= width)
+    return np.stack([np.where(bad, -1, r), np.where(bad, -1, c)], axis=2)
+
+
 def assemble_tiles_numpy(gathered, width, height, nranks):
     """Host mirror of the assemble kernel's index map (for CPU tests of the
     tiling / gather layout): gathered = nranks x tiles_per_rank x 64 x 3."""
-    tpr = tiles_per_rank(width, height, nranks) if _lib is not None else \
-        -(-(((width + 7) // 8) * ((height + 7) // 8)) // nranks)
+    tpr = tiles_per_rank_host(width, height, nranks)
     g = np.asarray(gathered, np.float32).reshape(nranks, tpr, 64, 3)
-    tx = (width + 7) // 8
     rows, cols = np.mgrid[0:height, 0:width]
-    t = (rows // 8) * tx + (cols // 8)
+    rk, loc = tile_local(cols // 8, rows // 8, nranks, width, height)
     lane = (rows % 8) * 8 + (cols % 8)
-    return g[t % nranks, t // nranks, lane]
+    return g[rk, loc, lane]
 
 
 def tiles_from_image_numpy(img, rank, nranks):
@@ -534,17 +605,9 @@ def tiles_from_image_numpy(img, rank, nranks):
     (tiles_per_rank x 64 x 3, zero-padded) cut from a full (H, W, 3) image."""
     img = np.asarray(img, np.float32)
     height, width, _ = img.shape
-    tx, ty = (width + 7) // 8, (height + 7) // 8
-    nt = tx * ty
-    tpr = -(-nt // nranks)
+    tpr = tiles_per_rank_host(width, height, nranks)
     out = np.zeros((tpr, 64, 3), np.float32)
-    for local in range(tpr):
-        g = local * nranks + rank
-        if g >= nt:
-            break
-        r0, c0 = (g // tx) * 8, (g % tx) * 8
-        blk = np.zeros((8, 8, 3), np.float32)
-        sub = img[r0:r0 + 8, c0:c0 + 8]
-        blk[:sub.shape[0], :sub.shape[1]] = sub
-        out[local] = blk.reshape(64, 3)
+    pix = tile_pixels(width, height, rank, nranks)
+    ok = pix[..., 0] >= 0
+    out[: len(pix)][ok] = img[pix[..., 0][ok], pix[..., 1][ok]]
     return out

@@ -1,7 +1,8 @@
 """Multi-rank path on CPU (gloo, world_size 2 and 3): each rank produces the
-tile buffer the renderer writes for it (tile t -> rank t % N), rank 0 gathers
-them rank-major exactly as bench.py does with RCCL, and the assemble index map
-(mirrored from the HIP assemble kernel) restores the PPM-order image."""
+tile buffer the renderer writes for it (4x4-tile blocks, block b -> rank b %
+N, csrc/rt_tiles.h), rank 0 gathers them rank-major exactly as bench.py does
+with RCCL, and the assemble index map (mirrored from the HIP assemble kernel)
+restores the PPM-order image."""
 import os
 import socket
 import sys
@@ -70,3 +71,31 @@ def test_tile_ownership_is_a_partition():
                     owned[g] += 1
         assert (owned == 1).all()
         assert tpr * n >= nt
+
+
+@pytest.mark.parametrize("W,H,n", [(96, 54, 2), (96, 54, 3), (192, 108, 8), (3840, 2160, 8),
+                                   (3840, 2160, 7), (1920, 1080, 3), (40, 24, 5)])
+def test_tile_map_partitions_the_frame(built, W, H, n):
+    """Every pixel belongs to exactly one (rank, tile-buffer slot); the host
+    mirror's sizes agree with the library's (rt_hip_tiles_per_rank); every
+    rank holds close to 1/n of the tiles (whole blocks)."""
+    sys.path.insert(0, os.path.join(REPO, "raytracing-gpu_amd"))
+    import rtgpu
+    tpr = rtgpu.tiles_per_rank(W, H, n)
+    assert tpr == rtgpu.tiles_per_rank_host(W, H, n)
+    seen = np.zeros((H, W), np.int32)
+    counts = []
+    for r in range(n):
+        pix = rtgpu.tile_pixels(W, H, r, n)
+        assert len(pix) <= tpr
+        ok = pix[..., 0] >= 0
+        np.add.at(seen, (pix[..., 0][ok], pix[..., 1][ok]), 1)
+        counts.append(int(ok.sum()))
+        tx, ty = rtgpu.tile_xy(np.arange(len(pix)), r, n, W, H)
+        rk, loc = rtgpu.tile_local(tx, ty, n, W, H)
+        assert (rk == r).all() and (loc == np.arange(len(pix))).all()
+    assert (seen == 1).all()
+    assert max(counts) - min(counts) <= 32 * 32 * (1 + (W * H) // (32 * 32 * n * 8))
+    img = np.random.default_rng(1).random((H, W, 3), dtype=np.float32)
+    g = np.stack([rtgpu.tiles_from_image_numpy(img, r, n) for r in range(n)])
+    assert np.array_equal(rtgpu.assemble_tiles_numpy(g, W, H, n), img)

@@ -9,7 +9,7 @@ ranks `--ranks` of an `--nranks`-way interleaved split, i.e. every nranks-th
 gpurun_out/c5_exact_<tag>.json with every differing pixel (both values), the
 octree frame time and the optional culling-slack sweep.
 
-    python tools/c5_exact.py --grid 32 --tris 9766 --W 3840 --H 2160 --nranks 64 --ranks 0
+    python tools/c5_exact.py --grid 32 --tris 9776 --W 3840 --H 2160 --nranks 64 --ranks 0
 """
 import argparse
 import ctypes as C
@@ -43,24 +43,13 @@ def render_rank(ctx, f, rank, nranks):
 
 def tile_pixels(f, rank, nranks):
     """(tiles, 64, 2) PPM (row, col) of the rank's tile buffer slots (-1 = pad)."""
-    tx, ty = (f.width + 7) // 8, (f.height + 7) // 8
-    nt = tx * ty
-    tpr = -(-nt // nranks)
-    loc = np.arange(tpr)
-    g = loc * nranks + rank
-    lane = np.arange(64)
-    r = (g // tx)[:, None] * 8 + (lane // 8)[None, :]
-    c = (g % tx)[:, None] * 8 + (lane % 8)[None, :]
-    bad = (g >= nt)[:, None] | (r >= f.height) | (c >= f.width)
-    r = np.where(bad, -1, r)
-    c = np.where(bad, -1, c)
-    return np.stack([r, c], axis=2)
+    return rtgpu.tile_pixels(f.width, f.height, rank, nranks)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--grid", type=int, default=32)
-    ap.add_argument("--tris", type=int, default=9766)
+    ap.add_argument("--tris", type=int, default=9776)
     ap.add_argument("--W", type=int, default=3840)
     ap.add_argument("--H", type=int, default=2160)
     ap.add_argument("--accel", default="octree_gpu")
@@ -104,7 +93,13 @@ def main():
         tn.append(time.perf_counter() - t)
     ctx.set_exact_camera(True)
     log(f"{a.accel} without candidate lists: {min(tn) * 1e3:.2f} ms")
-    ranks = [int(x) for x in a.ranks.split(",") if x != ""]
+    ranks = []
+    for x in a.ranks.split(","):  # "0,5,9" or ranges "0-127"
+        if "-" in x:
+            lo, hi = (int(y) for y in x.split("-"))
+            ranks.extend(range(lo, hi + 1))
+        elif x != "":
+            ranks.append(int(x))
     flat = rtgpu.Context(s, "flat")
     out = {"grid": a.grid, "tris": s.triangle_count, "W": a.W, "H": a.H, "accel": a.accel,
            "nranks": a.nranks, "ranks": ranks, "octree_ms": min(times) * 1e3, "octree_stats": st,
@@ -123,6 +118,7 @@ def main():
         tf, stf = render_rank(flat, f, r, a.nranks)
         el = time.perf_counter() - t
         pix = tile_pixels(f, r, a.nranks)
+        tf = tf[: len(pix)]
         ok = pix[..., 0] >= 0
         pr, pc = pix[..., 0][ok], pix[..., 1][ok]
         vf = tf[ok]
@@ -139,14 +135,21 @@ def main():
         for k in np.flatnonzero(d):
             out["differ"].append({"r": int(pr[k]), "c": int(pc[k]), "flat": vf[k].tolist(),
                                   "octree": vo[k].tolist()})
+        if r % 8 == 7 or r == ranks[-1]:  # partial results survive a cut-off run
+            _dump(out, a.tag)
         for sl, (im, el2) in imgs.items():
             ds = (vf.view(np.uint32) != im[pr, pc].view(np.uint32)).any(axis=1)
             out["slack_sweep"].append({"rank": r, "slack": sl, "ms": el2 * 1e3, "differ": int(ds.sum())})
             log(f"  slack {sl}: {el2 * 1e3:.1f} ms, {int(ds.sum())} differ")
+    _dump(out, a.tag)
+    log(json.dumps({k: v for k, v in out.items() if k not in ("differ", "octree_stats")}))
+
+
+def _dump(out, tag):
+    out["differ_count"] = len(out["differ"])
     os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
-    with open(os.path.join(REPO, "gpurun_out", f"c5_exact_{a.tag}.json"), "w") as fo:
+    with open(os.path.join(REPO, "gpurun_out", f"c5_exact_{tag}.json"), "w") as fo:
         json.dump(out, fo, indent=1)
-    log(json.dumps({k: v for k, v in out.items() if k != "differ"}))
 
 
 _buf = {}

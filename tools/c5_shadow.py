@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""Shadow queries of the headline frame, walk vs brute force (not part of
+the product): renders C5 (octree_gpu), then rt_hip_verify_shadows shades
+every stride-th hit record again through the shadow walk and by brute force
+over all 10M triangles (cpu/hit.c:93-109) and compares each record's
+per-light outcome.  Writes gpurun_out/c5_shadow_<tag>.json.
+
+    python tools/c5_shadow.py --stride 16 [--policy 0]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "raytracing-gpu_amd"))
+import rtgpu  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--grid", type=int, default=32)
+    ap.add_argument("--W", type=int, default=3840)
+    ap.add_argument("--H", type=int, default=2160)
+    ap.add_argument("--stride", type=int, default=16)
+    ap.add_argument("--policy", type=int, default=0)
+    ap.add_argument("--tag", default="c5")
+    a = ap.parse_args()
+    s = rtgpu.Scene.synthetic(a.grid, a.grid, 9776, seed=0x5EED, width=a.W, height=a.H)
+    ctx = rtgpu.Context(s, "octree_gpu")
+    ctx.set_policy(a.policy)
+    info = ctx.info()
+    img, st = ctx.render_image(s.frame())
+    t = time.perf_counter()
+    v = ctx.verify_shadows(a.stride)
+    out = {"scene_triangles": s.triangle_count, "W": a.W, "H": a.H, "stride": a.stride,
+           "policy": a.policy, "shadow_queries_in_frame": st["shadow"],
+           "hit_records_in_frame": st["hit_records"], "shadow_global_prims": info["shadow_global"],
+           "shadow_mu_max": info["shadow_mu_max"], "verify_seconds": time.perf_counter() - t, **v}
+    print(json.dumps(out), flush=True)
+    os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(REPO, "gpurun_out", f"c5_shadow_{a.tag}.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -43,14 +43,15 @@ def main():
     ctx.set_count_work(True)
     f = s.frame()
     img, st = ctx.render_image(f)
-    tx, ty = (a.W + 7) // 8, (a.H + 7) // 8
-    items = ctx.tile_cycles(4 * tx * ty).astype(np.float64)  # item 4t + s = (tile t, sample s)
+    nt = rtgpu.rank_tile_count(a.W, a.H, 0, 1)  # rank-local tiles (csrc/rt_tiles.h order)
+    txs, tys = rtgpu.tile_xy(np.arange(nt), 0, 1, a.W, a.H)
+    items = ctx.tile_cycles(4 * nt).astype(np.float64)  # item 4t + s = (tile t, sample s)
     c = items.reshape(-1, 4).sum(axis=1)
-    ph = {name: ctx.tile_phase_cycles(k, 4 * tx * ty).astype(np.float64)
-          for k, name in enumerate(("total", "camera_walk", "candidates", "secondary", "shadow",
-                                    "shadow_dir")) if k}
+    # trace kernel phases (shadow queries run in the shade kernel, not per item)
+    ph = {name: ctx.tile_phase_cycles(k, 4 * nt).astype(np.float64)
+          for k, name in enumerate(("total", "camera_walk", "candidates", "secondary")) if k}
     try:
-        ent = ctx.cand_tile_entries(tx * ty).astype(np.float64)
+        ent = ctx.cand_tile_entries(nt).astype(np.float64)
     except rtgpu.RtError:
         ent = None
     order = np.argsort(-c)
@@ -64,7 +65,7 @@ def main():
         # expensive work item (one sample of a tile), nor before total / 4096
         "max_item": items.max(),
         "bound_tail_over_balanced": items.max() / (tot / 4096.0),
-        "worst_tiles_rc": [[int(i // tx), int(i % tx)] for i in order[:10]],
+        "worst_tiles_rc": [[int(tys[i]) * 8, int(txs[i]) * 8] for i in order[:10]],
         "worst_items_cycles": [float(x) for x in np.sort(items)[::-1][:10]],
         # phase clocks of the 10 most expensive items and the mean item
         "worst_items_phases": [{k: float(ph[k][i]) for k in ph} for i in np.argsort(-items)[:10]],
