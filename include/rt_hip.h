@@ -156,13 +156,17 @@ size_t rt_hip_tile_buffer_floats(int width, int height, int nranks);
  * (a hipStream_t; NULL = the context's stream). */
 int rt_hip_render(rt_hip_ctx *ctx, const rt_frame *frame, int rank, int nranks, float *d_tiles,
                   void *stream);
-/* Waits for the last render and returns its counters. */
+/* Waits for the last render and returns its counters.  The counters are
+ * filled in whatever the return code: RT_EHITBUF (render again),
+ * RT_EDEPTH / RT_EZERONORMAL (the image may differ from cpu/rt's there),
+ * RT_EINEXACT (a parity-breaking tuning knob below was active, or a
+ * point-light shadow ray left from beyond the proven extent). */
 int rt_hip_stats(rt_hip_ctx *ctx, rt_stats *out);
 /* Octree culling slack, in units of 2^-24 x (ray-origin-to-scene distance):
  * boxes are grown by that much so a triangle the reference's float
  * Moller-Trumbore test accepts is never culled (DESIGN.md "Conservative
- * culling").  Default RT_EPS_ULPS_DEFAULT (64).  Tuning knob: smaller is
- * faster and risks parity on grazing rays. */
+ * culling").  Default RT_EPS_ULPS_DEFAULT (64).  Tuning knob: below the
+ * default rt_hip_stats returns RT_EINEXACT (reflection rays rely on it). */
 int rt_hip_set_cull_slack(rt_hip_ctx *ctx, float ulps);
 /* The same slack for camera rays only (bounce depth 0; rt_hip_set_cull_slack
  * sets both).  A wider camera slack costs a few more node visits and lets
@@ -193,8 +197,8 @@ int rt_hip_set_count_work(rt_hip_ctx *ctx, int enable);
 int rt_hip_tile_phase_cycles(rt_hip_ctx *ctx, int phase, unsigned long long *out, size_t n);
 /* Exact camera rays (default 1): per-frame candidate lists of the triangles
  * whose float Moller-Trumbore error region the octree slack does not cover
- * (csrc/rt_cand.hip).  0 = octree walk only (A/B timing; cpu/rt parity is
- * then not guaranteed for grazing camera rays). */
+ * (csrc/rt_cand.hip).  0 = octree walk only (A/B timing; rt_hip_stats then
+ * returns RT_EINEXACT: cpu/rt parity is not guaranteed for grazing camera rays). */
 int rt_hip_set_exact_camera(rt_hip_ctx *ctx, int enable);
 /* Octree traversal policy (default 0): 0 = staged packet walk for coherent
  * closest-hit queries, per-lane walks otherwise; 1 = every query per lane;
@@ -204,7 +208,7 @@ int rt_hip_set_exact_camera(rt_hip_ctx *ctx, int enable);
 int rt_hip_set_policy(rt_hip_ctx *ctx, int policy);
 /* Scale of the error-bound constants the candidate lists use (1 = the
  * proven bound of tools/mt_bound.py; smaller = a calibrated model, faster,
- * exactness then verified rather than proven). */
+ * exactness then verified rather than proven: rt_hip_stats returns RT_EINEXACT). */
 int rt_hip_set_camera_bound_scale(rt_hip_ctx *ctx, double scale);
 /* Host-only survey of the camera candidate lists of a scene's frame (no
  * device): out = {safe, footprint, global} triangle counts, tile entries,

@@ -1172,6 +1172,14 @@ extern "C" int rt_hip_stats(rt_hip_ctx* c, rt_stats* out) {
                         "%llu point-light shadow rays left from beyond the extent the shadow "
                         "walk's exactness bound assumes (csrc/rt_shadow.hip)",
                         out->shadow_unproven);
+  // tuning knobs that give up the parity guarantee (A/B measurements only):
+  // the image is complete, but not promised to equal cpu/rt's
+  if (c->accel == RT_ACCEL_OCTREE && c->d_node &&
+      (!c->exact_camera || c->bound_scale < 1.0 || c->eps_ulps < RT_EPS_ULPS_DEFAULT))
+    return rt_set_error(RT_EINEXACT,
+                        "rendered with exact_camera=%d, camera bound scale %g, culling slack %g ulps "
+                        "(defaults 1, 1, %d): cpu/rt parity not guaranteed",
+                        c->exact_camera, c->bound_scale, (double)c->eps_ulps, RT_EPS_ULPS_DEFAULT);
   return RT_OK;
 }
 

@@ -370,12 +370,21 @@ def tile_buffer_floats(width, height, nranks):
 class Context:
     """One device image of a scene (rt_hip_create); renders through the C ABI."""
 
+    RT_EINEXACT = -11
+
     def __init__(self, scene: Scene, accel="octree", device=0):
         self.device = device
         self.accel = ACCEL[accel] if isinstance(accel, str) else accel
+        self.inexact = False  # a parity-breaking tuning knob was set (A/B runs)
         h = C.c_void_p()
         _check(lib().rt_hip_create(device, scene.ptr, self.accel, C.byref(h)), "rt_hip_create")
         self.h = h
+
+    def _check_render(self, rc, what):
+        """RT_EINEXACT is expected after a parity-breaking knob was set."""
+        if rc == self.RT_EINEXACT and self.inexact:
+            return
+        _check(rc, what)
 
     def info(self):
         i = AccelInfo()
@@ -391,6 +400,8 @@ class Context:
 
     def set_exact_camera(self, on=True):
         _check(lib().rt_hip_set_exact_camera(self.h, 1 if on else 0), "exact_camera")
+        if not on:
+            self.inexact = True
 
     def set_timing(self, on=True):
         """HIP events around the candidate lists and the render kernel of
@@ -431,9 +442,13 @@ class Context:
 
     def set_camera_bound_scale(self, scale):
         _check(lib().rt_hip_set_camera_bound_scale(self.h, float(scale)), "bound_scale")
+        if scale < 1.0:
+            self.inexact = True
 
     def set_cull_slack(self, ulps):
         _check(lib().rt_hip_set_cull_slack(self.h, float(ulps)), "cull_slack")
+        if ulps < 64.0:
+            self.inexact = True
 
     def cand_verify(self, frame, rank=0, nranks=1):
         """Host re-derivation of the last render's candidate lists:
@@ -467,7 +482,7 @@ class Context:
 
     def stats(self):
         st = Stats()
-        _check(lib().rt_hip_stats(self.h, C.byref(st)), "rt_hip_stats")
+        self._check_render(lib().rt_hip_stats(self.h, C.byref(st)), "rt_hip_stats")
         return st.as_dict()
 
     def assemble(self, frame, d_gathered, nranks, d_rgb, stream=None):
@@ -479,9 +494,9 @@ class Context:
         """Whole frame on this device -> (H, W, 3) float32 in PPM order, stats."""
         img = np.empty((frame.height, frame.width, 3), np.float32)
         st = Stats()
-        _check(lib().rt_hip_render_image(self.h, C.byref(frame),
-                                         img.ctypes.data_as(C.c_void_p), C.byref(st)),
-               "rt_hip_render_image")
+        self._check_render(lib().rt_hip_render_image(self.h, C.byref(frame),
+                                                     img.ctypes.data_as(C.c_void_p), C.byref(st)),
+                           "rt_hip_render_image")
         return img, st.as_dict()
 
     def render_compat(self, camera):

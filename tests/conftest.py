@@ -64,3 +64,27 @@ def case_id(case):
 def load_manifest_static():
     with open(os.path.join(GOLDEN, "manifest.json")) as f:
         return json.load(f)["cases"]
+
+
+OWN = os.path.join(GOLDEN, "own")
+
+
+def load_own_manifest():
+    """Goldens of our own scenes, rendered by the reference cpu/rt
+    (tests/golden/make_golden_own.py)."""
+    with open(os.path.join(OWN, "manifest.json")) as f:
+        return json.load(f)["cases"]
+
+
+def own_scene_path(case, tmpdir):
+    """The case's .svati, unpacked into tmpdir."""
+    dst = os.path.join(str(tmpdir), case["svati"][:-3])
+    with gzip.open(os.path.join(OWN, case["svati"]), "rb") as i, open(dst, "wb") as o:
+        o.write(i.read())
+    return dst
+
+
+def own_golden_image(case):
+    with gzip.open(os.path.join(OWN, case["file"]), "rb") as f:
+        data = f.read()
+    return np.frombuffer(data, dtype=np.float32).reshape(case["height"], case["width"], 3)

@@ -12,10 +12,12 @@ import subprocess
 import numpy as np
 import pytest
 
-from conftest import REPO, case_id, golden_image, load_manifest_static
+from conftest import (REPO, case_id, golden_image, load_manifest_static, load_own_manifest,
+                      own_golden_image, own_scene_path)
 
 pytestmark = pytest.mark.gpu
 CASES = load_manifest_static()
+OWN_CASES = load_own_manifest()
 
 
 def ulp_diff(a, b):
@@ -53,6 +55,67 @@ def test_golden_bitexact(case, accel, gpu, scene_dir):
     assert st["closest"] == case["closest"]
     assert st["shadow"] == case["shadow"]
     assert st["depth_overflow"] == 0 and st["zero_normal"] == 0
+
+
+@pytest.mark.parametrize("accel", ["flat", "octree", "octree_gpu"])
+@pytest.mark.parametrize("case", OWN_CASES, ids=[case_id(c) for c in OWN_CASES])
+def test_deep_reflections_bitexact(case, accel, gpu, tmp_path):
+    """Paths as deep as cpu/rt's recursion makes them (cpu/raytracer.c:19-34):
+    two facing Nr 0.9 mirrors, 44 closest-hit queries per camera ray, against
+    the reference's own output -- round 2 stopped at 32 with RT_EDEPTH."""
+    s = gpu.Scene.load_svati(own_scene_path(case, tmp_path))
+    img, st = gpu.Context(s, accel).render_image(s.frame())
+    assert_bitexact(img, own_golden_image(case), f"{case_id(case)}/{accel}")
+    assert st["closest"] == case["closest"] and st["shadow"] == case["shadow"]
+    assert st["depth_overflow"] == 0 and st["hit_records"] == st["closest"]
+
+
+def test_endless_mirror_reports_depth(gpu, tmp_path):
+    """Nr 1.0 mirrors facing each other: cpu/rt's recursion never ends (its
+    stack overflows); the render stops each path at RT_MAX_BOUNCES and fails
+    loudly with RT_EDEPTH instead of writing a silently truncated image."""
+    text = open(own_scene_path(OWN_CASES[0], tmp_path)).read().replace("Nr 0.9", "Nr 1.0")
+    sv = tmp_path / "endless.svati"
+    sv.write_text(text.replace("camera 32 18", "camera 8 4"))
+    s = gpu.Scene.load_svati(str(sv))
+    with pytest.raises(gpu.RtError) as e:
+        gpu.Context(s, "octree").render_image(s.frame())
+    assert e.value.code == -7
+
+
+def test_c4_car_on_road_4k_eight_rank_split(gpu, scene_dir):
+    """Config C4 at its real size: car-on-road at 3840x2160 rendered as the
+    8-rank split (every rank's tiles, one rank at a time on this GPU), gathered
+    rank-major and assembled, equals the brute-force whole frame bit for bit,
+    with the same query counts; sampled pixels equal the oracle."""
+    import ctypes as C
+    s = gpu.Scene.load_svati(os.path.join(scene_dir, "car-on-road.svati"))
+    W, H, n = 3840, 2160, 8
+    s.set_size(W, H)
+    f = s.frame()
+    img_f, st_f = gpu.Context(s, "flat").render_image(f)
+    ctx = gpu.Context(s, "octree")
+    per = gpu.tile_buffer_floats(W, H, n)
+    L = gpu.lib()
+    dg, drgb = C.c_void_p(), C.c_void_p()
+    assert L.rt_hip_malloc(0, per * n * 4, C.byref(dg)) == 0
+    assert L.rt_hip_malloc(0, W * H * 12, C.byref(drgb)) == 0
+    tot = {"closest": 0, "shadow": 0}
+    for r in range(n):
+        ctx.render(f, r, n, dg.value + r * per * 4)
+        st = ctx.stats()
+        tot["closest"] += st["closest"]
+        tot["shadow"] += st["shadow"]
+    ctx.assemble(f, dg.value, n, drgb.value)
+    img = np.empty((H, W, 3), np.float32)
+    ctx.stats()  # sync
+    assert L.rt_hip_memcpy_d2h(img.ctypes.data_as(C.c_void_p), drgb, img.nbytes) == 0
+    L.rt_hip_free(dg)
+    L.rt_hip_free(drgb)
+    assert_bitexact(img, img_f, "C4 8-rank split vs brute force")
+    assert (tot["closest"], tot["shadow"]) == (st_f["closest"], st_f["shadow"])
+    pix, vals = _oracle_sample(s, W, H, 32, 4)
+    assert_bitexact(img[pix[:, 0], pix[:, 1]], vals, "C4 vs oracle sample")
 
 
 def test_cli_ppm_md5(gpu, scene_dir, tmp_path, manifest):

@@ -9,9 +9,11 @@ import os
 import numpy as np
 import pytest
 
-from conftest import case_id, golden_image, load_manifest_static
+from conftest import (case_id, golden_image, load_manifest_static, load_own_manifest,
+                      own_golden_image, own_scene_path)
 
 CASES = load_manifest_static()
+OWN_CASES = load_own_manifest()
 
 
 @pytest.mark.parametrize("case", CASES, ids=[case_id(c) for c in CASES])
@@ -51,3 +53,17 @@ def test_color_ops_known_answers(built):
     m = L.oracle_color_mul(orc.ColorS(255.0, 128.0, 0.0), 0.25)
     exp_g = np.float32(np.float32(np.float32(128.0) / np.float32(255)) * np.float32(0.25)) * np.float32(255)
     assert m.g == exp_g
+
+
+@pytest.mark.parametrize("case", OWN_CASES, ids=[case_id(c) for c in OWN_CASES])
+def test_oracle_matches_reference_on_own_scenes(case, built, tmp_path):
+    """Our own scenes (tests/golden/make_golden_own.py), rendered by the
+    reference cpu/rt: two facing Nr 0.9 mirrors make every camera ray's path
+    44 closest-hit queries deep (cpu/raytracer.c:19-34 recurses while coef >=
+    0.01; 0.9^44 < 0.01)."""
+    import oracle as orc
+    sc = orc.OracleScene(own_scene_path(case, tmp_path))
+    img, cnt = orc.render(sc, case["width"], case["height"], threads=0)
+    assert np.array_equal(img.view(np.uint32), own_golden_image(case).view(np.uint32))
+    assert cnt["closest"] == case["closest"] and cnt["shadow"] == case["shadow"]
+    assert cnt["max_depth"] >= 43
