@@ -40,6 +40,11 @@
 #ifndef RT_SHADE_MIN_WAVES
 #define RT_SHADE_MIN_WAVES 8
 #endif
+// the brute-force (FLAT) shade kernel streams records through LDS, two at a
+// time (mt_candidate2): at 8 waves it spilled 96 B per lane
+#ifndef RT_FLAT_SHADE_MIN_WAVES
+#define RT_FLAT_SHADE_MIN_WAVES 5
+#endif
 // triangle record flag (q2.w bits, host/accel.c rt_flatten): the record's
 // object has a triangle whose interpolated normal can be exactly zero, so
 // cpu/hit.c:99 may skip the object in collide_dist (early any-hit exit is

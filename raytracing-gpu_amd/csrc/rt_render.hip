@@ -112,6 +112,33 @@ __device__ __forceinline__ bool mt_candidate(f3 o, f3 d, f3 v0, f3 e1, f3 e2, fl
   return !(t < kEps * (1.0f - m) || t > t_cut);
 }
 
+// mt_candidate for two triangles at once (brute-force loops): the two
+// dependency chains are independent, so they interleave and hide each
+// other's VALU latency; the stages still end early when every lane of the
+// wave has rejected both (ballot).  Same float operations, same decisions.
+__device__ __forceinline__ void mt_candidate2(f3 o, f3 d, const float4* qa, const float4* qb,
+                                              float t_cut, bool& ca, bool& cb) {
+  const float m = 1e-5f;
+  const f3 v0a{qa[0].x, qa[0].y, qa[0].z}, e1a{qa[0].w, qa[1].x, qa[1].y}, e2a{qa[1].z, qa[1].w, qa[2].x};
+  const f3 v0b{qb[0].x, qb[0].y, qb[0].z}, e1b{qb[0].w, qb[1].x, qb[1].y}, e2b{qb[1].z, qb[1].w, qb[2].x};
+  const f3 ha = cross(d, e2a), hb = cross(d, e2b);
+  const float aa = dot(e1a, ha), ab = dot(e1b, hb);
+  const float ra = __builtin_amdgcn_rcpf(aa), rb = __builtin_amdgcn_rcpf(ab);
+  const f3 sa = sub(o, v0a), sb = sub(o, v0b);
+  const float ua = dot(sa, ha) * ra, ub = dot(sb, hb) * rb;
+  ca = !(aa > -kEps && aa < kEps) && !(ua < -1e-30f || ua > 1.0f + m);
+  cb = !(ab > -kEps && ab < kEps) && !(ub < -1e-30f || ub > 1.0f + m);
+  if (__ballot(ca || cb) == 0) return;
+  const f3 qva = cross(sa, e1a), qvb = cross(sb, e1b);
+  const float va = dot(d, qva) * ra, vb = dot(d, qvb) * rb;
+  ca = ca && !(va < -1e-30f || ua + va > 1.0f + m);
+  cb = cb && !(vb < -1e-30f || ub + vb > 1.0f + m);
+  if (__ballot(ca || cb) == 0) return;
+  const float ta = dot(e2a, qva) * ra, tb = dot(e2b, qvb) * rb;
+  ca = ca && !(ta < kEps * (1.0f - m) || ta > t_cut);
+  cb = cb && !(tb < kEps * (1.0f - m) || tb > t_cut);
+}
+
 struct Best {
   float dist;  // +inf = none
   float t_cut; // parametric bound beyond which no triangle can win (+inf = none)
@@ -120,10 +147,21 @@ struct Best {
   float t;  // the winner's MT t; its hit point is hit_point(r, t)
 };
 
+__device__ __forceinline__ void consider_exact(const Ray& r, const float4& q0, const float4& q1,
+                                               const float4& q2, Best& b);
+
 __device__ __forceinline__ void consider(const Ray& r, const float4& q0, const float4& q1,
                                          const float4& q2, Best& b) {
   f3 v0{q0.x, q0.y, q0.z}, e1{q0.w, q1.x, q1.y}, e2{q1.z, q1.w, q2.x};
   if (!mt_candidate(r.o, r.d, v0, e1, e2, b.t_cut)) return;
+  consider_exact(r, q0, q1, q2, b);
+}
+
+// The reference's exact test of a prefilter survivor and the lexicographic
+// (new_dist, prim) update (cpu/hit.c:15-37,58-59,82).
+__device__ __forceinline__ void consider_exact(const Ray& r, const float4& q0, const float4& q1,
+                                               const float4& q2, Best& b) {
+  f3 v0{q0.x, q0.y, q0.z}, e1{q0.w, q1.x, q1.y}, e2{q1.z, q1.w, q2.x};
   float t, u, v;
   if (!mt_test(r.o, r.d, v0, e1, e2, t, u, v)) return;
   float nd = hit_dist(r, t);
@@ -149,10 +187,20 @@ __device__ __forceinline__ void consider(const Ray& r, const float4& q0, const f
 // host/accel.c): its closest hit then counts in collide_dist whatever
 // triangle the walk met first.  A hit on a flagged object sets `risk`
 // (reported as RT_EZERONORMAL, never silent).
+__device__ __forceinline__ bool any_hit_exact(const Ray& r, const float4& q0, const float4& q1,
+                                              const float4& q2, uint32_t& risk);
+
 __device__ __forceinline__ bool any_hit_rec(const Ray& r, const float4& q0, const float4& q1,
                                             const float4& q2, uint32_t& risk) {
   f3 v0{q0.x, q0.y, q0.z}, e1{q0.w, q1.x, q1.y}, e2{q1.z, q1.w, q2.x};
   if (!mt_candidate(r.o, r.d, v0, e1, e2, __builtin_inff())) return false;
+  return any_hit_exact(r, q0, q1, q2, risk);
+}
+
+// the exact test of a prefilter survivor (any_hit_rec)
+__device__ __forceinline__ bool any_hit_exact(const Ray& r, const float4& q0, const float4& q1,
+                                              const float4& q2, uint32_t& risk) {
+  f3 v0{q0.x, q0.y, q0.z}, e1{q0.w, q1.x, q1.y}, e2{q1.z, q1.w, q2.x};
   float t, u, v;
   if (!mt_test(r.o, r.d, v0, e1, e2, t, u, v)) return false;
   if (!((double)hit_dist(r, t) > 0.01)) return false;
@@ -574,14 +622,19 @@ __device__ void flat_closest_w(const KParams& p, const Ray& r, bool act, Best& b
     fetch_commit(f, w);
     uint32_t nb = base + kFlatRecs;
     if (nb < n) f = fetch_issue(p.tri + 3 * (size_t)nb, 3 * (int)chunk<kFlatRecs>(n, nb), w.lane);
-    // software-pipelined: record k+1's LDS reads are in flight while k is tested
-    float4 n0 = w.stage[0], n1 = w.stage[1], n2 = w.stage[2];
-    for (uint32_t k = 0; k < m; k++) {
-      float4 q0 = n0, q1 = n1, q2 = n2;
-      uint32_t kn = k + 1 < m ? 3 * (k + 1) : 0;
-      n0 = w.stage[kn];
-      n1 = w.stage[kn + 1];
-      n2 = w.stage[kn + 2];
+    // two records per step (mt_candidate2: two independent chains), the
+    // survivors tested exactly in record order
+    uint32_t k = 0;
+    for (; k + 1 < m; k += 2) {
+      const float4 qa[3] = {w.stage[3 * k], w.stage[3 * k + 1], w.stage[3 * k + 2]};
+      const float4 qb[3] = {w.stage[3 * k + 3], w.stage[3 * k + 4], w.stage[3 * k + 5]};
+      bool ca = false, cb = false;
+      if (act) mt_candidate2(r.o, r.d, qa, qb, b.t_cut, ca, cb);
+      if (ca) consider_exact(r, qa[0], qa[1], qa[2], b);
+      if (cb) consider_exact(r, qb[0], qb[1], qb[2], b);
+    }
+    if (k < m) {
+      const float4 q0 = w.stage[3 * k], q1 = w.stage[3 * k + 1], q2 = w.stage[3 * k + 2];
       if (act) consider(r, q0, q1, q2, b);
     }
   }
@@ -607,18 +660,26 @@ __device__ bool flat_any_w(const KParams& p, const Ray& r, bool act, WaveCtx& w,
       wc.tris += m;
       wc.sh_tris += m * (uint32_t)__popcll(__ballot(alive));
     }
-    float4 n0 = w.stage[0], n1 = w.stage[1], n2 = w.stage[2];
-    for (uint32_t k = 0; k < m; k++) {
-      float4 q0 = n0, q1 = n1, q2 = n2;
-      uint32_t kn = k + 1 < m ? 3 * (k + 1) : 0;
-      n0 = w.stage[kn];
-      n1 = w.stage[kn + 1];
-      n2 = w.stage[kn + 2];
-      if (alive && any_hit_rec(r, q0, q1, q2, risk)) {
+    // two records per step (mt_candidate2), as flat_closest_w
+    uint32_t k = 0;
+    for (; k + 1 < m; k += 2) {
+      const float4 qa[3] = {w.stage[3 * k], w.stage[3 * k + 1], w.stage[3 * k + 2]};
+      const float4 qb[3] = {w.stage[3 * k + 3], w.stage[3 * k + 4], w.stage[3 * k + 5]};
+      bool ca = false, cb = false;
+      if (alive) mt_candidate2(r.o, r.d, qa, qb, __builtin_inff(), ca, cb);
+      if ((ca && any_hit_exact(r, qa[0], qa[1], qa[2], risk)) ||
+          (cb && any_hit_exact(r, qb[0], qb[1], qb[2], risk))) {
         hit = true;
         alive = false;
       }
       if (__ballot(alive) == 0) break;
+    }
+    if (k < m && __ballot(alive) != 0) {
+      const float4 q0 = w.stage[3 * k], q1 = w.stage[3 * k + 1], q2 = w.stage[3 * k + 2];
+      if (alive && any_hit_rec(r, q0, q1, q2, risk)) {
+        hit = true;
+        alive = false;
+      }
     }
     if (__ballot(alive) == 0) break;
   }
@@ -1387,7 +1448,7 @@ __device__ __forceinline__ col shade_record(const KParams& p, bool valid, size_t
 // cpu/light.c:33-100 with the shadow queries of cpu/light.c:24-31, then the
 // term color_mul(local, coef) of cpu/raytracer.c:30.
 template <int ACCEL, bool COUNT, int POL>
-__global__ __launch_bounds__(64, RT_SHADE_MIN_WAVES) void shade_kernel(KParams p) {
+__global__ __launch_bounds__(64, ACCEL == RT_ACCEL_FLAT_D ? RT_FLAT_SHADE_MIN_WAVES : RT_SHADE_MIN_WAVES) void shade_kernel(KParams p) {
   const int lane = threadIdx.x & 63;
   WorkCount wc = {};
   constexpr bool kStaged = POL == RT_POLICY_STAGED || POL == RT_POLICY_DIR_STAGED;
