@@ -200,6 +200,15 @@ int rt_hip_tile_phase_cycles(rt_hip_ctx *ctx, int phase, unsigned long long *out
  * (csrc/rt_cand.hip).  0 = octree walk only (A/B timing; rt_hip_stats then
  * returns RT_EINEXACT: cpu/rt parity is not guaranteed for grazing camera rays). */
 int rt_hip_set_exact_camera(rt_hip_ctx *ctx, int enable);
+/* Proven shadow rays (default 0): the shadow walk grows each node's box by
+ * a per-node multiple of the culling slack that covers the float
+ * Moller-Trumbore error region of every triangle below it for every shadow
+ * ray of the scene's lights, plus a global list (csrc/rt_shadow.hip,
+ * DESIGN.md §2).  Exact by construction but, near the terminators where
+ * shadow rays graze the surfaces, the bound grows like 1/cos: on C5 it
+ * costs ~160x the shade time.  Default: the plain slack, whose shadow
+ * decisions are verified against brute force (rt_hip_verify_shadows). */
+int rt_hip_set_exact_shadows(rt_hip_ctx *ctx, int enable);
 /* Octree traversal policy (default 0): 0 = staged packet walk for coherent
  * closest-hit queries, per-lane walks otherwise; 1 = every query per lane;
  * 2 = every query as a staged packet; 3 = 0 plus staged packet walks for

@@ -90,6 +90,7 @@ struct rt_hip_ctx {
   float sh_ulps = -1.0f;
   float sh_omax = 0.0f;
   float sh_mu_max = 1.0f;
+  int exact_shadows = 0;  // opt-in: the proven shadow walk (rt_hip_set_exact_shadows)
   size_t tile_cycles_cap = 0, tile_cycles_n = 0;
   // exact camera rays (csrc/rt_cand.hip)
   int exact_camera = 1;
@@ -220,7 +221,7 @@ extern "C" void rt_hip_destroy(rt_hip_ctx* c) {
 // slack (csrc/rt_shadow.hip): once per scene and slack, on the context's
 // stream, synchronous (setup; it reads back the global list's length).
 static int shadow_prepare(rt_hip_ctx* c, hipStream_t s) {
-  if (c->accel != RT_ACCEL_OCTREE || !c->d_node) return RT_OK;
+  if (!c->exact_shadows || c->accel != RT_ACCEL_OCTREE || !c->d_node) return RT_OK;
   if (c->d_node_mu && c->sh_ulps == c->eps_ulps) return RT_OK;
   const size_t np = c->nprim, nn = c->info.nodes;
   if (!c->d_node_mu) {
@@ -403,11 +404,6 @@ extern "C" int rt_hip_create(int device, const rt_scene* scene, int accel, rt_hi
     rt_hip_destroy(c);
     return rt_set_error(RT_EHIP, "hipMalloc traversal spill stack");
   }
-  rc = shadow_prepare(c, c->stream);
-  if (rc) {
-    rt_hip_destroy(c);
-    return rc;
-  }
   *out = c;
   return RT_OK;
 }
@@ -458,6 +454,16 @@ extern "C" int rt_hip_set_camera_slack(rt_hip_ctx* c, float ulps) {
 extern "C" int rt_hip_set_exact_camera(rt_hip_ctx* c, int enable) {
   if (!c) return rt_set_error(RT_EINVAL, "null context");
   c->exact_camera = enable ? 1 : 0;
+  return RT_OK;
+}
+
+extern "C" int rt_hip_set_exact_shadows(rt_hip_ctx* c, int enable) {
+  if (!c) return rt_set_error(RT_EINVAL, "null context");
+  c->exact_shadows = enable ? 1 : 0;
+  if (c->exact_shadows) {  // built now (setup), reported by rt_hip_accel_info
+    HIP_TRY(hipSetDevice(c->device));
+    return shadow_prepare(c, c->stream);
+  }
   return RT_OK;
 }
 
@@ -984,10 +990,12 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
     int rc = shadow_prepare(c, s);  // no-op unless the culling slack changed
     if (rc) return rc;
   }
-  p.node_mu = c->d_node_mu;
-  p.sh_global = c->d_sh_global;
-  p.n_sh_global = c->n_sh_global;
-  p.sh_omax = c->sh_omax;
+  if (c->exact_shadows) {
+    p.node_mu = c->d_node_mu;
+    p.sh_global = c->d_sh_global;
+    p.n_sh_global = c->n_sh_global;
+    p.sh_omax = c->sh_omax;
+  }
   c->cand_prims = c->cand_entries = c->cand_global = 0;
   hipEvent_t* ev = c->ev[c->frames % RT_TIMED_FRAMES];
   if (c->timing) HIP_TRY(hipEventRecord(ev[0], s));
@@ -1286,10 +1294,12 @@ extern "C" int rt_hip_render_compat(rt_hip_ctx* c, const rt_camera* cam, unsigne
     (void)hipFree(d_lo);
     return rc;
   }
-  p.node_mu = c->d_node_mu;
-  p.sh_global = c->d_sh_global;
-  p.n_sh_global = c->n_sh_global;
-  p.sh_omax = c->sh_omax;
+  if (c->exact_shadows) {
+    p.node_mu = c->d_node_mu;
+    p.sh_global = c->d_sh_global;
+    p.n_sh_global = c->n_sh_global;
+    p.sh_omax = c->sh_omax;
+  }
   p.tri_prim = c->d_tri_prim;
   if (hipMemsetAsync(c->d_counter, 0, 8 * 128, s) != hipSuccess ||
       hipMemsetAsync(c->d_stats, 0, RT_NSTATS * sizeof(unsigned long long), s) != hipSuccess ||

@@ -30,6 +30,9 @@
 namespace rt {
 
 static constexpr float kEps = 0.0000001f;  // cpu/hit.c:7 (float)1e-7
+#ifndef RT_CAND_PAIR
+#define RT_CAND_PAIR 1  // camera candidates tested two per step (A/B: 0)
+#endif
 
 // The workgroup is one wave and a wave's LDS instructions execute in issue
 // order, so LDS staging needs no s_barrier: only a compiler barrier that
@@ -407,7 +410,8 @@ __device__ __forceinline__ void push_children_any(const float4* __restrict__ nod
   const int step = up ? 1 : -1;
   uint32_t ci = first + (uint32_t)k;
   float4 nlo = node[2 * ci], nhi = node[2 * ci + 1];
-  float2 nmu = mu[ci];
+  // exact-shadow mode (mu != NULL, a kernel argument: a uniform branch)
+  float2 nmu = mu ? mu[ci] : make_float2(1.0f, 0.0f);
   if (COUNT) wc.nodes += lanes_distinct(ci);
   for (int n = 0; n < cnt; n++) {
     float4 clo = nlo, chi = nhi;
@@ -416,10 +420,11 @@ __device__ __forceinline__ void push_children_any(const float4* __restrict__ nod
       ci += (uint32_t)step;
       nlo = node[2 * ci];
       nhi = node[2 * ci + 1];
-      nmu = mu[ci];
+      if (mu) nmu = mu[ci];
       if (COUNT) wc.nodes += lanes_distinct(ci);
     }
-    if (box_hit_sh(r, inv, clo, chi, cmu)) push(s, __float_as_uint(clo.w), chi.w, wc);
+    const bool h = mu ? box_hit_sh(r, inv, clo, chi, cmu) : box_enter(r, inv, clo, chi) != __builtin_inff();
+    if (h) push(s, __float_as_uint(clo.w), chi.w, wc);
   }
 }
 
@@ -492,7 +497,9 @@ __device__ bool oct_any(const KParams& p, const Ray& r, Stack& s, LaneCount& wc)
   {
     float4 lo = node[0], hi = node[1];
     if (COUNT) wc.nodes += lanes_distinct(0);
-    if (box_hit_sh(r, inv, lo, hi, p.node_mu[0])) push(s, __float_as_uint(lo.w), hi.w, wc);
+    const bool h = p.node_mu ? box_hit_sh(r, inv, lo, hi, p.node_mu[0])
+                             : box_enter(r, inv, lo, hi) != __builtin_inff();
+    if (h) push(s, __float_as_uint(lo.w), hi.w, wc);
   }
   Best unused;
   while (s.sp > 0) {
@@ -809,7 +816,8 @@ __device__ __forceinline__ void stage_push_children(const Ray& r, f3 inv, uint32
       float4 clo = w.stage[2 * c], chi = w.stage[2 * c + 1];
       bool w2;
       if (ANY) {
-        w2 = want && box_hit_sh(r, inv, clo, chi, mu[c]);  // the shadow walk's grown boxes
+        w2 = want && (mu ? box_hit_sh(r, inv, clo, chi, mu[c])  // exact-shadow mode's grown boxes
+                         : box_enter(r, inv, clo, chi) != __builtin_inff());
       } else {
         float t0 = box_enter(r, inv, clo, chi);
         w2 = want && t0 != __builtin_inff() && !(t0 * r.dlen > limit);
@@ -944,7 +952,8 @@ __device__ bool staged_any(const KParams& p, const Ray& r, bool act, WaveCtx& w,
       if (__ballot(alive) == 0) break;
     } else {
       stage_load(node + 2 * (size_t)first, 2 * (int)RT_NODE_COUNT(info), w);
-      stage_push_children<true>(r, inv, dm, info, want, 0.0f, sp, w, wc, p.node_mu + first);
+      stage_push_children<true>(r, inv, dm, info, want, 0.0f, sp, w, wc,
+                                p.node_mu ? p.node_mu + first : nullptr);
     }
   }
   wc.zero_risk += (uint32_t)__popcll(__ballot(risk != 0));
@@ -1027,8 +1036,9 @@ __device__ __forceinline__ bool shadow_q(const KParams& p, f3 o, f3 d, uint32_t 
     }
     wc.zero_risk += (uint32_t)__popcll(__ballot(risk != 0));
   }
-  // point lights: the cosine bound assumed origins within sh_omax of the scene centre
-  if (type == 2) {
+  // point lights (exact-shadow mode): the cosine bound assumed origins within
+  // sh_omax of the scene centre
+  if (type == 2 && p.node_mu) {
     const float m = fmaxf(fabsf(o.x - p.scene_c.x), fmaxf(fabsf(o.y - p.scene_c.y), fabsf(o.z - p.scene_c.z)));
     wc.sh_unproven += (uint32_t)__popcll(__ballot(act && !(m <= p.sh_omax)));
   }
@@ -1165,7 +1175,16 @@ __device__ __forceinline__ void cand_closest(const KParams& p, const Ray& r, boo
       w.stage[3 * slot + 2] = g2;
     }
     wave_sync();
-    for (uint32_t k = 0; k < n; k++) {
+    uint32_t k = 0;
+    for (; RT_CAND_PAIR && k + 1 < n; k += 2) {  // two candidates per step (mt_candidate2)
+      const float4 qa[3] = {w.stage[3 * k], w.stage[3 * k + 1], w.stage[3 * k + 2]};
+      const float4 qb[3] = {w.stage[3 * k + 3], w.stage[3 * k + 4], w.stage[3 * k + 5]};
+      bool ca = false, cb = false;
+      if (act) mt_candidate2(r.o, r.d, qa, qb, b.t_cut, ca, cb);
+      if (ca) consider_exact(r, qa[0], qa[1], qa[2], b);
+      if (cb) consider_exact(r, qb[0], qb[1], qb[2], b);
+    }
+    for (; k < n; k++) {
       float4 q0 = w.stage[3 * k], q1 = w.stage[3 * k + 1], q2 = w.stage[3 * k + 2];
       if (act) consider(r, q0, q1, q2, b);
     }

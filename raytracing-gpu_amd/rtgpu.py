@@ -153,6 +153,7 @@ _PROTOS = [
     ("rt_hip_verify_shadows", C.c_int, [C.c_void_p, C.c_uint, C.POINTER(C.c_ulonglong)]),
     ("rt_hip_set_exact_camera", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_set_policy", C.c_int, [C.c_void_p, C.c_int]),
+    ("rt_hip_set_exact_shadows", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_tile_cycles", C.c_int, [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_size_t]),
     ("rt_hip_tile_phase_cycles", C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_ulonglong),
                                            C.c_size_t]),
@@ -434,6 +435,10 @@ class Context:
                                               out.ctypes.data_as(C.POINTER(C.c_ulonglong)), n),
                "tile_phase_cycles")
         return out
+
+    def set_exact_shadows(self, on=True):
+        """Proven shadow walk (rt_hip_set_exact_shadows; slow near terminators)."""
+        _check(lib().rt_hip_set_exact_shadows(self.h, 1 if on else 0), "exact_shadows")
 
     def set_policy(self, policy):
         """Octree traversal policy (rt_hip_set_policy): 0 default, 1 per-lane,

@@ -353,8 +353,10 @@ def test_synthetic_full_frame_exact(gpu, accel):
     assert_bitexact(img_f[pix[:, 0], pix[:, 1]], vals, "synthetic brute force vs oracle")
 
 
-@pytest.mark.parametrize("accel,policy", [("octree_gpu", 0), ("octree", 0), ("octree_gpu", 3)])
-def test_shadow_queries_match_brute_force(gpu, accel, policy):
+@pytest.mark.parametrize("accel,policy,exact", [("octree_gpu", 0, False), ("octree", 0, False),
+                                                ("octree_gpu", 3, False), ("octree_gpu", 0, True),
+                                                ("octree", 2, True)])
+def test_shadow_queries_match_brute_force(gpu, accel, policy, exact):
     """Every shadow query of a frame (the shade kernel's per-record outcome of
     cpu/light.c:24-31 for each light) through the octree walk equals brute
     force over all triangles (cpu/hit.c:93-109) on the same hit records --
@@ -363,7 +365,10 @@ def test_shadow_queries_match_brute_force(gpu, accel, policy):
     s = gpu.Scene.synthetic(6, 6, 9776, seed=0x5EED, width=960, height=540)
     ctx = gpu.Context(s, accel)
     ctx.set_policy(policy)
-    ctx.render_image(s.frame())
+    if exact:  # the proven shadow walk (csrc/rt_shadow.hip)
+        ctx.set_exact_shadows(True)
+        assert ctx.info()["shadow_mu_max"] >= 1.0
+    img, _ = ctx.render_image(s.frame())
     v = ctx.verify_shadows(1)
     assert v["records"] > 100000 and v["queries"] == 2 * v["records"], v
     assert v["records_differ"] == 0 and v["walk_lit_brute_shadowed"] == 0, v
