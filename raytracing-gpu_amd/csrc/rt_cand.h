@@ -89,3 +89,8 @@ extern "C" hipError_t rt_cand_entry_skip(const uint32_t* cand, const float* skip
                                          uint32_t n, hipStream_t s);
 extern "C" hipError_t rt_cand_bounds(const uint32_t* keys, uint32_t n, uint32_t* start,
                                      uint32_t ntiles, hipStream_t s);
+// longest-first work order of the tiles (heavy candidate lists first):
+// perm[position] = tile.  tmp == NULL: *tmp_bytes = the scan's need.
+extern "C" hipError_t rt_cand_order(const uint32_t* start, uint32_t ntiles, uint32_t total,
+                                    uint32_t* flags, uint32_t* pos, uint32_t* perm, void* tmp,
+                                    size_t* tmp_bytes, hipStream_t s);

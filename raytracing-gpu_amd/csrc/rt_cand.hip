@@ -807,6 +807,29 @@ __global__ __launch_bounds__(256) void entry_skip_kernel(const uint32_t* cand, c
   if (i < n) out[i] = skip[cand[i]];
 }
 
+// Work order of the trace kernel's tiles (longest processing time first): a
+// tile's camera-candidate entries predict its cost (r = 0.89 on C5,
+// tools/tile_cost.py), so tiles with more than 8x the mean go first and the
+// persistent waves' last items are short ones.  flags -> exclusive scan ->
+// perm: heavy tiles first, then the rest, each in their own order.
+__global__ __launch_bounds__(256) void heavy_flag_kernel(const uint32_t* start, uint32_t ntiles,
+                                                         uint32_t total, uint32_t* flags) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t > ntiles) return;
+  flags[t] = t < ntiles && (unsigned long long)(start[t + 1] - start[t]) * ntiles >
+                               8ull * (unsigned long long)total
+                 ? 1u
+                 : 0u;
+}
+
+__global__ __launch_bounds__(256) void heavy_perm_kernel(const uint32_t* flags, const uint32_t* pos,
+                                                         uint32_t ntiles, uint32_t* perm) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntiles) return;
+  const uint32_t nheavy = pos[ntiles];
+  perm[flags[t] ? pos[t] : nheavy + t - pos[t]] = t;
+}
+
 }  // namespace rtc
 
 #include <algorithm>
@@ -1025,3 +1048,15 @@ extern "C" hipError_t rt_cand_bounds(const uint32_t* keys, uint32_t n, uint32_t*
   return hipGetLastError();
 }
 
+
+extern "C" hipError_t rt_cand_order(const uint32_t* start, uint32_t ntiles, uint32_t total,
+                                    uint32_t* flags, uint32_t* pos, uint32_t* perm, void* tmp,
+                                    size_t* tmp_bytes, hipStream_t s) {
+  if (!tmp) return rt_cand_scan(flags, pos, ntiles, nullptr, tmp_bytes, s);
+  const dim3 b(256), g((ntiles + 1 + 255) / 256);
+  hipLaunchKernelGGL(rtc::heavy_flag_kernel, g, b, 0, s, start, ntiles, total, flags);
+  hipError_t e = rt_cand_scan(flags, pos, ntiles, tmp, tmp_bytes, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(rtc::heavy_perm_kernel, g, b, 0, s, flags, pos, ntiles, perm);
+  return hipGetLastError();
+}

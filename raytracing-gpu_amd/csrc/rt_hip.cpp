@@ -112,7 +112,8 @@ struct rt_hip_ctx {
   uint32_t* d_cand_big_lane = nullptr;  // kBigLaneCap x 64 lane subtotals of big footprints
   uint32_t* d_prim_leaf = nullptr;    // nprim: a leaf holding each prim (camera-independent)
   uint32_t* d_cand = nullptr;
-  size_t cand_cap = 0, cand_tiles_cap = 0;
+  uint32_t* d_order = nullptr;        // 3 x (ntiles + 1): heavy flags, their scan, the work order
+  size_t cand_cap = 0, cand_tiles_cap = 0, order_cap = 0;
   void* d_scan_tmp = nullptr;
   size_t scan_tmp_bytes = 0;
   uint32_t* h_cand = nullptr;  // pinned: total entries, risky, global, visits
@@ -208,6 +209,7 @@ extern "C" void rt_hip_destroy(rt_hip_ctx* c) {
   (void)hipFree(c->d_cand_skip);
   (void)hipFree(c->d_prim_leaf);
   (void)hipFree(c->d_cand);
+  (void)hipFree(c->d_order);
   (void)hipFree(c->d_scan_tmp);
   if (c->h_cand) (void)hipHostFree(c->h_cand);
   for (auto& f : c->ev)
@@ -879,6 +881,23 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
   // the sorted keys are spent: their buffer takes the per-entry skip bounds
   float* entry_skip = (float*)c->d_cand_keys2;
   HIP_TRY(rt_cand_entry_skip(c->d_cand, c->d_cand_skip, entry_skip, total, s));
+  // longest-first work order of the rank's tiles (heavy lists first)
+  if (nt + 1 > c->order_cap) {
+    (void)hipFree(c->d_order);
+    c->d_order = nullptr;
+    c->order_cap = 0;
+    HIP_TRY(hipMalloc((void**)&c->d_order, 3 * (nt + 1) * sizeof(uint32_t)));
+    c->order_cap = nt + 1;
+  }
+  tb = 0;
+  HIP_TRY(rt_cand_order(c->d_cand_start, (uint32_t)nt, total, c->d_order, c->d_order + nt + 1,
+                        c->d_order + 2 * (nt + 1), nullptr, &tb, s));
+  rc = ensure_tmp(c, tb);
+  if (rc) return rc;
+  tb = c->scan_tmp_bytes;
+  HIP_TRY(rt_cand_order(c->d_cand_start, (uint32_t)nt, total, c->d_order, c->d_order + nt + 1,
+                        c->d_order + 2 * (nt + 1), c->d_scan_tmp, &tb, s));
+  kp->tile_order = c->d_order + 2 * (nt + 1);
   kp->cand_start = c->d_cand_start;
   kp->cand = c->d_cand;
   kp->cand_global = c->d_cand_global;

@@ -122,6 +122,7 @@ struct KParams {
   uint32_t n_cand_global;
   const float4* tri_prim;       // prim-order triangle records
   const float* cand_skip;       // per cand entry: lower bound of new_dist - |pos - o| (depth skip)
+  const uint32_t* tile_order;   // trace_kernel's work order: position -> rank-local tile (NULL: identity)
 };
 
 // The three launches of one render (policy = RT_POLICY_*, octree only):

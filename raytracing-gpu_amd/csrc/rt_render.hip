@@ -30,9 +30,6 @@
 namespace rt {
 
 static constexpr float kEps = 0.0000001f;  // cpu/hit.c:7 (float)1e-7
-#ifndef RT_CAND_PAIR
-#define RT_CAND_PAIR 1  // camera candidates tested two per step (A/B: 0)
-#endif
 
 // The workgroup is one wave and a wave's LDS instructions execute in issue
 // order, so LDS staging needs no s_barrier: only a compiler barrier that
@@ -1175,16 +1172,9 @@ __device__ __forceinline__ void cand_closest(const KParams& p, const Ray& r, boo
       w.stage[3 * slot + 2] = g2;
     }
     wave_sync();
-    uint32_t k = 0;
-    for (; RT_CAND_PAIR && k + 1 < n; k += 2) {  // two candidates per step (mt_candidate2)
-      const float4 qa[3] = {w.stage[3 * k], w.stage[3 * k + 1], w.stage[3 * k + 2]};
-      const float4 qb[3] = {w.stage[3 * k + 3], w.stage[3 * k + 4], w.stage[3 * k + 5]};
-      bool ca = false, cb = false;
-      if (act) mt_candidate2(r.o, r.d, qa, qb, b.t_cut, ca, cb);
-      if (ca) consider_exact(r, qa[0], qa[1], qa[2], b);
-      if (cb) consider_exact(r, qb[0], qb[1], qb[2], b);
-    }
-    for (; k < n; k++) {
+    // (two candidates per step, as the brute-force loops do, measured
+    // slower here: C5 frame 15.96 -> 16.10 ms, profiles/r03f_bench/ab.log)
+    for (uint32_t k = 0; k < n; k++) {
       float4 q0 = w.stage[3 * k], q1 = w.stage[3 * k + 1], q2 = w.stage[3 * k + 2];
       if (act) consider(r, q0, q1, q2, b);
     }
@@ -1361,7 +1351,10 @@ __global__ __launch_bounds__(64, RT_TRACE_MIN_WAVES) void trace_kernel(KParams p
   // tile's samples share one XCD's L2, all XCDs work on the same few tile
   // rows (their geometry stays in the Infinity Cache), and the item counters'
   // atomic traffic is split 8 ways; a drained stream's waves move on to the
-  // next.  Each item writes its lanes' deepest hit records.
+  // next.  Each item writes its lanes' deepest hit records.  With camera
+  // candidate lists the tiles come longest-first (rt_cand_order): a tile's
+  // list length predicts its cost, and the heavy tiles -- the horizon's
+  // grazing rays, up to 20x the mean on C5 -- no longer finish the kernel.
   const uint32_t nt = (uint32_t)p.ntiles_local;
   const uint32_t home = (uint32_t)blockIdx.x & 7u;
   uint32_t probe = 0;
@@ -1375,7 +1368,8 @@ __global__ __launch_bounds__(64, RT_TRACE_MIN_WAVES) void trace_kernel(KParams p
       if (++probe == 8u) break;  // every stream drained: the wave exits
       continue;
     }
-    const uint32_t u = 4u * (8u * (q >> 2) + x) + (q & 3u);  // item index 4t + s
+    const uint32_t pos = 8u * (q >> 2) + x;  // the tile's place in the work order
+    const uint32_t u = 4u * (p.tile_order ? p.tile_order[pos] : pos) + (q & 3u);  // item 4t + s
     const unsigned long long c0 = COUNT ? __builtin_readcyclecounter() : 0ull;
     const uint32_t ph0[3] = {wc.cy_cam, wc.cy_cand, wc.cy_sec};
     const uint32_t t = u >> 2;
