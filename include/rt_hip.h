@@ -221,11 +221,13 @@ int rt_hip_set_policy(rt_hip_ctx *ctx, int policy);
 int rt_hip_set_camera_bound_scale(rt_hip_ctx *ctx, double scale);
 /* Host-only survey of the camera candidate lists of a scene's frame (no
  * device): out = {safe, footprint, global} triangle counts, tile entries,
- * then 16 log2 buckets of triangles by entries and 16 of their entries;
- * use_leaves: also accept triangles whose error region fits a leaf box of the
+ * then 16 log2 buckets of triangles by entries and 16 of their entries,
+ * then 16 log2 buckets of footprint triangles by how far their error region
+ * (grown by its distance error) reaches beyond the triangle, in units of the
+ * walk's slack, and 16 of their entries; use_leaves: also accept triangles whose error region fits a leaf box of the
  * host-built octree. */
 int rt_cand_survey(const rt_scene *scene, float eps_ulps, double bound_scale, int threads,
-                   int use_leaves, unsigned long long out[36]);
+                   int use_leaves, unsigned long long out[72]);
 
 /* Test hook: after an rt_hip_render of (frame, rank, nranks) with exact
  * camera rays, re-derive its candidate lists on the host from the same code

@@ -57,7 +57,7 @@ struct CandParams {
 // the device count pass disagrees with the tiles the raster emits.
 extern "C" int rt_cand_survey_host(const CandParams* p, const float* tri, const float* node,
                                    const uint32_t* prim_leaf, int threads,
-                                   unsigned long long out[36]);
+                                   unsigned long long out[72]);
 // Host check of one frame's device-built lists (tests; see rt_cand.hip)
 extern "C" int rt_cand_verify_host(const CandParams* p, const float* tri, const float* node,
                                    const uint32_t* prim_leaf, const uint32_t* list, uint32_t nlist,

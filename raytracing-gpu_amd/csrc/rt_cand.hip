@@ -106,7 +106,11 @@ RTC_FN double pt_tri_dist(const double* x, const double* a, const double* b, con
 }
 
 // Classify one triangle (record r: v0, e1, e2 as floats) and build its footprint.
-RTC_FN int classify(const CandParams& p, const float* r, const float* leafbox, Footprint& fp) {
+// td (optional, FOOTPRINT only): the bounding box of T_D(cl) (lo xyz, hi xyz)
+// and the distance error derr; td[6] = -1 when T_D has no bound for every
+// candidate line (c_ok > 0).
+RTC_FN int classify(const CandParams& p, const float* r, const float* leafbox, Footprint& fp,
+                    double* td = nullptr) {
   const double v0[3] = {r[0], r[1], r[2]}, e1[3] = {r[3], r[4], r[5]}, e2[3] = {r[6], r[7], r[8]};
   const double v1[3] = {v0[0] + e1[0], v0[1] + e1[1], v0[2] + e1[2]};
   const double v2[3] = {v0[0] + e2[0], v0[1] + e2[1], v0[2] + e2[2]};
@@ -264,6 +268,13 @@ RTC_FN int classify(const CandParams& p, const float* r, const float* leafbox, F
   // depth skip: new_dist >= |pos - o| + |X - pos| - 2 dline - derr
   const double sk = c_ok > 0.0 ? -1e30 : rmin - 2.0 * p.dline - derr - 1e-6 * (p.lmax + rmax) - 1e-3;
   fp.skip = sk > 0.0 ? (float)(sk * (1.0 - 1e-6)) : -1e30f;
+  if (td) {
+    for (int a = 0; a < 3; a++) {
+      td[a] = fmin(P[0][a], fmin(P[1][a], P[2][a]));
+      td[3 + a] = fmax(P[0][a], fmax(P[1][a], P[2][a]));
+    }
+    td[6] = c_ok > 0.0 ? -1.0 : derr;
+  }
   return FOOTPRINT;
 }
 
@@ -846,20 +857,26 @@ extern "C" hipError_t rt_cand_prim_leaf(const float4* node, uint32_t nnode, cons
 
 extern "C" int rt_cand_survey_host(const CandParams* p, const float* tri, const float* node,
                                    const uint32_t* prim_leaf, int threads,
-                                   unsigned long long out[36]) {
+                                   unsigned long long out[72]) {
   // out: [0] safe, [1] footprint, [2] global, [3] entries, [4 + k] prims
-  // with 2^k <= entries < 2^(k+1), [20 + k] their entries (k < 16)
+  // with 2^k <= entries < 2^(k+1), [20 + k] their entries (k < 16);
+  // [36 + k] footprint prims whose T_D box (grown by the distance error
+  // beyond the pruning margin) reaches beyond the triangle's own box by
+  // g with 2^(k-8) <= g / eps_avail < 2^(k-7) (k = 0: below 2^-7; k = 15:
+  // 2^7 and more, or unbounded), [52 + k] their entries
   if (threads < 1) threads = 1;
-  std::vector<unsigned long long> part(36 * (size_t)threads, 0);
+  std::vector<unsigned long long> part(72 * (size_t)threads, 0);
   std::vector<unsigned long long> bad((size_t)threads, 0);
   std::vector<std::thread> th;
   for (int t = 0; t < threads; t++)
     th.emplace_back([=, &part, &bad]() {
-      unsigned long long* o = &part[36 * (size_t)t];
+      unsigned long long* o = &part[72 * (size_t)t];
       for (uint32_t i = (uint32_t)t; i < p->nprim; i += (uint32_t)threads) {
         rtc::Footprint fp;
         const float* lb = prim_leaf ? node + 8 * (size_t)prim_leaf[i] : nullptr;
-        const int c = rtc::classify(*p, tri + 12 * (size_t)i, lb, fp);
+        double td[7];
+        const float* rec = tri + 12 * (size_t)i;
+        const int c = rtc::classify(*p, rec, lb, fp, td);
         o[c]++;
         if (c == rtc::FOOTPRINT) {
           unsigned long long v = 0;
@@ -887,13 +904,26 @@ extern "C" int rt_cand_survey_host(const CandParams* p, const float* tri, const 
             o[4 + k]++;
             o[20 + k] += v;
           }
+          double g = 1e300;
+          if (td[6] >= 0.0) {
+            g = fmax(0.0, td[6] - 2.0 * p->eps_avail);
+            for (int a = 0; a < 3; a++) {
+              const double lo = fmin((double)rec[a], fmin((double)rec[a] + rec[3 + a], (double)rec[a] + rec[6 + a]));
+              const double hi = fmax((double)rec[a], fmax((double)rec[a] + rec[3 + a], (double)rec[a] + rec[6 + a]));
+              g = fmax(g, fmax(lo - td[a], td[3 + a] - hi) + fmax(0.0, td[6] - 2.0 * p->eps_avail));
+            }
+          }
+          int kg = 0;
+          while (kg < 15 && g >= p->eps_avail * std::ldexp(1.0, kg - 7)) kg++;
+          o[36 + kg]++;
+          o[52 + kg] += v;
         }
       }
     });
   for (auto& x : th) x.join();
-  for (int k = 0; k < 36; k++) {
+  for (int k = 0; k < 72; k++) {
     out[k] = 0;
-    for (int t = 0; t < threads; t++) out[k] += part[36 * (size_t)t + k];
+    for (int t = 0; t < threads; t++) out[k] += part[72 * (size_t)t + k];
   }
   unsigned long long nbad = 0;
   for (int t = 0; t < threads; t++) nbad += bad[t];

@@ -484,7 +484,7 @@ extern "C" int rt_hip_set_camera_bound_scale(rt_hip_ctx* c, double scale) {
 }
 
 extern "C" int rt_cand_survey(const rt_scene* scene, float eps_ulps, double bound_scale, int threads,
-                              int use_leaves, unsigned long long out[36]) {
+                              int use_leaves, unsigned long long out[72]) {
   if (!scene || !out) return rt_set_error(RT_EINVAL, "null argument");
   rt_frame f;
   int rc = rt_frame_from_camera(&scene->camera, &f);

@@ -346,11 +346,15 @@ def accel_probe(scene, accel="octree", stride=97, check=True):
 def cand_survey(scene, eps_ulps=64.0, bound_scale=1.0, threads=8, leaves=False):
     """Host-only: {safe, footprint, global, entries} of the camera candidate
     lists of the scene's frame (csrc/rt_cand.hip classify + raster)."""
-    out = (C.c_ulonglong * 36)()
+    out = (C.c_ulonglong * 72)()
     _check(lib().rt_cand_survey(scene.ptr, eps_ulps, bound_scale, threads, 1 if leaves else 0, out),
            "cand_survey")
     r = dict(zip(("safe", "footprint", "global", "entries"), (int(x) for x in out[:4])))
     r["hist"] = [(1 << k, int(out[4 + k]), int(out[20 + k])) for k in range(16) if out[4 + k]]
+    # footprint prims by how far their T_D box reaches beyond the triangle, in
+    # units of the walk's slack: (lower edge 2^(k-8), prims, entries)
+    r["growth_hist"] = [(2.0 ** (k - 8) if k else 0.0, int(out[36 + k]), int(out[52 + k]))
+                        for k in range(16) if out[36 + k]]
     return r
 
 

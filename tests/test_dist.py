@@ -4,7 +4,6 @@ N, csrc/rt_tiles.h), rank 0 gathers them rank-major exactly as bench.py does
 with RCCL, and the assemble index map (mirrored from the HIP assemble kernel)
 restores the PPM-order image."""
 import os
-import socket
 import sys
 
 import numpy as np
@@ -14,19 +13,13 @@ import torch.multiprocessing as mp
 from conftest import REPO, golden_image, load_manifest_static
 
 
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
-def _worker(rank, world, port, case, q):
+def _worker(rank, world, store, case, q):
     import torch
     import torch.distributed as dist
     sys.path.insert(0, os.path.join(REPO, "raytracing-gpu_amd"))
     import rtgpu
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # a file rendezvous: no port to race for with other tests on the machine
+    dist.init_process_group("gloo", init_method="file://" + store, rank=rank, world_size=world)
     img = golden_image(case)
     mine = torch.from_numpy(rtgpu.tiles_from_image_numpy(img, rank, world).ravel().copy())
     per = mine.numel()
@@ -40,13 +33,13 @@ def _worker(rank, world, port, case, q):
 
 @pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.parametrize("size", [(96, 54), (192, 108)])
-def test_gather_assemble_gloo(world, size):
+def test_gather_assemble_gloo(world, size, tmp_path):
     case = next(c for c in load_manifest_static()
                 if (c["width"], c["height"]) == size and c["scene"] == "island_smooth")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, case, q)) for r in range(world)]
+    store = str(tmp_path / "rendezvous")
+    procs = [ctx.Process(target=_worker, args=(r, world, store, case, q)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
