@@ -429,7 +429,10 @@ def main():
                 "width": W, "height": H, "triangles": ntri, "accel": wl["accel"],
                 "accel_build": {"seconds": round(info["build_seconds"], 3),
                                 "where": "device" if wl["accel"] == "octree_gpu" else "host",
-                                "records": info["tri_refs"], "nodes": info["nodes"]},
+                                "records": info["tri_refs"], "nodes": info["nodes"],
+                                "light_buffer_entries": info["lightbuf_entries"],
+                                "light_buffer_global": info["lightbuf_global"],
+                                "light_buffer_seconds": round(info["lightbuf_seconds"], 3)},
                 "parallelism": f"image tiles over {world} GPU(s) + RCCL gather" if world > 1
                                else "1 GPU",
                 "queries_per_frame": {"closest": int(closest), "shadow": int(shadow),

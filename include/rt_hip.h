@@ -105,6 +105,12 @@ typedef struct rt_accel_info {
    * multiplier of the shadow walk's culling slack */
   unsigned long long shadow_global;
   double shadow_mu_max;
+  /* light buffers of the default shadow queries (csrc/rt_lightbuf.hip):
+   * cell entries over all lights, and triangles every query of their light
+   * tests (footprint unbounded) */
+  unsigned long long lightbuf_entries;
+  unsigned long long lightbuf_global;
+  double lightbuf_seconds;             /* their build time (device, at rt_hip_create) */
 } rt_accel_info;
 
 /* Host-only: build the acceleration structure rt_hip_create would build and
@@ -208,6 +214,12 @@ int rt_hip_set_exact_camera(rt_hip_ctx *ctx, int enable);
  * shadow rays graze the surfaces, the bound grows like 1/cos: on C5 it
  * costs ~160x the shade time.  Default: the plain slack, whose shadow
  * decisions are verified against brute force (rt_hip_verify_shadows). */
+/* Light buffers for the shadow queries of the default walk (1, the default):
+ * per directional / point light a grid over the light's view whose cells list
+ * the triangles a shadow ray starting there can meet (csrc/rt_lightbuf.hip),
+ * built once per scene and slack; 0: every shadow query walks the octree.
+ * Both are exact in the same sense (DESIGN.md §2 "Shadow rays"). */
+int rt_hip_set_light_buffers(rt_hip_ctx *ctx, int enable);
 int rt_hip_set_exact_shadows(rt_hip_ctx *ctx, int enable);
 /* Octree traversal policy (default 0): 0 = staged packet walk for coherent
  * closest-hit queries, per-lane walks otherwise; 1 = every query per lane;

@@ -19,6 +19,7 @@
 #include "rt_build.h"
 #include "rt_cand.h"
 #include "rt_kernels.h"
+#include "rt_lightbuf.h"
 #include "rt_shadow.h"
 #include "rt_tiles.h"
 
@@ -81,6 +82,12 @@ struct rt_hip_ctx {
   int grid_of[2][4][2] = {};        // persistent grids [trace][policy][count_work]
   int cus = 0;                      // compute units of the device
   std::vector<uint32_t> light_type; // per light (rt_hip_verify_shadows)
+  std::vector<float> light_v;       // per light: l.v (3 floats)
+  // light buffers (csrc/rt_lightbuf.hip), built for the slack lb_ulps
+  int light_buffers = 1;            // rt_hip_set_light_buffers
+  std::vector<LBDevice*> lb_dev;    // per light (nullptr: the walk)
+  RtLightBuf* d_lbuf = nullptr;     // per light, device
+  float lb_ulps = -1.0f;
   KParams last_p{};                 // the last render's parameters (rt_hip_verify_shadows)
   // exact shadow rays (csrc/rt_shadow.hip), built for the slack sh_ulps
   float2* d_prim_mu = nullptr;
@@ -193,6 +200,8 @@ extern "C" void rt_hip_destroy(rt_hip_ctx* c) {
   (void)hipFree(c->d_prim_mu);
   (void)hipFree(c->d_node_mu);
   (void)hipFree(c->d_sh_global);
+  for (LBDevice* d : c->lb_dev) rt_lightbuf_free(d);
+  (void)hipFree(c->d_lbuf);
   if (c->d_tri_prim != c->d_tri) (void)hipFree(c->d_tri_prim);
   (void)hipFree(c->d_cand_list);
   (void)hipFree(c->d_cand_fp);
@@ -274,6 +283,92 @@ static int shadow_prepare(rt_hip_ctx* c, hipStream_t s) {
   c->sh_ulps = c->eps_ulps;
   c->info.shadow_global = n;
   c->info.shadow_mu_max = nm[0].x;
+  return RT_OK;
+}
+
+// Light buffers of the scene's directional and point lights for the
+// context's culling slack (csrc/rt_lightbuf.hip): once per scene and slack,
+// synchronous (setup).  The shadow queries of the default walk then look up
+// the cells their origins project to instead of walking the octree.
+static void lbuf_release(rt_hip_ctx* c) {
+  for (LBDevice*& d : c->lb_dev) {
+    rt_lightbuf_free(d);
+    d = nullptr;
+  }
+  (void)hipFree(c->d_lbuf);
+  c->d_lbuf = nullptr;
+  c->lb_ulps = -1.0f;
+}
+
+static int lbuf_prepare(rt_hip_ctx* c, hipStream_t s) {
+  if (!c->light_buffers || c->accel != RT_ACCEL_OCTREE || !c->d_node || !c->nlight) return RT_OK;
+  if (c->d_lbuf && c->lb_ulps == c->eps_ulps) return RT_OK;
+  lbuf_release(c);
+  c->lb_dev.assign(c->nlight, nullptr);
+  std::vector<RtLightBuf> hb(c->nlight);
+  std::memset(hb.data(), 0, hb.size() * sizeof(RtLightBuf));
+  // a shadow ray leaves a hit point: inside the scene cube up to the float
+  // error of the hit, so its slack eps(o) (host/rt_cull.h, float) is at most
+  const double R = c->scene_r, eps_rel = (double)(c->eps_ulps * 5.9604645e-8f);
+  const double cmag = std::fmax(std::fabs(c->scene_c[0]), std::fmax(std::fabs(c->scene_c[1]),
+                                                                  std::fabs(c->scene_c[2])));
+  const double slack = (eps_rel * (2.0 * R * 1.001 + 1e-3) + (double)RT_CULL_PLANE * (cmag + R) + 1e-6) * 1.01;
+  double lo[3], hi[3], s1 = 0.0;
+  for (int a = 0; a < 3; a++) {
+    lo[a] = c->scene_c[a] - R * 1.001 - 1e-3;
+    hi[a] = c->scene_c[a] + R * 1.001 + 1e-3;
+    s1 += std::fmax(std::fabs(lo[a]), std::fabs(hi[a]));
+  }
+  char err[256] = {0};
+  for (uint32_t li = 0; li < c->nlight; li++) {
+    const uint32_t t = c->light_type[li];
+    if (t != 1 && t != 2) continue;
+    LBParams lp;
+    std::memset(&lp, 0, sizeof lp);
+    lp.tri = c->d_tri_prim;
+    lp.nprim = c->nprim;
+    lp.kind = t == 1 ? RT_LB_DIR : RT_LB_POINT;
+    double dmax = 0.0;
+    for (int a = 0; a < 3; a++) {
+      lp.lv[a] = c->light_v[3 * li + a];
+      lp.box_lo[a] = lo[a];
+      lp.box_hi[a] = hi[a];
+    }
+    for (int k = 0; k < 8; k++) {
+      double d2 = 0.0;
+      for (int a = 0; a < 3; a++) {
+        const double x = ((k >> a) & 1 ? hi[a] : lo[a]) - lp.lv[a];
+        d2 += x * x;
+      }
+      dmax = std::fmax(dmax, std::sqrt(d2));
+    }
+    lp.slack = slack;
+    lp.s1 = s1;
+    lp.dmax = dmax * 1.01 + 1.0;
+    lp.target_cells = c->nprim < 4096u ? 4096u : (c->nprim > (1u << 24) ? (1u << 24) : c->nprim);
+    if (rt_lightbuf_build(&lp, &hb[li], &c->lb_dev[li], s, err, sizeof err)) {
+      lbuf_release(c);
+      return rt_set_error(RT_EHIP, "light buffer of light %u: %s", li, err);
+    }
+  }
+  HIP_TRY(hipMalloc((void**)&c->d_lbuf, hb.size() * sizeof(RtLightBuf)));
+  HIP_TRY(hipMemcpy(c->d_lbuf, hb.data(), hb.size() * sizeof(RtLightBuf), hipMemcpyHostToDevice));
+  c->lb_ulps = c->eps_ulps;
+  unsigned long long e = 0, n = 0, g = 0, te = 0, tg = 0;
+  for (LBDevice* d : c->lb_dev) {
+    rt_lightbuf_sizes(d, &e, &n, &g);
+    te += e;
+    tg += g;
+  }
+  c->info.lightbuf_entries = te;
+  c->info.lightbuf_global = tg;
+  return RT_OK;
+}
+
+extern "C" int rt_hip_set_light_buffers(rt_hip_ctx* c, int enable) {
+  if (!c) return rt_set_error(RT_EINVAL, "null context");
+  c->light_buffers = enable ? 1 : 0;
+  if (!c->light_buffers) lbuf_release(c);
   return RT_OK;
 }
 
@@ -385,7 +480,12 @@ extern "C" int rt_hip_create(int device, const rt_scene* scene, int accel, rt_hi
   // keeps 16 per CU
   c->grid = prop.multiProcessorCount * 16;
   c->cus = prop.multiProcessorCount;
-  for (size_t li = 0; li < scene->light_count; li++) c->light_type.push_back((uint32_t)scene->lights[li].type);
+  for (size_t li = 0; li < scene->light_count; li++) {
+    c->light_type.push_back((uint32_t)scene->lights[li].type);
+    c->light_v.push_back(scene->lights[li].v.x);
+    c->light_v.push_back(scene->lights[li].v.y);
+    c->light_v.push_back(scene->lights[li].v.z);
+  }
   int gmax = c->grid;
   const int dacc = c->accel == RT_ACCEL_FLAT ? RT_ACCEL_FLAT_D : RT_ACCEL_OCTREE_D;
   for (int tr = 0; tr < 2; tr++)
@@ -405,6 +505,15 @@ extern "C" int rt_hip_create(int device, const rt_scene* scene, int accel, rt_hi
       hipMalloc((void**)&c->d_spill, (size_t)gmax * 64 * RT_SPILL_STACK * sizeof(uint2)) != hipSuccess) {
     rt_hip_destroy(c);
     return rt_set_error(RT_EHIP, "hipMalloc traversal spill stack");
+  }
+  {  // light buffers: part of the scene's setup, like the octree
+    const auto l0 = std::chrono::steady_clock::now();
+    rc = lbuf_prepare(c, c->stream);
+    c->info.lightbuf_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - l0).count();
+    if (rc) {
+      rt_hip_destroy(c);
+      return rc;
+    }
   }
   *out = c;
   return RT_OK;
@@ -1008,6 +1117,11 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
   {
     int rc = shadow_prepare(c, s);  // no-op unless the culling slack changed
     if (rc) return rc;
+  }
+  if (!c->exact_shadows) {
+    int rc = lbuf_prepare(c, s);  // no-op unless the culling slack changed
+    if (rc) return rc;
+    if (c->policy == RT_POLICY_DEFAULT || c->policy == RT_POLICY_LANE) p.lbuf = c->d_lbuf;
   }
   if (c->exact_shadows) {
     p.node_mu = c->d_node_mu;

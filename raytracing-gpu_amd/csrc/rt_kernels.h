@@ -6,6 +6,7 @@
 #include <stdint.h>
 
 #include "rt_device.h"
+#include "rt_lightbuf.h"
 
 #define RT_ACCEL_FLAT_D 0
 #define RT_ACCEL_OCTREE_D 1
@@ -102,6 +103,8 @@ struct KParams {
   uint32_t shade_stride;
   // exact shadow rays (csrc/rt_shadow.hip): per-node (mu, nu) multipliers of
   // the shadow walk's slack, and the prims every unshadowed shadow ray tests
+  // light buffers (csrc/rt_lightbuf.hip), per light; NULL: every shadow query walks
+  const RtLightBuf* lbuf;
   const float2* node_mu;
   const uint32_t* sh_global;
   uint32_t n_sh_global;

@@ -1001,11 +1001,89 @@ __device__ __forceinline__ void closest_q(const KParams& p, const Ray& r, bool a
   }
 }
 
+// Shadow query through the light's buffer (csrc/rt_lightbuf.hip): the
+// triangles listed in the cell the ray's origin projects to, in key order,
+// up to the first any-hit -- for a point light also the opposite cell, whose
+// triangles lie beyond the light (cpu/rt's shadow ray does not stop there,
+// cpu/hit.c:93-109) -- then the light's global list.  Per lane.
+template <bool COUNT>
+__device__ bool lbuf_any(const KParams& p, const RtLightBuf& L, const Ray& r, LaneCount& lc) {
+  uint32_t cell[2] = {0xffffffffu, 0xffffffffu};
+  float lim = __builtin_inff();  // key limit of cell[0] (cell[1]: none)
+  if (L.kind == RT_LB_DIR) {
+    // the same float operations the build's margins assume (no contraction)
+    const float pu = r.o.x * L.u[0] + r.o.y * L.u[1] + r.o.z * L.u[2];
+    const float pv = r.o.x * L.v[0] + r.o.y * L.v[1] + r.o.z * L.v[2];
+    const float pw = r.o.x * L.w[0] + r.o.y * L.w[1] + r.o.z * L.w[2];
+    const float fx = (pu - L.u0) * L.inv_cs, fy = (pv - L.v0) * L.inv_cs;
+    if (fx >= 0.0f && fy >= 0.0f && fx < (float)L.nx && fy < (float)L.ny) {
+      cell[0] = (uint32_t)fy * L.nx + (uint32_t)fx;
+      lim = -pw;  // keys are minus the triangles' depth bounds toward the light
+    }
+  } else {
+    // from the light to the origin: -d, the ray's own direction negated
+    const f3 x{-r.d.x, -r.d.y, -r.d.z};
+    const float ax = fabsf(x.x), ay = fabsf(x.y), az = fabsf(x.z);
+    uint32_t a = 0;
+    float m = ax, xa = x.x, xj = x.y, xk = x.z;
+    if (ay > m) {
+      a = 1;
+      m = ay;
+      xa = x.y;
+      xj = x.z;
+      xk = x.x;
+    }
+    if (az > m) {
+      a = 2;
+      m = az;
+      xa = x.z;
+      xj = x.x;
+      xk = x.y;
+    }
+    if (m > 0.0f) {
+      const uint32_t n = L.nx;
+      const float sc = xj / m, tc = xk / m;
+      const uint32_t f = 2u * a + (xa < 0.0f ? 1u : 0u);
+      const uint32_t ix = min((uint32_t)((sc + 1.0f) * L.half_n), n - 1u);
+      const uint32_t iy = min((uint32_t)((tc + 1.0f) * L.half_n), n - 1u);
+      const uint32_t jx = min((uint32_t)((1.0f - sc) * L.half_n), n - 1u);
+      const uint32_t jy = min((uint32_t)((1.0f - tc) * L.half_n), n - 1u);
+      cell[0] = (f * n + iy) * n + ix;
+      cell[1] = ((f ^ 1u) * n + jy) * n + jx;
+      lim = length(x) * (1.0f + 1e-6f);  // keys: nearest distance from the light
+    }
+  }
+  for (int h = 0; h < 2; h++) {
+    if (cell[h] == 0xffffffffu) continue;
+    const float q = h == 0 ? lim : __builtin_inff();
+    const uint32_t e = L.start[cell[h] + 1];
+    for (uint32_t k = L.start[cell[h]]; k < e; k++) {
+      if (L.key[k] > q) break;
+      const uint32_t prim = L.prim[k];
+      const float4* t = p.tri_prim + 3 * (size_t)prim;
+      if (COUNT) {
+        lc.tris += lanes_distinct(prim);
+        lc.ltris++;
+      }
+      if (any_hit_rec(r, t[0], t[1], t[2], lc.risk)) return true;
+    }
+  }
+  for (uint32_t k = 0; k < L.nglobal; k++) {
+    const float4* t = p.tri_prim + 3 * (size_t)L.global[k];
+    if (COUNT) {
+      lc.tris += lanes_distinct(L.global[k]);
+      lc.ltris++;
+    }
+    if (any_hit_rec(r, t[0], t[1], t[2], lc.risk)) return true;
+  }
+  return false;
+}
+
 // Shadow query (collide_dist > 0.01, cpu/light.c:24-31) of a light of the
 // given type; converged call.
 template <int ACCEL, bool COUNT, int POL>
-__device__ __forceinline__ bool shadow_q(const KParams& p, f3 o, f3 d, uint32_t type, bool act,
-                                         Stack& s, WaveCtx& w, WorkCount& wc) {
+__device__ __forceinline__ bool shadow_q(const KParams& p, f3 o, f3 d, uint32_t type, uint32_t li,
+                                         bool act, Stack& s, WaveCtx& w, WorkCount& wc) {
   uint64_t am = __ballot(act);
   wc.shadow += (uint32_t)__popcll(am);
   Ray r = make_ray(p, o, d, p.eps_rel);
@@ -1016,6 +1094,10 @@ __device__ __forceinline__ bool shadow_q(const KParams& p, f3 o, f3 d, uint32_t 
   bool hit;
   if (staged) {
     hit = staged_any<COUNT>(p, r, act, w, wc);
+  } else if (p.lbuf && p.lbuf[li].kind != RT_LB_NONE) {
+    LaneCount lc = {0, 0, 0, 0, 0, 0, 0};
+    hit = act && lbuf_any<COUNT>(p, p.lbuf[li], r, lc);
+    absorb<COUNT>(wc, lc, true);
   } else {
     LaneCount lc = {0, 0, 0, 0, 0, 0, 0};
     hit = act && oct_any<COUNT>(p, r, s, lc);
@@ -1106,7 +1188,7 @@ __device__ col apply_light(const KParams& p, bool hit, const float* m, f3 P, f3 
       if (hit) acc = color_add(acc, color_mul2(lc, init_color(m[0], m[1], m[2])));
     } else if (type == 1 || type == 2) {
       const uint64_t c0 = COUNT ? __builtin_readcyclecounter() : 0ull;
-      bool sh = shadow_q<ACCEL, COUNT, POL>(p, P, shadow_dir(type, lv, P), type, hit, s, w, wc);
+      bool sh = shadow_q<ACCEL, COUNT, POL>(p, P, shadow_dir(type, lv, P), type, li, hit, s, w, wc);
       if (COUNT) {
         const uint32_t dc = (uint32_t)(__builtin_readcyclecounter() - c0);
         wc.cy_shadow += dc;
@@ -1429,7 +1511,7 @@ __device__ __forceinline__ col shade_record(const KParams& p, bool valid, size_t
         if (type != 1 && type != 2) continue;
         const f3 lv = f3{L[4], L[5], L[6]};
         const uint64_t c0 = COUNT ? __builtin_readcyclecounter() : 0ull;
-        const bool sh = shadow_q<ACCEL, COUNT, POL>(p, P, shadow_dir(type, lv, P), type, valid, s, w, wc);
+        const bool sh = shadow_q<ACCEL, COUNT, POL>(p, P, shadow_dir(type, lv, P), type, li, valid, s, w, wc);
         if (COUNT) {
           const uint32_t dc = (uint32_t)(__builtin_readcyclecounter() - c0);
           wc.cy_shadow += dc;
@@ -1621,7 +1703,7 @@ __device__ col apply_light8(const KParams& p, bool hit, const float* m, f3 P, f3
     if (type == 0) {
       if (hit) acc = add8(acc, mults8(lc, init8(m[0], m[1], m[2])));
     } else if (type == 1 || type == 2) {
-      bool sh = shadow_q<ACCEL, false, POL>(p, P, shadow_dir(type, lv, P), type, hit, s, w, wc);
+      bool sh = shadow_q<ACCEL, false, POL>(p, P, shadow_dir(type, lv, P), type, li, hit, s, w, wc);
       if (hit && !sh) acc = add8(acc, light_lit8(type, lc, lv, m, P, N));
     }
   }

@@ -107,7 +107,8 @@ class AccelInfo(C.Structure):
                 ("tri_record_bytes", C.c_ulonglong), ("node_record_bytes", C.c_ulonglong),
                 ("device_bytes", C.c_ulonglong), ("build_seconds", C.c_double),
                 ("max_leaf", C.c_ulonglong), ("shadow_global", C.c_ulonglong),
-                ("shadow_mu_max", C.c_double)]
+                ("shadow_mu_max", C.c_double), ("lightbuf_entries", C.c_ulonglong),
+                ("lightbuf_global", C.c_ulonglong), ("lightbuf_seconds", C.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -154,6 +155,7 @@ _PROTOS = [
     ("rt_hip_set_exact_camera", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_set_policy", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_set_exact_shadows", C.c_int, [C.c_void_p, C.c_int]),
+    ("rt_hip_set_light_buffers", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_tile_cycles", C.c_int, [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_size_t]),
     ("rt_hip_tile_phase_cycles", C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_ulonglong),
                                            C.c_size_t]),
@@ -439,6 +441,10 @@ class Context:
                                               out.ctypes.data_as(C.POINTER(C.c_ulonglong)), n),
                "tile_phase_cycles")
         return out
+
+    def set_light_buffers(self, on=True):
+        """Light buffers for the default shadow queries (rt_hip_set_light_buffers)."""
+        _check(lib().rt_hip_set_light_buffers(self.h, 1 if on else 0), "light_buffers")
 
     def set_exact_shadows(self, on=True):
         """Proven shadow walk (rt_hip_set_exact_shadows; slow near terminators)."""

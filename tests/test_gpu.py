@@ -353,17 +353,24 @@ def test_synthetic_full_frame_exact(gpu, accel):
     assert_bitexact(img_f[pix[:, 0], pix[:, 1]], vals, "synthetic brute force vs oracle")
 
 
-@pytest.mark.parametrize("accel,policy,exact", [("octree_gpu", 0, False), ("octree", 0, False),
-                                                ("octree_gpu", 3, False), ("octree_gpu", 0, True),
-                                                ("octree", 2, True)])
-def test_shadow_queries_match_brute_force(gpu, accel, policy, exact):
+@pytest.mark.parametrize("accel,policy,exact,lbuf", [("octree_gpu", 0, False, True),
+                                                     ("octree", 0, False, True),
+                                                     ("octree_gpu", 0, False, False),
+                                                     ("octree_gpu", 3, False, True),
+                                                     ("octree_gpu", 0, True, True),
+                                                     ("octree", 2, True, True)])
+def test_shadow_queries_match_brute_force(gpu, accel, policy, exact, lbuf):
     """Every shadow query of a frame (the shade kernel's per-record outcome of
-    cpu/light.c:24-31 for each light) through the octree walk equals brute
-    force over all triangles (cpu/hit.c:93-109) on the same hit records --
-    shadow rays leave surfaces at grazing angles near the terminators, where
-    the float Moller-Trumbore test is least conditioned."""
+    cpu/light.c:24-31 for each light) through the light buffers (default) or
+    the octree walk equals brute force over all triangles (cpu/hit.c:93-109)
+    on the same hit records -- shadow rays leave surfaces at grazing angles
+    near the terminators, where the float Moller-Trumbore test is least
+    conditioned."""
     s = gpu.Scene.synthetic(6, 6, 9776, seed=0x5EED, width=960, height=540)
     ctx = gpu.Context(s, accel)
+    if lbuf and not exact and policy == 0:
+        assert ctx.info()["lightbuf_entries"] > 0
+    ctx.set_light_buffers(lbuf)
     ctx.set_policy(policy)
     if exact:  # the proven shadow walk (csrc/rt_shadow.hip)
         ctx.set_exact_shadows(True)
@@ -372,6 +379,28 @@ def test_shadow_queries_match_brute_force(gpu, accel, policy, exact):
     v = ctx.verify_shadows(1)
     assert v["records"] > 100000 and v["queries"] == 2 * v["records"], v
     assert v["records_differ"] == 0 and v["walk_lit_brute_shadowed"] == 0, v
+
+
+@pytest.mark.parametrize("height", [0.02, 0.5])
+def test_light_buffer_point_light_near_surface(gpu, height):
+    """A point light just above a sphere: triangles around it span wide
+    angles of the light's cube map (or go to its global list); every shadow
+    query still equals brute force, and the image equals the walk's."""
+    s = gpu.Scene.synthetic(4, 4, 9776, seed=0x5EED, width=480, height=270)
+    tri = s.triangles_array()
+    top = tri[2 + 5 * 9776: 2 + 6 * 9776, :3].reshape(-1, 3)  # sphere 5's vertices
+    k = int(np.argmax(top[:, 1]))
+    L = s.s.lights[2]
+    assert int(L.type) == 2
+    L.v.x, L.v.y, L.v.z = float(top[k, 0]), float(top[k, 1]) + height, float(top[k, 2])
+    f = s.frame()
+    ctx = gpu.Context(s, "octree_gpu")
+    img, _ = ctx.render_image(f)
+    v = ctx.verify_shadows(1)
+    assert v["records"] > 10000 and v["records_differ"] == 0 and v["walk_lit_brute_shadowed"] == 0, v
+    ctx.set_light_buffers(False)
+    img_w, _ = ctx.render_image(f)
+    assert_bitexact(img, img_w, f"light buffers vs walk, light {height} above a sphere")
 
 
 def test_exact_camera_rank_split(gpu):
