@@ -56,6 +56,11 @@ struct Foot {
   bool plane;
   double pn_u, pn_v, pn_w, pn_d;  // n.u, n.v, n.w, n.v0 of the triangle's plane
   double m;                       // footprint margin (world units)
+  // per rect: the triangle's image in the rect's coordinates (DIR: u, v;
+  // POINT: the face's (s, t)) and its margin there, for the cell overlap
+  // test of small footprints; tri_ok = 0: bounding rect only
+  bool tri_ok[kMaxRects];
+  double tx[kMaxRects][3], ty[kMaxRects][3], tm[kMaxRects];
 };
 
 __device__ inline double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
@@ -83,6 +88,7 @@ __device__ void footprint(const BP& p, uint32_t prim, Foot& f) {
   f.n = 0;
   f.global = false;
   f.plane = false;
+  for (int q = 0; q < kMaxRects; q++) f.tri_ok[q] = false;
   if (p.kind == RT_LB_DIR) {
     // the query's float projection of its origin is within 3 eps s1 of the
     // exact one; the triangle's points are within the slack of the ray
@@ -95,7 +101,11 @@ __device__ void footprint(const BP& p, uint32_t prim, Foot& f) {
       lvv = fmin(lvv, b);
       hvv = fmax(hvv, b);
       hw = fmax(hw, c);
+      f.tx[0][k] = a;
+      f.ty[0][k] = b;
     }
+    f.tri_ok[0] = true;
+    f.tm[0] = m;
     f.n = 1;
     f.face[0] = 0;
     f.x0[0] = clampi(floor((lu - m - p.u0) * p.inv_cs - 0.01), (int)p.nx - 1);
@@ -159,6 +169,29 @@ __device__ void footprint(const BP& p, uint32_t prim, Foot& f) {
       if (slo > 1.0 + 1e-9 || shi < -1.0 - 1e-9 || tlo > 1.0 + 1e-9 || thi < -1.0 - 1e-9) continue;
       const int q = f.n++;
       f.face[q] = (uint32_t)(2 * a + sg);
+      // the triangle's central projection onto the face (valid when every
+      // vertex lies well on the face's side), grown by the cone's widening
+      // beta (slack / rmin + alpha) through the face map's Lipschitz bound
+      {
+        const double beta = p.slack / rmin + alpha;
+        const double sgn = sg == 0 ? 1.0 : -1.0;
+        double xamin = 1e300, smax = 1.0;
+        bool ok = true;
+        for (int v = 0; v < 3 && ok; v++) {
+          const double X[3] = {V[v][0] - p.lv[0], V[v][1] - p.lv[1], V[v][2] - p.lv[2]};
+          const double xl = sqrt(dot3(X, X)), xa = sgn * X[a];
+          ok = xl > 0.0 && xa > 1e-3 * xl;
+          if (!ok) break;
+          xamin = fmin(xamin, xa / xl);
+          f.tx[q][v] = X[j] / xa;
+          f.ty[q][v] = X[k] / xa;
+          smax = fmax(smax, fmax(fabs(f.tx[q][v]), fabs(f.ty[q][v])));
+        }
+        if (ok && xamin > 4.0 * beta) {
+          f.tri_ok[q] = true;
+          f.tm[q] = 2.0 * beta * (1.0 + smax + 2.0 * beta) / (xamin - 2.0 * beta) * 1.01 + 1e-9;
+        }
+      }
       f.x0[q] = clampi(floor((fmax(slo, -1.0) + 1.0) * hn - 0.01), (int)p.n - 1);
       f.x1[q] = clampi(floor((fmin(shi, 1.0) + 1.0) * hn + 0.01), (int)p.n - 1);
       f.y0[q] = clampi(floor((fmax(tlo, -1.0) + 1.0) * hn - 0.01), (int)p.n - 1);
@@ -195,6 +228,47 @@ __device__ inline float cell_key(const BP& p, const Foot& f, int x, int y) {
   return __double2float_rd(key);
 }
 
+// Can the triangle's grown image in rect q reach cell (x, y)?  Separating
+// axis test of the cell square (grown by the margin) against the image's edge
+// lines; conservative (true when unsure: degenerate images, rect-only).
+__device__ inline bool cell_overlaps(const BP& p, const Foot& f, int q, int x, int y) {
+  if (!f.tri_ok[q]) return true;
+  double ox, oy, cs;
+  if (p.kind == RT_LB_DIR) {
+    ox = p.u0;
+    oy = p.v0;
+    cs = p.cs;
+  } else {
+    cs = 2.0 / (double)p.n;
+    ox = oy = -1.0;
+  }
+  // the query's own cell index is within 0.01 cells of its exact position
+  // (the bounding rects' margin): the square grows by as much
+  const double M = f.tm[q] + 0.01 * cs;
+  const double xa = ox + x * cs - M, xb = ox + (x + 1) * cs + M;
+  const double ya = oy + y * cs - M, yb = oy + (y + 1) * cs + M;
+  const double* X = f.tx[q];
+  const double* Y = f.ty[q];
+  const double area = (X[1] - X[0]) * (Y[2] - Y[0]) - (X[2] - X[0]) * (Y[1] - Y[0]);
+  const double scale = fabs(X[1] - X[0]) + fabs(X[2] - X[0]) + fabs(Y[1] - Y[0]) + fabs(Y[2] - Y[0]);
+  if (!(fabs(area) > 1e-9 * scale * scale)) return true;  // (nearly) degenerate image: keep
+  for (int e = 0; e < 3; e++) {
+    const int a = e, b = (e + 1) % 3;
+    // inward normal of edge a -> b (toward the third vertex)
+    double nx = -(Y[b] - Y[a]), ny = X[b] - X[a];
+    if (area < 0.0) {
+      nx = -nx;
+      ny = -ny;
+    }
+    // the square is outside when all its corners are beyond the edge line
+    const double cx = nx > 0.0 ? xb : xa, cy = ny > 0.0 ? yb : ya;  // the corner farthest inward
+    const double d = nx * (cx - X[a]) + ny * (cy - Y[a]);
+    const double tol = 1e-9 * (fabs(nx) + fabs(ny)) * (fabs(cx) + fabs(cy) + fabs(X[a]) + fabs(Y[a]) + cs);
+    if (d < -tol) return false;
+  }
+  return true;
+}
+
 __device__ inline uint32_t cell_index(const BP& p, const Foot& f, int q, int x, int y) {
   if (p.kind == RT_LB_DIR) return (uint32_t)y * p.nx + (uint32_t)x;
   return f.face[q] * p.n * p.n + (uint32_t)y * p.n + (uint32_t)x;
@@ -210,7 +284,14 @@ __global__ __launch_bounds__(256) void count_kernel(BP p) {
     p.global[atomicAdd(p.ctr + 1, 1u)] = prim;
   } else {
     c = foot_cells(p, f);
-    if (c > kSmallCells) p.big[atomicAdd(p.ctr, 1u)] = prim;
+    if (c > kSmallCells) {
+      p.big[atomicAdd(p.ctr, 1u)] = prim;  // emitted rect-wise by a workgroup
+    } else {
+      c = 0;  // small: only the cells the grown image overlaps
+      for (int q = 0; q < f.n; q++)
+        for (int y = f.y0[q]; y <= f.y1[q]; y++)
+          for (int x = f.x0[q]; x <= f.x1[q]; x++) c += cell_overlaps(p, f, q, x, y) ? 1u : 0u;
+    }
   }
   p.count[prim] = (uint32_t)c;  // the host checks the total against 2^32
 }
@@ -233,11 +314,19 @@ __global__ __launch_bounds__(256) void emit_kernel(BP p) {
   const uint32_t prim = blockIdx.x * blockDim.x + threadIdx.x;
   if (prim >= p.nprim) return;
   const uint32_t c = p.count[prim];
-  if (c == 0 || c > kSmallCells) return;
+  if (c == 0) return;
   Foot f;
   footprint(p, prim, f);
-  const uint64_t o = p.off[prim];
-  for (uint32_t i = 0; i < c; i++) emit_cell(p, f, prim, i, o + i);
+  if (foot_cells(p, f) > kSmallCells) return;  // big: emit_big_kernel
+  uint64_t at = p.off[prim];
+  for (int q = 0; q < f.n; q++)
+    for (int y = f.y0[q]; y <= f.y1[q]; y++)
+      for (int x = f.x0[q]; x <= f.x1[q]; x++)
+        if (cell_overlaps(p, f, q, x, y)) {
+          p.keys[at] = ((unsigned long long)cell_index(p, f, q, x, y) << 32) | orderable(cell_key(p, f, x, y));
+          p.vals[at] = prim;
+          at++;
+        }
 }
 
 // one workgroup per big footprint (ground planes, triangles near a point light)
