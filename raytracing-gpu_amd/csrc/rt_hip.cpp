@@ -908,7 +908,15 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
   }
   cp.node = c->d_node;
   cp.prim_leaf = c->d_prim_leaf;
-  if (!c->d_cand_global) {
+  if (!c->h_cand) {
+    // h_cand is allocated last: a partial set left by an earlier failure is
+    // freed here, never allocated over
+    for (void** b : {(void**)&c->d_cand_list, &c->d_cand_fp, (void**)&c->d_cand_visits, (void**)&c->d_cand_off,
+                     (void**)&c->d_cand_global, (void**)&c->d_cand_big, (void**)&c->d_cand_ctr,
+                     (void**)&c->d_cand_skip, (void**)&c->d_cand_big_lane}) {
+      (void)hipFree(*b);
+      *b = nullptr;
+    }
     HIP_TRY(hipMalloc((void**)&c->d_cand_list, (np + 1) * sizeof(uint32_t)));
     HIP_TRY(hipMalloc(&c->d_cand_fp, (np + 1) * rt_cand_footprint_bytes()));
     HIP_TRY(hipMalloc((void**)&c->d_cand_visits, (np + 1) * sizeof(uint32_t)));
@@ -963,13 +971,13 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
       *b = nullptr;
     }
 
+    c->cand_cap = 0;  // set only once all four entry buffers exist
     size_t cap = 0;
     rc = grow_dev(&c->d_cand_keys, &cap, total + 1);
     if (rc) return rc;
-    c->cand_cap = cap;
     for (uint32_t** b : {&c->d_cand_vals, &c->d_cand_keys2, &c->d_cand})
-      HIP_TRY(hipMalloc((void**)b, c->cand_cap * sizeof(uint32_t)));
-
+      HIP_TRY(hipMalloc((void**)b, cap * sizeof(uint32_t)));
+    c->cand_cap = cap;
   }
   cp.keys = c->d_cand_keys;
   cp.vals = c->d_cand_vals;
