@@ -1095,6 +1095,9 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
   p.scene_cmag = std::fmax(std::fabs(c->scene_c[0]), std::fmax(std::fabs(c->scene_c[1]),
                                                                std::fabs(c->scene_c[2])));
   p.spill = c->d_spill;
+  // prim-order records: camera candidates, light buffers and the exact
+  // shadow mode's global list all index them (set with or without lists)
+  p.tri_prim = c->d_tri_prim;
   // culling slack: eps_ulps ulps of the origin-to-geometry distance
   // (DESIGN.md "Conservative culling")
   p.eps_rel = c->eps_ulps * 5.9604645e-8f;
@@ -1150,6 +1153,12 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
   const int dacc = (c->accel == RT_ACCEL_FLAT || empty) ? RT_ACCEL_FLAT_D : RT_ACCEL_OCTREE_D;
   const int pol = dacc == RT_ACCEL_FLAT_D ? 0 : c->policy, cw = c->count_work ? 1 : 0;
   const int gt = empty ? c->grid : c->grid_of[1][pol][cw], gs = empty ? c->grid : c->grid_of[0][pol][cw];
+  // every device pointer the kernels will follow must exist (a null one
+  // would fault the card, not fail the call)
+  if (!p.tri_prim && (p.lbuf || p.n_sh_global || p.cand_start))
+    return rt_set_error(RT_EHIP, "render: prim-order records missing");
+  if (!p.hit || !p.last || !p.out || (p.nrec && (!p.tri || !p.nrm)))
+    return rt_set_error(RT_EHIP, "render: device buffers missing");
   HIP_TRY(hipMemsetAsync(c->d_counter, 0, 8 * 128, s));  // 8 item streams, 128 B apart
   HIP_TRY(hipMemsetAsync(c->d_stats, 0, RT_NSTATS * sizeof(unsigned long long), s));
   HIP_TRY(hipMemsetAsync(c->d_hit_count, 0, 2 * RT_HIT_REGIONS * 32 * sizeof(uint32_t), s));

@@ -381,6 +381,24 @@ def test_shadow_queries_match_brute_force(gpu, accel, policy, exact, lbuf):
     assert v["records_differ"] == 0 and v["walk_lit_brute_shadowed"] == 0, v
 
 
+@pytest.mark.parametrize("exact_shadows", [False, True])
+def test_no_camera_lists_with_light_buffers(gpu, exact_shadows):
+    """exact_camera off (an A/B knob) leaves the render without candidate
+    lists; the shadow queries still index the prim-order records (light
+    buffers, the exact mode's global list).  Round 3 first ran this with a
+    null record pointer -- it must render, and agree with the lists' image
+    wherever camera rays are not grazing (here: everywhere)."""
+    s = gpu.Scene.synthetic(3, 3, 9776, seed=0x5EED, width=320, height=180)
+    f = s.frame()
+    ctx = gpu.Context(s, "octree_gpu")
+    if exact_shadows:
+        ctx.set_exact_shadows(True)
+    img, _ = ctx.render_image(f)
+    ctx.set_exact_camera(False)
+    img_nc, _ = ctx.render_image(f)
+    assert_bitexact(img_nc, img, "without camera candidate lists")
+
+
 @pytest.mark.parametrize("height", [0.02, 0.5])
 def test_light_buffer_point_light_near_surface(gpu, height):
     """A point light just above a sphere: triangles around it span wide
