@@ -194,6 +194,9 @@ def main():
     ap.add_argument("--policy", type=int, default=None,
                     help="octree traversal policy (A/B only; rt_hip_set_policy, default = library "
                          "default 0)")
+    ap.add_argument("--exact-shadows", type=int, default=None, choices=[0, 1],
+                    help="shadow queries through proven (1) or slack-grown (0) light buffers "
+                         "(rt_hip_set_exact_shadows; default = library default)")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary (tools/pmc_traffic.py) to report as roofline.traffic")
     ap.add_argument("--valu-json", default=None,
@@ -224,6 +227,8 @@ def main():
         ctx.set_camera_slack(args.camera_slack)
     if args.policy is not None:
         ctx.set_policy(args.policy)
+    if args.exact_shadows is not None:
+        ctx.set_exact_shadows(bool(args.exact_shadows))
     info = ctx.info()
     log(f"[rank {rank}] scene {ntri} triangles, accel {wl['accel']}: {info['tri_refs']} records, "
         f"{info['nodes']} nodes, build {info['build_seconds']:.1f}s, setup {time.perf_counter()-t:.1f}s")
@@ -344,7 +349,8 @@ def main():
     traffic = traffic_hi = None
     traffic_src = None
     if world == 1 and args.traffic_json is None and args.cull_slack is None and \
-            args.camera_slack is None and args.policy is None and args.accel is None:
+            args.camera_slack is None and args.policy is None and args.accel is None and \
+            args.exact_shadows is None:
         # default run: the newest committed rocprofv3 PMC passes of this
         # workload (profiles/r*_<workload>/, tools/gpu_profile.sh); a PMC
         # pass cannot run inside the bench, so the line says where it came from
@@ -432,6 +438,8 @@ def main():
                                 "records": info["tri_refs"], "nodes": info["nodes"],
                                 "light_buffer_entries": info["lightbuf_entries"],
                                 "light_buffer_global": info["lightbuf_global"],
+                                "light_buffer_never": info["lightbuf_never"],
+                                "light_buffer_band": info["lightbuf_band"],
                                 "light_buffer_seconds": round(info["lightbuf_seconds"], 3)},
                 "parallelism": f"image tiles over {world} GPU(s) + RCCL gather" if world > 1
                                else "1 GPU",

@@ -111,6 +111,11 @@ typedef struct rt_accel_info {
   unsigned long long lightbuf_entries;
   unsigned long long lightbuf_global;
   double lightbuf_seconds;             /* their build time (device, at rt_hip_create) */
+  /* proven light buffers (rt_hip_set_exact_shadows): triangles no shadow ray
+   * of a light can make the float test accept (listed nowhere), and
+   * triangles listed along a band of a point light's cube map */
+  unsigned long long lightbuf_never;
+  unsigned long long lightbuf_band;
 } rt_accel_info;
 
 /* Host-only: build the acceleration structure rt_hip_create would build and
@@ -221,6 +226,12 @@ int rt_hip_set_exact_camera(rt_hip_ctx *ctx, int enable);
  * Both are exact in the same sense (DESIGN.md §2 "Shadow rays"). */
 int rt_hip_set_light_buffers(rt_hip_ctx *ctx, int enable);
 int rt_hip_set_exact_shadows(rt_hip_ctx *ctx, int enable);
+/* Shadow-query probe (tests, tools): light `light`'s shadow ray
+ * (cpu/light.c:53,78) from each of n origins (x, y, z floats), answered
+ * through the context's light buffer (brute = 0) or by brute force over every
+ * triangle (brute = 1, cpu/hit.c:93-109); hit[i] = 1 when shadowed. */
+int rt_hip_probe_shadows(rt_hip_ctx *ctx, unsigned light, const float *origins, size_t n, int brute,
+                         unsigned char *hit);
 /* Octree traversal policy (default 0): 0 = staged packet walk for coherent
  * closest-hit queries, per-lane walks otherwise; 1 = every query per lane;
  * 2 = every query as a staged packet; 3 = 0 plus staged packet walks for

@@ -88,6 +88,7 @@ struct rt_hip_ctx {
   std::vector<LBDevice*> lb_dev;    // per light (nullptr: the walk)
   RtLightBuf* d_lbuf = nullptr;     // per light, device
   float lb_ulps = -1.0f;
+  int lb_proven = -1;               // built proven (exact_shadows) or slack-grown
   KParams last_p{};                 // the last render's parameters (rt_hip_verify_shadows)
   // exact shadow rays (csrc/rt_shadow.hip), built for the slack sh_ulps
   float2* d_prim_mu = nullptr;
@@ -302,7 +303,7 @@ static void lbuf_release(rt_hip_ctx* c) {
 
 static int lbuf_prepare(rt_hip_ctx* c, hipStream_t s) {
   if (!c->light_buffers || c->accel != RT_ACCEL_OCTREE || !c->d_node || !c->nlight) return RT_OK;
-  if (c->d_lbuf && c->lb_ulps == c->eps_ulps) return RT_OK;
+  if (c->d_lbuf && c->lb_ulps == c->eps_ulps && c->lb_proven == c->exact_shadows) return RT_OK;
   lbuf_release(c);
   c->lb_dev.assign(c->nlight, nullptr);
   std::vector<RtLightBuf> hb(c->nlight);
@@ -346,6 +347,7 @@ static int lbuf_prepare(rt_hip_ctx* c, hipStream_t s) {
     lp.s1 = s1;
     lp.dmax = dmax * 1.01 + 1.0;
     lp.target_cells = c->nprim < 4096u ? 4096u : (c->nprim > (1u << 24) ? (1u << 24) : c->nprim);
+    lp.proven = c->exact_shadows ? 1u : 0u;
     if (rt_lightbuf_build(&lp, &hb[li], &c->lb_dev[li], s, err, sizeof err)) {
       lbuf_release(c);
       return rt_set_error(RT_EHIP, "light buffer of light %u: %s", li, err);
@@ -354,14 +356,20 @@ static int lbuf_prepare(rt_hip_ctx* c, hipStream_t s) {
   HIP_TRY(hipMalloc((void**)&c->d_lbuf, hb.size() * sizeof(RtLightBuf)));
   HIP_TRY(hipMemcpy(c->d_lbuf, hb.data(), hb.size() * sizeof(RtLightBuf), hipMemcpyHostToDevice));
   c->lb_ulps = c->eps_ulps;
-  unsigned long long e = 0, n = 0, g = 0, te = 0, tg = 0;
+  c->lb_proven = c->exact_shadows;
+  unsigned long long e = 0, n = 0, g = 0, te = 0, tg = 0, nv = 0, bd = 0, tnv = 0, tbd = 0;
   for (LBDevice* d : c->lb_dev) {
     rt_lightbuf_sizes(d, &e, &n, &g);
+    rt_lightbuf_proof_counts(d, &nv, &bd);
     te += e;
     tg += g;
+    tnv += nv;
+    tbd += bd;
   }
   c->info.lightbuf_entries = te;
   c->info.lightbuf_global = tg;
+  c->info.lightbuf_never = tnv;
+  c->info.lightbuf_band = tbd;
   return RT_OK;
 }
 
@@ -571,10 +579,12 @@ extern "C" int rt_hip_set_exact_camera(rt_hip_ctx* c, int enable) {
 extern "C" int rt_hip_set_exact_shadows(rt_hip_ctx* c, int enable) {
   if (!c) return rt_set_error(RT_EINVAL, "null context");
   c->exact_shadows = enable ? 1 : 0;
-  if (c->exact_shadows) {  // built now (setup), reported by rt_hip_accel_info
-    HIP_TRY(hipSetDevice(c->device));
-    return shadow_prepare(c, c->stream);
-  }
+  // built now (setup), reported by rt_hip_accel_info: the light buffers in
+  // the matching mode, and the walk's multipliers (policies that walk)
+  HIP_TRY(hipSetDevice(c->device));
+  int rc = lbuf_prepare(c, c->stream);
+  if (rc) return rc;
+  if (c->exact_shadows) return shadow_prepare(c, c->stream);
   return RT_OK;
 }
 
@@ -1129,12 +1139,14 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
     int rc = shadow_prepare(c, s);  // no-op unless the culling slack changed
     if (rc) return rc;
   }
-  if (!c->exact_shadows) {
-    int rc = lbuf_prepare(c, s);  // no-op unless the culling slack changed
+  {
+    // light buffers, proven in exact-shadow mode (no-op unless the slack or
+    // the mode changed); the staged policies walk
+    int rc = lbuf_prepare(c, s);
     if (rc) return rc;
     if (c->policy == RT_POLICY_DEFAULT || c->policy == RT_POLICY_LANE) p.lbuf = c->d_lbuf;
   }
-  if (c->exact_shadows) {
+  if (c->exact_shadows && !p.lbuf) {  // the proven walk
     p.node_mu = c->d_node_mu;
     p.sh_global = c->d_sh_global;
     p.n_sh_global = c->n_sh_global;
@@ -1260,6 +1272,55 @@ done:
   (void)hipFree(term);
   (void)hipFree(ctr);
   (void)hipFree(st);
+  return rc;
+}
+
+// Shadow-query probe (tests, tools): light `light`'s shadow ray from each
+// of n host origins (x, y, z), through the context's light buffer (brute =
+// 0; built as the context's mode -- slack-grown or proven -- says) or by brute
+// force over every triangle (brute = 1).  hit[i] = 1: shadowed.
+extern "C" int rt_hip_probe_shadows(rt_hip_ctx* c, unsigned light, const float* origins, size_t n, int brute,
+                                    unsigned char* hit) {
+  if (!c || (!origins && n) || (!hit && n)) return rt_set_error(RT_EINVAL, "null argument");
+  if (light >= c->nlight || (c->light_type[light] != 1 && c->light_type[light] != 2))
+    return rt_set_error(RT_EINVAL, "light %u is not a directional or point light", light);
+  if (n > (1u << 26)) return rt_set_error(RT_EINVAL, "%zu origins (at most 2^26 per call)", n);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  if (!brute) {
+    int rc = lbuf_prepare(c, s);
+    if (rc) return rc;
+    if (!c->d_lbuf) return rt_set_error(RT_EINVAL, "no light buffers (octree contexts with light buffers on)");
+  }
+  if (!c->d_tri_prim) return rt_set_error(RT_EINVAL, "no triangles");
+  KParams p;
+  std::memset(&p, 0, sizeof p);
+  p.light = c->d_light;
+  p.nlight = c->nlight;
+  p.tri_prim = c->d_tri_prim;
+  p.lbuf = brute ? nullptr : c->d_lbuf;
+  p.scene_c = rt::f3{c->scene_c[0], c->scene_c[1], c->scene_c[2]};
+  p.scene_r = c->scene_r;
+  p.scene_cmag = std::fmax(std::fabs(c->scene_c[0]), std::fmax(std::fabs(c->scene_c[1]),
+                                                               std::fabs(c->scene_c[2])));
+  p.eps_rel = c->eps_ulps * 5.9604645e-8f;
+  float* d_o = nullptr;
+  uint32_t* d_h = nullptr;
+  std::vector<uint32_t> h(n);
+  int rc = RT_OK;
+  if (hipMalloc((void**)&d_o, (n * 3 + 1) * sizeof(float)) != hipSuccess ||
+      hipMalloc((void**)&d_h, (n + 1) * sizeof(uint32_t)) != hipSuccess) {
+    rc = rt_set_error(RT_EHIP, "hipMalloc probe buffers");
+  } else if (hipMemcpy(d_o, origins, n * 3 * sizeof(float), hipMemcpyHostToDevice) != hipSuccess ||
+             rt_launch_probe_shadow(&p, d_o, (uint32_t)n, light, (uint32_t)c->nprim, brute, d_h, s) != hipSuccess ||
+             hipStreamSynchronize(s) != hipSuccess ||
+             hipMemcpy(h.data(), d_h, n * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess) {
+    rc = rt_set_error(RT_EHIP, "shadow probe: %s", hipGetErrorString(hipGetLastError()));
+  } else {
+    for (size_t i = 0; i < n; i++) hit[i] = (unsigned char)h[i];
+  }
+  (void)hipFree(d_o);
+  (void)hipFree(d_h);
   return rc;
 }
 

@@ -136,6 +136,11 @@ extern "C" hipError_t rt_launch_trace(const KParams* p, int accel, int count_wor
 extern "C" hipError_t rt_launch_shade(const KParams* p, int accel, int count_work, int policy,
                                       int grid, hipStream_t stream);
 extern "C" hipError_t rt_launch_fold(const KParams* p, hipStream_t stream);
+// shadow-query probe: light li's shadow ray from each of n origins through
+// the light buffer p->lbuf[li] (brute = 0) or brute force over nprim
+// prim-order records p->tri_prim (brute = 1); out[i] = shadowed
+extern "C" hipError_t rt_launch_probe_shadow(const KParams* p, const float* org, uint32_t n, uint32_t li,
+                                             uint32_t nprim, int brute, uint32_t* out, hipStream_t stream);
 // persistent grid (one-wave workgroups) of trace (trace = 1) or shade on `cus` CUs
 extern "C" hipError_t rt_render_grid(int trace, int accel, int count_work, int policy, int cus,
                                      int* grid);

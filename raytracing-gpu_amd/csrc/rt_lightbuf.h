@@ -45,6 +45,10 @@ struct LBParams {
   double dmax;        // POINT: >= the distance from the light to any scene point
   double box_lo[3], box_hi[3];  // a box holding every triangle and shadow-ray origin
   uint32_t target_cells;
+  // 0: footprints grown by the walk's slack (tested exactness, like the
+  // walk); 1: grown by the reference float test's proven error region for the
+  // light's ray family (exact by construction, DESIGN.md §2 "Shadow rays")
+  uint32_t proven;
 };
 
 struct LBDevice;  // device allocations of one light's buffer (rt_lightbuf.hip)
@@ -57,3 +61,7 @@ extern "C" void rt_lightbuf_free(LBDevice* dev);
 // entries and cells of a built buffer (bench / info)
 extern "C" void rt_lightbuf_sizes(const LBDevice* dev, unsigned long long* entries,
                                   unsigned long long* cells, unsigned long long* global);
+// proven mode: triangles no ray of the light can make the float test accept
+// (skipped), and triangles listed along a band of the cube map (point lights)
+extern "C" void rt_lightbuf_proof_counts(const LBDevice* dev, unsigned long long* never,
+                                         unsigned long long* band);

@@ -3,14 +3,47 @@
 // the device: count (cells per triangle) -> scan -> emit (cell, key, prim) ->
 // radix sort by (cell, key) -> cell starts.
 //
-// Conservative by construction, relative to the octree walk it replaces: a
-// triangle is listed in every cell that a shadow ray passing within the walk's
-// slack of it can start from (the float rounding of the query's own cell and
-// key computations added as margins), and skipped by a query only where it
-// lies entirely behind the ray's origin by more than twice that slack.  The
-// walk tests a triangle when the ray passes within the slack of the leaf box
-// holding it, so both find every hit within the slack of a triangle -- the same
-// exactness class (DESIGN.md §2 "Shadow rays").
+// Two ways to grow a triangle's footprint (LBParams::proven):
+//
+// * slack (default): a triangle is listed in every cell that a shadow ray
+//   passing within the walk's slack of it can start from (the float rounding
+//   of the query's own cell and key computations added as margins), and
+//   skipped by a query only where it lies entirely behind the ray's origin by
+//   more than twice that slack.  The walk tests a triangle when the ray
+//   passes within the slack of the leaf box holding it, so both find every
+//   hit within the slack of a triangle -- the same exactness class ("tested,
+//   not proven", DESIGN.md §2 "Shadow rays").
+//
+// * proven: listed wherever a shadow ray of this light can make the
+//   reference's float Moller-Trumbore test (cpu/hit.c:15-33) accept the
+//   triangle.  tools/mt_bound.py bounds the float test: an accept implies the
+//   exact line crosses the triangle's plane inside the expanded triangle
+//     T_D = { v0 + U e1 + V e2 : U >= -du, V >= -dv, U + V <= 1 + dw },
+//   du, dv, dw from the rounding errors E_sh, E_dq, E_a of s.h, d.q, a and a
+//   lower bound a_lb of the float |a| (>= 1e-7 for any accept).
+//   - A directional light's rays all have the direction d = -l.v exactly
+//     (cpu/light.c:53): the exact a = -d.n is one number per triangle, so
+//     a_lb = max(1e-7, |a| - E_a) and T_D are fixed (|S| = |o - v0| bounded
+//     over the origin box, componentwise).  T_D's projection along the light
+//     is the footprint; the crossing X has the origin's projection, and lies
+//     at most derr = |d| E_eq / |a| behind it.  No ray accepts a triangle with
+//     |a| + E_a < 1e-7: such triangles are listed nowhere.
+//   - A point light's rays (P, l.v - P) (cpu/light.c:78) pass within dline of
+//     the light.  A ray crossing the plane at X has cosine c >= (s_L - dline)
+//     / (|X - l.v| + dline) with the plane (s_L = the light's distance from
+//     it), and the bound at cosine c moves X at most h(c) from the triangle;
+//     so X lies within r of it only if r <= g(r) = h(c(r)).  g is convex and
+//     increasing, and the smallest R with g(R) <= R (iterated from 0) bounds
+//     every crossing of rays at c >= c*, provided h(c*) < r(c*) (the r at
+//     which c(r) = c*).  Rays at c < c* are accepted only from origins within
+//     H_o(c*) of the plane, on lines nearly parallel to it (|s_o| bounded by
+//     u, v in [0, 1] and |a_f| <= |a| + E_a), which needs s_L <= H_o(c*) +
+//     Dmax c* + dline: for larger s_L there are none.  Triangles whose plane
+//     passes that close to the light are listed, in addition, in the band of
+//     cube-map cells within asin(c* + dline / rmin_o) of the great circle of
+//     the plane through the light parallel to theirs (with the key that is
+//     always tested).  The cone of directions to T's ball grown by R is the
+//     footprint; keys as in slack mode with derr in place of the slack.
 #include <hip/hip_runtime.h>
 #include <cstring>  // before rocPRIM
 #include <rocprim/rocprim.hpp>
@@ -26,23 +59,33 @@ namespace rtl {
 
 constexpr double kEps = 0x1p-24;
 constexpr double kInvSqrt3 = 0.57735026918962573;
-constexpr uint32_t kSmallCells = 1024;  // more: emitted by a workgroup
+constexpr double kSqrt3 = 1.7320508075688772;
+constexpr double kAMin = 9.99999997e-08;   // (double)(float)1e-7, cpu/hit.c:7
+constexpr double kCDot = 8.6, kCA = 7.2;   // tools/mt_bound.py C_DOT, C_A (Cauchy-Schwarz)
+constexpr double kCW = 6.01, kCWA = 5.01;  // tools/mt_bound.py bound_cw (componentwise)
+constexpr double kDMax = 1.0 + 4.0 * kEps;
+constexpr uint32_t kSmallCells = 1024;  // more (or a band): counted and emitted by a workgroup
 constexpr int kMaxRects = 6;
+constexpr int kBlock = 256;
 
 struct BP {
   const float4* tri;
-  uint32_t nprim, kind;
+  uint32_t nprim, kind, proven;
   double lv[3];
   double u[3], v[3], w[3];  // DIR: the float axes, as doubles
   double u0, v0, cs, inv_cs;
   uint32_t nx, ny, n;       // DIR grid / POINT face side
   double slack, s1, dmax;
+  double olo[3], ohi[3];    // the origin box (LBParams::box_lo/hi)
+  double d[3], dlen;        // DIR: the rays' direction -l.v (float) and its length
+  double skew;              // DIR: max |u.d^|, |v.d^| (the float axes vs the exact direction)
+  const uint32_t* rmin_bits;  // POINT proven: float bits of a lower bound of |o - l.v| over origins
   uint32_t* count;
   uint32_t* off;
   unsigned long long* keys;
   uint32_t* vals;
   uint32_t* big;
-  uint32_t* ctr;  // [0] big prims, [1] global prims
+  uint32_t* ctr;  // [0] big prims, [1] global prims, [2] never accepted, [3] band, [4] emission overflow
   uint32_t* global;
 };
 
@@ -52,18 +95,31 @@ struct Foot {
   int x0[kMaxRects], x1[kMaxRects], y0[kMaxRects], y1[kMaxRects];
   double key;    // whole-triangle key (ascending = tested first)
   bool global;
+  bool never;    // proven: no ray of the light can make the float test accept it
   // DIR per-cell refinement: the plane's depth over a cell column
   bool plane;
   double pn_u, pn_v, pn_w, pn_d;  // n.u, n.v, n.w, n.v0 of the triangle's plane
   double m;                       // footprint margin (world units)
+  double kpad;                    // behind-origin tolerance of the keys (2 slack; proven: derr)
   // per rect: the triangle's image in the rect's coordinates (DIR: u, v;
   // POINT: the face's (s, t)) and its margin there, for the cell overlap
   // test of small footprints; tri_ok = 0: bounding rect only
   bool tri_ok[kMaxRects];
   double tx[kMaxRects][3], ty[kMaxRects][3], tm[kMaxRects];
+  // POINT proven: also every cell whose directions x can have |x.bn| <= bB
+  // |x|_inf-scaled (the band around the great circle of the plane through
+  // the light parallel to the triangle)
+  bool band;
+  double bn[3], bB;
 };
 
 __device__ inline double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+__device__ inline double norm3(const double* a) { return sqrt(dot3(a, a)); }
+__device__ inline void cross3d(const double* a, const double* b, double* o) {
+  o[0] = a[1] * b[2] - a[2] * b[1];
+  o[1] = a[2] * b[0] - a[0] * b[2];
+  o[2] = a[0] * b[1] - a[1] * b[0];
+}
 
 __device__ inline uint32_t orderable(float f) {
   const uint32_t b = __float_as_uint(f);
@@ -79,78 +135,64 @@ __device__ inline int clampi(double x, int hi) {
   return (int)x;
 }
 
-__device__ void footprint(const BP& p, uint32_t prim, Foot& f) {
-  const float* r = (const float*)(p.tri + 3 * (size_t)prim);
-  const double v0[3] = {r[0], r[1], r[2]}, e1[3] = {r[3], r[4], r[5]}, e2[3] = {r[6], r[7], r[8]};
-  const double V[3][3] = {{v0[0], v0[1], v0[2]},
-                          {v0[0] + e1[0], v0[1] + e1[1], v0[2] + e1[2]},
-                          {v0[0] + e2[0], v0[1] + e2[1], v0[2] + e2[2]}};
+__device__ inline void foot_init(Foot& f) {
   f.n = 0;
   f.global = false;
+  f.never = false;
   f.plane = false;
+  f.band = false;
+  f.kpad = 0.0;
+  f.m = 0.0;
   for (int q = 0; q < kMaxRects; q++) f.tri_ok[q] = false;
-  if (p.kind == RT_LB_DIR) {
-    // the query's float projection of its origin is within 3 eps s1 of the
-    // exact one; the triangle's points are within the slack of the ray
-    const double m = p.slack + 3.0 * kEps * p.s1 * 1.01 + 1e-9 * p.s1;
-    double lu = 1e300, hu = -1e300, lvv = 1e300, hvv = -1e300, hw = -1e300;
-    for (int k = 0; k < 3; k++) {
-      const double a = dot3(V[k], p.u), b = dot3(V[k], p.v), c = dot3(V[k], p.w);
-      lu = fmin(lu, a);
-      hu = fmax(hu, a);
-      lvv = fmin(lvv, b);
-      hvv = fmax(hvv, b);
-      hw = fmax(hw, c);
-      f.tx[0][k] = a;
-      f.ty[0][k] = b;
-    }
-    f.tri_ok[0] = true;
-    f.tm[0] = m;
-    f.n = 1;
-    f.face[0] = 0;
-    f.x0[0] = clampi(floor((lu - m - p.u0) * p.inv_cs - 0.01), (int)p.nx - 1);
-    f.x1[0] = clampi(floor((hu + m - p.u0) * p.inv_cs + 0.01), (int)p.nx - 1);
-    f.y0[0] = clampi(floor((lvv - m - p.v0) * p.inv_cs - 0.01), (int)p.ny - 1);
-    f.y1[0] = clampi(floor((hvv + m - p.v0) * p.inv_cs + 0.01), (int)p.ny - 1);
-    // skipped by a query when its deepest point, grown by the slack on both
-    // sides (behind-origin tolerance of the walk) and the rounding of the
-    // query's depth, lies below the origin: key = -(that bound)
-    f.key = -(hw + 2.0 * p.slack + 6.0 * kEps * p.s1 * 1.01 + 1e-9 * p.s1);
-    f.m = m;
-    const double n[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2],
-                         e1[0] * e2[1] - e1[1] * e2[0]};
-    const double nl = sqrt(dot3(n, n));
-    f.pn_u = dot3(n, p.u);
-    f.pn_v = dot3(n, p.v);
-    f.pn_w = dot3(n, p.w);
-    f.pn_d = dot3(n, v0);
-    f.plane = nl > 0.0 && fabs(f.pn_w) > 0.05 * nl;
-    return;
-  }
-  // POINT: the cone from the light around the triangle's bounding sphere
-  // (grown by the slack), widened by the angle the rounding of the shadow
-  // direction l.v - P can turn a ray's points as seen from the light
-  double C[3];
-  for (int a = 0; a < 3; a++) C[a] = (V[0][a] + V[1][a] + V[2][a]) / 3.0;
-  double rb = 0.0;
+}
+
+// DIR: rect and image of the points P[0..2] (the triangle, or T_D) projected
+// on (u, v) with margin m; the plane of the triangle for the per-cell keys
+__device__ inline void dir_rect(const BP& p, const double P[3][3], const double* v0, const double* e1,
+                                const double* e2, double m, Foot& f, double& hw) {
+  double lu = 1e300, hu = -1e300, lvv = 1e300, hvv = -1e300;
+  hw = -1e300;
   for (int k = 0; k < 3; k++) {
-    const double d[3] = {V[k][0] - C[0], V[k][1] - C[1], V[k][2] - C[2]};
-    rb = fmax(rb, sqrt(dot3(d, d)));
+    const double a = dot3(P[k], p.u), b = dot3(P[k], p.v), c = dot3(P[k], p.w);
+    lu = fmin(lu, a);
+    hu = fmax(hu, a);
+    lvv = fmin(lvv, b);
+    hvv = fmax(hvv, b);
+    hw = fmax(hw, c);
+    f.tx[0][k] = a;
+    f.ty[0][k] = b;
   }
-  rb = rb * (1.0 + 1e-12) + p.slack + 1e-12;
+  f.tri_ok[0] = true;
+  f.tm[0] = m;
+  f.n = 1;
+  f.face[0] = 0;
+  f.x0[0] = clampi(floor((lu - m - p.u0) * p.inv_cs - 0.01), (int)p.nx - 1);
+  f.x1[0] = clampi(floor((hu + m - p.u0) * p.inv_cs + 0.01), (int)p.nx - 1);
+  f.y0[0] = clampi(floor((lvv - m - p.v0) * p.inv_cs - 0.01), (int)p.ny - 1);
+  f.y1[0] = clampi(floor((hvv + m - p.v0) * p.inv_cs + 0.01), (int)p.ny - 1);
+  f.m = m;
+  double n[3];
+  cross3d(e1, e2, n);
+  const double nl = norm3(n);
+  f.pn_u = dot3(n, p.u);
+  f.pn_v = dot3(n, p.v);
+  f.pn_w = dot3(n, p.w);
+  f.pn_d = dot3(n, v0);
+  f.plane = nl > 0.0 && fabs(f.pn_w) > 0.05 * nl;
+}
+
+// POINT: the cube-map rects of the cone from the light around the ball
+// (C, rb), widened by alpha, and the central projection of V grown by beta
+// for the overlap test.  false: the cone is too wide (global list).
+__device__ inline bool point_cone(const BP& p, const double V[3][3], const double C[3], double rb, double& rmin,
+                                  double grow, Foot& f) {
   const double D[3] = {C[0] - p.lv[0], C[1] - p.lv[1], C[2] - p.lv[2]};
-  const double dc = sqrt(dot3(D, D));
-  if (!(dc > rb * 1.001 + 1e-9)) {
-    f.global = true;
-    return;
-  }
-  const double rmin = dc - rb;
-  const double alpha = 4.0 * 1.7320508075688772 * kEps * p.dmax / rmin + 8.0 * kEps;
+  const double dc = norm3(D);
+  if (!(dc > rb * 1.001 + 1e-9)) return false;
+  rmin = dc - rb;
+  const double alpha = 4.0 * kSqrt3 * kEps * p.dmax / rmin + 8.0 * kEps;
   const double th = asin(fmin(1.0, rb / dc)) + alpha + 1e-12;
-  if (!(th < 1.2)) {
-    f.global = true;
-    return;
-  }
+  if (!(th < 1.2)) return false;
   double xlo[3], xhi[3];
   for (int a = 0; a < 3; a++) {
     const double ph = acos(fmax(-1.0, fmin(1.0, D[a] / dc)));
@@ -171,15 +213,15 @@ __device__ void footprint(const BP& p, uint32_t prim, Foot& f) {
       f.face[q] = (uint32_t)(2 * a + sg);
       // the triangle's central projection onto the face (valid when every
       // vertex lies well on the face's side), grown by the cone's widening
-      // beta (slack / rmin + alpha) through the face map's Lipschitz bound
+      // beta (grow / rmin + alpha) through the face map's Lipschitz bound
       {
-        const double beta = p.slack / rmin + alpha;
+        const double beta = grow / rmin + alpha;
         const double sgn = sg == 0 ? 1.0 : -1.0;
         double xamin = 1e300, smax = 1.0;
         bool ok = true;
         for (int v = 0; v < 3 && ok; v++) {
           const double X[3] = {V[v][0] - p.lv[0], V[v][1] - p.lv[1], V[v][2] - p.lv[2]};
-          const double xl = sqrt(dot3(X, X)), xa = sgn * X[a];
+          const double xl = norm3(X), xa = sgn * X[a];
           ok = xl > 0.0 && xa > 1e-3 * xl;
           if (!ok) break;
           xamin = fmin(xamin, xa / xl);
@@ -197,9 +239,245 @@ __device__ void footprint(const BP& p, uint32_t prim, Foot& f) {
       f.y0[q] = clampi(floor((fmax(tlo, -1.0) + 1.0) * hn - 0.01), (int)p.n - 1);
       f.y1[q] = clampi(floor((fmin(thi, 1.0) + 1.0) * hn + 0.01), (int)p.n - 1);
     }
+  return true;
+}
+
+// ---- slack-grown footprints (default) ----
+__device__ void footprint_slack(const BP& p, const double V[3][3], const double* v0, const double* e1,
+                                const double* e2, Foot& f) {
+  if (p.kind == RT_LB_DIR) {
+    // the query's float projection of its origin is within 3 eps s1 of the
+    // exact one; the triangle's points are within the slack of the ray
+    const double m = p.slack + 3.0 * kEps * p.s1 * 1.01 + 1e-9 * p.s1;
+    double hw;
+    dir_rect(p, V, v0, e1, e2, m, f, hw);
+    // skipped by a query when its deepest point, grown by the slack on both
+    // sides (behind-origin tolerance of the walk) and the rounding of the
+    // query's depth, lies below the origin: key = -(that bound)
+    f.kpad = 2.0 * p.slack;
+    f.key = -(hw + 2.0 * p.slack + 6.0 * kEps * p.s1 * 1.01 + 1e-9 * p.s1);
+    return;
+  }
+  // POINT: the cone from the light around the triangle's bounding sphere
+  // (grown by the slack), widened by the angle the rounding of the shadow
+  // direction l.v - P can turn a ray's points as seen from the light
+  double C[3];
+  for (int a = 0; a < 3; a++) C[a] = (V[0][a] + V[1][a] + V[2][a]) / 3.0;
+  double rb = 0.0;
+  for (int k = 0; k < 3; k++) {
+    const double d[3] = {V[k][0] - C[0], V[k][1] - C[1], V[k][2] - C[2]};
+    rb = fmax(rb, norm3(d));
+  }
+  rb = rb * (1.0 + 1e-12) + p.slack + 1e-12;
+  double rmin = 0.0;
+  if (!point_cone(p, V, C, rb, rmin, p.slack, f)) {
+    f.n = 0;
+    f.global = true;
+    return;
+  }
   // a query toward the light stops once the triangle's nearest possible
   // point lies farther from the light than its origin (plus the slack)
+  f.kpad = 2.0 * p.slack;
   f.key = rmin - 2.0 * p.slack - 1e-9 * p.dmax;
+}
+
+// ---- proven footprints (module comment) ----
+__device__ void footprint_dir_proven(const BP& p, const double* v0, const double* e1, const double* e2, Foot& f) {
+  const double* d = p.d;
+  double n[3];
+  cross3d(e1, e2, n);
+  const double A = fabs(dot3(n, d));  // |a| exact: a = e1.(d x e2) = -d.n, every ray alike
+  double M[3], S[3], N[3];
+  for (int i = 0; i < 3; i++) S[i] = fmax(fabs(p.olo[i] - v0[i]), fabs(p.ohi[i] - v0[i]));
+  for (int i = 0; i < 3; i++) {
+    const int j = (i + 1) % 3, k = (i + 2) % 3;
+    M[i] = fabs(d[j]) * fabs(e2[k]) + fabs(d[k]) * fabs(e2[j]);
+    N[i] = S[j] * fabs(e1[k]) + S[k] * fabs(e1[j]);
+  }
+  double Ea = 0.0, Esh = 0.0, Edq = 0.0, Eeq = 0.0;
+  for (int i = 0; i < 3; i++) {
+    Ea += fabs(e1[i]) * M[i];
+    Esh += S[i] * M[i];
+    Edq += fabs(d[i]) * N[i];
+    Eeq += fabs(e2[i]) * N[i];
+  }
+  const double r1 = 1.0 + 1e-6;
+  Ea *= kCWA * kEps * r1;
+  Esh *= kCW * kEps * r1;
+  Edq *= kCW * kEps * r1;
+  Eeq *= kCW * kEps * r1;
+  if (A + Ea < kAMin * (1.0 - 1e-9)) {  // |a_f| < 1e-7 for every ray: rejected (cpu/hit.c:19)
+    f.never = true;
+    return;
+  }
+  const double alb = fmax(kAMin, A - Ea);
+  const double rho = Ea / alb;
+  if (!(rho < 0.5)) {
+    f.global = true;
+    return;
+  }
+  const double du = Esh / (alb * (1.0 - rho)), dv = Edq / (alb * (1.0 - rho));
+  const double dw = (4.0 * kEps + (Esh + Edq) / alb + rho) / (1.0 - rho);
+  // T_D's corners (U, V) = (-du, -dv), (1 + dw + dv, -dv), (-du, 1 + dw + du)
+  const double cU[3] = {-du, 1.0 + dw + dv, -du}, cV[3] = {-dv, -dv, 1.0 + dw + du};
+  double P[3][3];
+  for (int k = 0; k < 3; k++)
+    for (int a = 0; a < 3; a++) P[k][a] = v0[a] + cU[k] * e1[a] + cV[k] * e2[a];
+  const double Smax = sqrt(S[0] * S[0] + S[1] * S[1] + S[2] * S[2]);
+  const double ext = (1.0 + du + dv + dw) * (norm3(e1) + norm3(e2));
+  // the query's float projection (3 eps s1), and X - o along d seen through
+  // the float axes (|X - o| <= |S| + T_D's extent)
+  const double m = 3.0 * kEps * p.s1 * 1.01 + 1e-9 * p.s1 + p.skew * (Smax + ext) * 1.01;
+  double hw;
+  dir_rect(p, P, v0, e1, e2, m, f, hw);
+  // an accept has t* >= -E_eq / |a|: X at most derr behind the origin
+  const double derr = Eeq * p.dlen / A * 1.01;
+  f.kpad = derr;
+  f.key = -(hw + derr + 6.0 * kEps * p.s1 * 1.01 + 1e-9 * p.s1);
+}
+
+// reach of T_D beyond T for rays at cosine c (|d| cancels), Cauchy-Schwarz
+// form as csrc/rt_shadow.hip; > 1e300: no bound
+__device__ inline double reach_at(double c, double nl, double ea, double l1, double l2, double Smax) {
+  const double den = nl * c - ea;
+  if (!(den > 2.0001 * ea) || !(den > 0.0)) return 1e301;
+  const double rho = ea / den, kap = kCDot * kEps / den;
+  const double lmax = fmax(l1, l2), ls = l1 + l2;
+  return (kap * ls * (lmax + ls) * Smax / (1.0 - rho) + (4.0 * kEps + rho) * lmax / (1.0 - rho)) * (1.0 + 1e-6);
+}
+
+__device__ void footprint_point_proven(const BP& p, const double V[3][3], const double* v0, const double* e1,
+                                       const double* e2, Foot& f) {
+  double n[3];
+  cross3d(e1, e2, n);
+  const double nl = norm3(n), l1 = norm3(e1), l2 = norm3(e2);
+  const double lmax = fmax(l1, l2), ls = l1 + l2;
+  const double ea = kCA * kEps * l1 * l2 * kDMax;  // E_a / |d|
+  const double Dmax = p.dmax;
+  // |a_f| <= |d| (|n| + e_a) < 1e-7 for every ray: never accepted
+  if (Dmax * (nl + ea) * kDMax < kAMin * (1.0 - 1e-9)) {
+    f.never = true;
+    return;
+  }
+  if (!(nl > 0.0)) {  // degenerate: a is rounding noise, u, v unbounded
+    f.global = true;
+    return;
+  }
+  const double nh[3] = {n[0] / nl, n[1] / nl, n[2] / nl};
+  const double LV[3] = {p.lv[0] - v0[0], p.lv[1] - v0[1], p.lv[2] - v0[2]};
+  const double sL = fabs(dot3(nh, LV));
+  double vmax = 0.0, S[3];
+  for (int k = 0; k < 3; k++) {
+    const double X[3] = {V[k][0] - p.lv[0], V[k][1] - p.lv[1], V[k][2] - p.lv[2]};
+    vmax = fmax(vmax, norm3(X));
+  }
+  for (int i = 0; i < 3; i++) S[i] = fmax(fabs(p.olo[i] - v0[i]), fabs(p.ohi[i] - v0[i]));
+  const double Smax = sqrt(S[0] * S[0] + S[1] * S[1] + S[2] * S[2]) * (1.0 + 1e-9);
+  const double dline = 2.0 * kSqrt3 * kEps * Dmax;  // fl(l.v - o) from o passes this close to l.v
+  const double a_ = sL - dline, b_ = vmax * (1.0 + 1e-12) + dline;
+  // rays crossing within r of T: cosine >= c(r) = a_ / (b_ + r); R = a point
+  // past the smallest fixed point of g(r) = reach_at(c(r)) (g(R) <= R)
+  double R = 1e301;
+  if (a_ > 0.0) {
+    double r = 0.0;
+    for (int it = 0; it < 64; it++) {
+      const double g = reach_at(a_ / (b_ + r), nl, ea, l1, l2, Smax);
+      if (!(g < 1e300)) break;
+      if (g <= r) {
+        R = r;
+        break;
+      }
+      r = g * (1.0 + 1e-9) + 1e-300;
+    }
+  }
+  bool band = true;
+  double clo = 0.0;
+  if (R < 1e300) {
+    // H_o(c) + Dmax c + dline: how close to the plane the light must be for a
+    // ray at cosine < c to be accepted at all (module comment)
+    auto q = [&](double c) {
+      return ls / (nl * (1.0 - c)) *
+                 ((nl * c + ea) * (1.0 + 4.0 * kEps) + kCDot * kEps * Smax * lmax + c * Smax * lmax) *
+                 (1.0 + 1e-6) +
+             Dmax * c * (1.0 + 4.0 * kEps) + dline;
+    };
+    if (q(0.0) < sL) {
+      double lo = 0.0, hi = 0.5;
+      if (q(hi) <= sL) {
+        lo = hi;
+      } else {
+        for (int it = 0; it < 64; it++) {
+          const double mid = 0.5 * (lo + hi);
+          if (q(mid) <= sL)
+            lo = mid;
+          else
+            hi = mid;
+        }
+      }
+      const double cst = lo;  // q(cst) <= sL: no accepted ray below cst
+      if (cst > 0.0) {
+        const double rhi = a_ / cst - b_;
+        const double hc = reach_at(cst, nl, ea, l1, l2, Smax);
+        if (hc < rhi) {  // rays at c >= cst cross within R (convexity of g)
+          band = false;
+          clo = a_ / (b_ + R);
+        }
+      }
+    }
+  }
+  if (band) {
+    // rays at c >= cst: within reach_at(cst) of T; rays below: origins in the
+    // band of directions within asin(cst + dline / rmin_o) of the plane through
+    // the light parallel to T's
+    const double rmin_o = p.rmin_bits ? (double)__uint_as_float(*p.rmin_bits) : 0.0;
+    const double cst = fmax(1e-3, 8.0 * ea / nl);
+    R = reach_at(cst, nl, ea, l1, l2, Smax);
+    const double bs = cst * (1.0 + 1e-6) + (rmin_o > 0.0 ? dline / rmin_o : 1e300) + 4.0 * kEps;
+    if (!(cst < 0.25) || !(R < 1e300) || !(bs < 0.3)) {
+      f.global = true;
+      return;
+    }
+    clo = cst;
+    f.band = true;
+    for (int a = 0; a < 3; a++) f.bn[a] = nh[a];
+    // a face cell holds directions x = (s, t, +-1): |x| <= sqrt 3
+    f.bB = bs * kSqrt3 * (1.0 + 1e-9) + 1e-12;
+  }
+  double C[3];
+  for (int a = 0; a < 3; a++) C[a] = (V[0][a] + V[1][a] + V[2][a]) / 3.0;
+  double rb = 0.0;
+  for (int k = 0; k < 3; k++) {
+    const double d[3] = {V[k][0] - C[0], V[k][1] - C[1], V[k][2] - C[2]};
+    rb = fmax(rb, norm3(d));
+  }
+  rb = rb * (1.0 + 1e-12) + R + 1e-12;
+  double rmin = 0.0;
+  if (!point_cone(p, V, C, rb, rmin, R, f)) {
+    f.n = 0;
+    f.band = false;
+    f.global = true;
+    return;
+  }
+  // an accept has t* >= -E_eq / |a|, |a| >= |d| |n| clo: X at most derr
+  // behind the origin (toward the light)
+  const double derr = kCDot * kEps * Smax * l1 * l2 / (nl * clo) * 1.01;
+  f.kpad = derr;
+  f.key = rmin - derr - 2.0 * dline - 1e-9 * p.dmax;
+}
+
+__device__ void footprint(const BP& p, uint32_t prim, Foot& f) {
+  const float* r = (const float*)(p.tri + 3 * (size_t)prim);
+  const double v0[3] = {r[0], r[1], r[2]}, e1[3] = {r[3], r[4], r[5]}, e2[3] = {r[6], r[7], r[8]};
+  const double V[3][3] = {{v0[0], v0[1], v0[2]},
+                          {v0[0] + e1[0], v0[1] + e1[1], v0[2] + e1[2]},
+                          {v0[0] + e2[0], v0[1] + e2[1], v0[2] + e2[2]}};
+  foot_init(f);
+  if (!p.proven)
+    footprint_slack(p, V, v0, e1, e2, f);
+  else if (p.kind == RT_LB_DIR)
+    footprint_dir_proven(p, v0, e1, e2, f);
+  else
+    footprint_point_proven(p, V, v0, e1, e2, f);
 }
 
 __device__ inline uint64_t foot_cells(const BP& p, const Foot& f) {
@@ -222,7 +500,7 @@ __device__ inline float cell_key(const BP& p, const Foot& f, int x, int y) {
     const double us[2] = {ua, ub}, vs[2] = {va, vb};
     for (int i = 0; i < 2; i++)
       for (int k = 0; k < 2; k++) h = fmax(h, (f.pn_d - f.pn_u * us[i] - f.pn_v * vs[k]) / f.pn_w);
-    const double kc = -(h + 2.0 * p.slack + 6.0 * kEps * p.s1 * 1.01 + 1e-6 * p.s1);
+    const double kc = -(h + f.kpad + 6.0 * kEps * p.s1 * 1.01 + 1e-6 * p.s1);
     key = fmax(key, kc);  // the tighter (larger) of the two lower bounds of -depth
   }
   return __double2float_rd(key);
@@ -274,70 +552,202 @@ __device__ inline uint32_t cell_index(const BP& p, const Foot& f, int q, int x, 
   return f.face[q] * p.n * p.n + (uint32_t)y * p.n + (uint32_t)x;
 }
 
+// Band row (face, y) of a POINT footprint: the columns whose cells hold a
+// direction x = (s, t, sigma) (face frame: s along axis a+1, t along a+2, as
+// the query maps them) with |x.bn| <= bB; false: none.  Widened by 0.02 cells
+// for the query's rounding.
+__device__ inline bool band_row(const BP& p, const Foot& f, uint32_t face, uint32_t y, int& xa, int& xb) {
+  const int a = (int)(face >> 1), j = (a + 1) % 3, k = (a + 2) % 3;
+  const double sigma = (face & 1) ? -1.0 : 1.0;
+  const double cs = 2.0 / (double)p.n, pad = 0.02 * cs;
+  const double t0 = -1.0 + y * cs - pad, t1 = -1.0 + (y + 1) * cs + pad;
+  const double nj = f.bn[j], nk = f.bn[k], na = f.bn[a];
+  const double g0 = nk * t0 + na * sigma, g1 = nk * t1 + na * sigma;
+  const double glo = fmin(g0, g1), ghi = fmax(g0, g1);
+  const double B = f.bB;
+  double lo, hi;
+  if (fabs(nj) < 1e-12) {
+    if (glo > B + 1e-12 || ghi < -B - 1e-12) return false;
+    lo = -1.0;
+    hi = 1.0;
+  } else {
+    const double A0 = (-B - ghi) / nj, A1 = (B - glo) / nj;
+    lo = fmin(A0, A1) - pad;
+    hi = fmax(A0, A1) + pad;
+  }
+  if (lo > 1.0 || hi < -1.0) return false;
+  const double hn = 0.5 * (double)p.n;
+  xa = clampi(floor((fmax(lo, -1.0) + 1.0) * hn - 0.02), (int)p.n - 1);
+  xb = clampi(floor((fmin(hi, 1.0) + 1.0) * hn + 0.02), (int)p.n - 1);
+  return xa <= xb;
+}
+
+// A footprint as rows: each rect's rows, then (band) the 6 n rows of the cube map.
+__device__ inline uint32_t foot_rows(const BP& p, const Foot& f) {
+  uint32_t r = 0;
+  for (int q = 0; q < f.n; q++) r += (uint32_t)(f.y1[q] - f.y0[q] + 1);
+  if (f.band) r += 6u * p.n;
+  return r;
+}
+
+// entries of row `row`; with emit, written from `at` on, never at or past
+// `lim` (the prim's own range: a count/emission mismatch is flagged in
+// ctr[4], not written out of bounds)
+template <bool EMIT>
+__device__ inline uint32_t row_entries(const BP& p, const Foot& f, uint32_t prim, uint32_t row, uint64_t at,
+                                       uint64_t lim) {
+  for (int q = 0; q < f.n; q++) {
+    const uint32_t nr = (uint32_t)(f.y1[q] - f.y0[q] + 1);
+    if (row >= nr) {
+      row -= nr;
+      continue;
+    }
+    const int y = f.y0[q] + (int)row;
+    uint32_t c = 0;
+    for (int x = f.x0[q]; x <= f.x1[q]; x++)
+      if (cell_overlaps(p, f, q, x, y)) {
+        if (EMIT) {
+          if (at + c >= lim) {
+            p.ctr[4] = 1u;
+            return c;
+          }
+          p.keys[at + c] = ((unsigned long long)cell_index(p, f, q, x, y) << 32) | orderable(cell_key(p, f, x, y));
+          p.vals[at + c] = prim;
+        }
+        c++;
+      }
+    return c;
+  }
+  // band rows: always tested (key -inf)
+  const uint32_t face = row / p.n, y = row % p.n;
+  int xa = 0, xb = -1;
+  if (!band_row(p, f, face, y, xa, xb)) return 0;
+  if (EMIT) {
+    const uint32_t kb = orderable(-__builtin_inff());
+    for (int x = xa; x <= xb; x++) {
+      const uint64_t i = at + (uint64_t)(x - xa);
+      if (i >= lim) {
+        p.ctr[4] = 1u;
+        break;
+      }
+      p.keys[i] = ((unsigned long long)(face * p.n * p.n + y * p.n + (uint32_t)x) << 32) | kb;
+      p.vals[i] = prim;
+    }
+  }
+  return (uint32_t)(xb - xa + 1);
+}
+
+__device__ inline bool foot_is_big(const BP& p, const Foot& f) { return f.band || foot_cells(p, f) > kSmallCells; }
+
+__global__ __launch_bounds__(256) void rmin_kernel(BP p, uint32_t* bits) {
+  const uint32_t prim = blockIdx.x * blockDim.x + threadIdx.x;
+  if (prim >= p.nprim) return;
+  const float* r = (const float*)(p.tri + 3 * (size_t)prim);
+  const double v0[3] = {r[0], r[1], r[2]}, e1[3] = {r[3], r[4], r[5]}, e2[3] = {r[6], r[7], r[8]};
+  double C[3], rc = 0.0;
+  for (int a = 0; a < 3; a++) C[a] = v0[a] + (e1[a] + e2[a]) / 3.0;
+  for (int k = 0; k < 3; k++) {
+    double X[3];
+    for (int a = 0; a < 3; a++) X[a] = v0[a] + (k == 1 ? e1[a] : 0.0) + (k == 2 ? e2[a] : 0.0) - C[a];
+    rc = fmax(rc, norm3(X));
+  }
+  const double D[3] = {C[0] - p.lv[0], C[1] - p.lv[1], C[2] - p.lv[2]};
+  // a hit point lies on a triangle up to its float rounding (1e-6 s1 covers it)
+  const double dist = norm3(D) - rc * (1.0 + 1e-12) - 1e-6 * p.s1;
+  const float fd = dist > 0.0 ? __double2float_rd(dist) : 0.0f;
+  atomicMin(bits, __float_as_uint(fd));  // non-negative floats order as their bits
+}
+
 __global__ __launch_bounds__(256) void count_kernel(BP p) {
   const uint32_t prim = blockIdx.x * blockDim.x + threadIdx.x;
   if (prim >= p.nprim) return;
   Foot f;
   footprint(p, prim, f);
-  uint64_t c = 0;
-  if (f.global) {
+  uint32_t c = 0;
+  if (f.never) {
+    atomicAdd(p.ctr + 2, 1u);
+  } else if (f.global) {
     p.global[atomicAdd(p.ctr + 1, 1u)] = prim;
+  } else if (foot_is_big(p, f)) {
+    p.big[atomicAdd(p.ctr, 1u)] = prim;  // counted and emitted row-wise by a workgroup
+    if (f.band) atomicAdd(p.ctr + 3, 1u);
   } else {
-    c = foot_cells(p, f);
-    if (c > kSmallCells) {
-      p.big[atomicAdd(p.ctr, 1u)] = prim;  // emitted rect-wise by a workgroup
-    } else {
-      c = 0;  // small: only the cells the grown image overlaps
-      for (int q = 0; q < f.n; q++)
-        for (int y = f.y0[q]; y <= f.y1[q]; y++)
-          for (int x = f.x0[q]; x <= f.x1[q]; x++) c += cell_overlaps(p, f, q, x, y) ? 1u : 0u;
-    }
+    const uint32_t rows = foot_rows(p, f);
+    for (uint32_t r = 0; r < rows; r++) c += row_entries<false>(p, f, prim, r, 0, 0);
   }
-  p.count[prim] = (uint32_t)c;  // the host checks the total against 2^32
+  p.count[prim] = c;  // the host checks the total against 2^31
 }
 
-__device__ inline void emit_cell(const BP& p, const Foot& f, uint32_t prim, uint64_t i, uint64_t at) {
-  int q = 0;
-  for (;; q++) {
-    const uint64_t rc = (uint64_t)(f.x1[q] - f.x0[q] + 1) * (uint64_t)(f.y1[q] - f.y0[q] + 1);
-    if (i < rc) break;
-    i -= rc;
+__device__ inline uint32_t block_sum(uint32_t v, uint32_t* red) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  uint32_t t = 0;
+  for (int w = 0; w < kBlock / 64; w++) t += red[w];
+  __syncthreads();
+  return t;
+}
+
+// one workgroup per big footprint: its rows over the threads
+__global__ __launch_bounds__(256) void big_count_kernel(BP p) {
+  __shared__ uint32_t red[kBlock / 64];
+  for (uint32_t b = blockIdx.x; b < p.ctr[0]; b += gridDim.x) {
+    const uint32_t prim = p.big[b];
+    Foot f;
+    footprint(p, prim, f);
+    const uint32_t rows = foot_rows(p, f);
+    uint32_t s = 0;
+    for (uint32_t r = threadIdx.x; r < rows; r += kBlock) s += row_entries<false>(p, f, prim, r, 0, 0);
+    const uint32_t t = block_sum(s, red);
+    if (threadIdx.x == 0) p.count[prim] = t;
   }
-  const uint32_t wq = (uint32_t)(f.x1[q] - f.x0[q] + 1);
-  const int x = f.x0[q] + (int)(i % wq), y = f.y0[q] + (int)(i / wq);
-  const uint32_t cell = cell_index(p, f, q, x, y);
-  p.keys[at] = ((unsigned long long)cell << 32) | orderable(cell_key(p, f, x, y));
-  p.vals[at] = prim;
 }
 
 __global__ __launch_bounds__(256) void emit_kernel(BP p) {
   const uint32_t prim = blockIdx.x * blockDim.x + threadIdx.x;
   if (prim >= p.nprim) return;
-  const uint32_t c = p.count[prim];
-  if (c == 0) return;
+  if (p.count[prim] == 0) return;
   Foot f;
   footprint(p, prim, f);
-  if (foot_cells(p, f) > kSmallCells) return;  // big: emit_big_kernel
+  if (f.never || f.global || foot_is_big(p, f)) return;  // big: big_emit_kernel
   uint64_t at = p.off[prim];
-  for (int q = 0; q < f.n; q++)
-    for (int y = f.y0[q]; y <= f.y1[q]; y++)
-      for (int x = f.x0[q]; x <= f.x1[q]; x++)
-        if (cell_overlaps(p, f, q, x, y)) {
-          p.keys[at] = ((unsigned long long)cell_index(p, f, q, x, y) << 32) | orderable(cell_key(p, f, x, y));
-          p.vals[at] = prim;
-          at++;
-        }
+  const uint64_t lim = at + p.count[prim];
+  const uint32_t rows = foot_rows(p, f);
+  for (uint32_t r = 0; r < rows; r++) at += row_entries<true>(p, f, prim, r, at, lim);
 }
 
-// one workgroup per big footprint (ground planes, triangles near a point light)
-__global__ __launch_bounds__(256) void emit_big_kernel(BP p) {
+// one workgroup per big footprint: 256 rows at a time, each row's entries at
+// its exclusive prefix within the block
+__global__ __launch_bounds__(256) void big_emit_kernel(BP p) {
+  __shared__ uint32_t wsum[kBlock / 64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   for (uint32_t b = blockIdx.x; b < p.ctr[0]; b += gridDim.x) {
     const uint32_t prim = p.big[b];
     Foot f;
     footprint(p, prim, f);
-    const uint32_t c = p.count[prim];
-    const uint64_t o = p.off[prim];
-    for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) emit_cell(p, f, prim, i, o + i);
+    const uint32_t rows = foot_rows(p, f);
+    uint64_t base = p.off[prim];
+    const uint64_t lim = base + p.count[prim];
+    for (uint32_t r0 = 0; r0 < rows; r0 += kBlock) {
+      const uint32_t r = r0 + threadIdx.x;
+      const uint32_t c = r < rows ? row_entries<false>(p, f, prim, r, 0, 0) : 0u;
+      uint32_t incl = c;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+      }
+      if (lane == 63) wsum[wid] = incl;
+      __syncthreads();
+      uint32_t woff = 0, tot = 0;
+      for (int w = 0; w < kBlock / 64; w++) {
+        if (w < wid) woff += wsum[w];
+        tot += wsum[w];
+      }
+      if (c) row_entries<true>(p, f, prim, r, base + woff + incl - c, lim);
+      base += tot;
+      __syncthreads();
+    }
   }
 }
 
@@ -371,7 +781,7 @@ struct LBDevice {
   uint32_t* prim = nullptr;
   float* key = nullptr;
   uint32_t* global = nullptr;
-  unsigned long long entries = 0, cells = 0, nglobal = 0;
+  unsigned long long entries = 0, cells = 0, nglobal = 0, never = 0, band = 0;
 };
 
 static void cross3(const double* a, const double* b, double* o) {
@@ -396,6 +806,11 @@ extern "C" void rt_lightbuf_sizes(const LBDevice* d, unsigned long long* entries
   *global = d ? d->nglobal : 0;
 }
 
+extern "C" void rt_lightbuf_proof_counts(const LBDevice* d, unsigned long long* never, unsigned long long* band) {
+  *never = d ? d->never : 0;
+  *band = d ? d->band : 0;
+}
+
 #define LB_TRY(x)                                                                     \
   do {                                                                                \
     hipError_t e_ = (x);                                                              \
@@ -418,17 +833,24 @@ extern "C" int rt_lightbuf_build(const LBParams* in, RtLightBuf* out, LBDevice**
   uint32_t* off = nullptr;
   uint32_t* ctr = nullptr;
   uint32_t* big = nullptr;
+  uint32_t* rmin = nullptr;
   unsigned long long *k0 = nullptr, *k1 = nullptr;
   uint32_t* v0 = nullptr;
   void* tmp = nullptr;
   size_t tb = 0;
-  uint32_t hc[2] = {0, 0}, last_off = 0, last_cnt = 0;
+  uint32_t hc[5] = {0, 0, 0, 0, 0}, last_off = 0, last_cnt = 0;
   uint64_t total = 0, ncell = 0;
   const uint32_t np = in->nprim;
+  const dim3 gp((np + 255) / 256), bk(256);
   p.tri = in->tri;
   p.nprim = np;
   p.kind = in->kind;
-  for (int a = 0; a < 3; a++) p.lv[a] = in->lv[a];
+  p.proven = in->proven ? 1u : 0u;
+  for (int a = 0; a < 3; a++) {
+    p.lv[a] = in->lv[a];
+    p.olo[a] = in->box_lo[a];
+    p.ohi[a] = in->box_hi[a];
+  }
   p.slack = in->slack;
   p.s1 = in->s1;
   p.dmax = in->dmax;
@@ -442,7 +864,11 @@ extern "C" int rt_lightbuf_build(const LBParams* in, RtLightBuf* out, LBDevice**
       delete dev;
       return -1;
     }
-    for (int a = 0; a < 3; a++) w[a] /= wl;
+    for (int a = 0; a < 3; a++) {
+      p.d[a] = (double)(float)(-in->lv[a]);  // the rays' direction, exactly (cpu/light.c:53)
+      w[a] /= wl;
+    }
+    p.dlen = sqrt(p.d[0] * p.d[0] + p.d[1] * p.d[1] + p.d[2] * p.d[2]);
     int m = 0;
     for (int a = 1; a < 3; a++)
       if (fabs(w[a]) < fabs(w[m])) m = a;
@@ -459,6 +885,14 @@ extern "C" int rt_lightbuf_build(const LBParams* in, RtLightBuf* out, LBDevice**
       p.u[a] = out->u[a];
       p.v[a] = out->v[a];
       p.w[a] = out->w[a];
+    }
+    {
+      double su = 0.0, sv = 0.0;
+      for (int a = 0; a < 3; a++) {
+        su += p.u[a] * p.d[a] / p.dlen;
+        sv += p.v[a] * p.d[a] / p.dlen;
+      }
+      p.skew = (fmax(fabs(su), fabs(sv)) + 1e-15) * 1.01;
     }
     // grid over the projected scene box (in->lv unused beyond the axes)
     const double m0 = in->slack + 3.0 * kEps * in->s1 * 1.01 + 1e-9 * in->s1;
@@ -510,18 +944,28 @@ extern "C" int rt_lightbuf_build(const LBParams* in, RtLightBuf* out, LBDevice**
   }
   LB_TRY(hipMalloc((void**)&count, ((size_t)np + 1) * sizeof(uint32_t)));
   LB_TRY(hipMalloc((void**)&off, ((size_t)np + 1) * sizeof(uint32_t)));
-  LB_TRY(hipMalloc((void**)&ctr, 2 * sizeof(uint32_t)));
+  LB_TRY(hipMalloc((void**)&ctr, 5 * sizeof(uint32_t)));
   LB_TRY(hipMalloc((void**)&big, ((size_t)np + 1) * sizeof(uint32_t)));
   LB_TRY(hipMalloc((void**)&dev->global, ((size_t)np + 1) * sizeof(uint32_t)));
   LB_TRY(hipMalloc((void**)&dev->start, (ncell + 1) * sizeof(uint32_t)));
-  LB_TRY(hipMemsetAsync(ctr, 0, 2 * sizeof(uint32_t), s));
+  LB_TRY(hipMemsetAsync(ctr, 0, 5 * sizeof(uint32_t), s));
   LB_TRY(hipMemsetAsync(count + np, 0, sizeof(uint32_t), s));
   p.count = count;
   p.off = off;
   p.ctr = ctr;
   p.big = big;
   p.global = dev->global;
-  if (np) hipLaunchKernelGGL(count_kernel, dim3((np + 255) / 256), dim3(256), 0, s, p);
+  if (p.proven && p.kind == RT_LB_POINT) {
+    // the nearest shadow-ray origin's distance from the light (band widths)
+    LB_TRY(hipMalloc((void**)&rmin, sizeof(uint32_t)));
+    LB_TRY(hipMemsetAsync(rmin, 0x7f, sizeof(uint32_t), s));  // 0x7f7f7f7f: a large float
+    if (np) hipLaunchKernelGGL(rmin_kernel, gp, bk, 0, s, p, rmin);
+    LB_TRY(hipGetLastError());
+    p.rmin_bits = rmin;
+  }
+  if (np) hipLaunchKernelGGL(count_kernel, gp, bk, 0, s, p);
+  LB_TRY(hipGetLastError());
+  hipLaunchKernelGGL(big_count_kernel, dim3(2048), bk, 0, s, p);
   LB_TRY(hipGetLastError());
   LB_TRY(rocprim::exclusive_scan(nullptr, tb, count, off, 0u, (size_t)np + 1, rocprim::plus<uint32_t>(), s));
   LB_TRY(hipMalloc(&tmp, tb + 16));
@@ -553,6 +997,8 @@ extern "C" int rt_lightbuf_build(const LBParams* in, RtLightBuf* out, LBDevice**
   dev->entries = total;
   dev->cells = ncell;
   dev->nglobal = hc[1];
+  dev->never = hc[2];
+  dev->band = hc[3];
   LB_TRY(hipMalloc((void**)&dev->prim, (total + 1) * sizeof(uint32_t)));
   LB_TRY(hipMalloc((void**)&dev->key, (total + 1) * sizeof(float)));
   if (total) {
@@ -561,10 +1007,10 @@ extern "C" int rt_lightbuf_build(const LBParams* in, RtLightBuf* out, LBDevice**
     LB_TRY(hipMalloc((void**)&v0, total * sizeof(uint32_t)));
     p.keys = k0;
     p.vals = v0;
-    hipLaunchKernelGGL(emit_kernel, dim3((np + 255) / 256), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(emit_kernel, gp, bk, 0, s, p);
     LB_TRY(hipGetLastError());
     if (hc[0]) {
-      hipLaunchKernelGGL(emit_big_kernel, dim3(hc[0] < 4096 ? hc[0] : 4096), dim3(256), 0, s, p);
+      hipLaunchKernelGGL(big_emit_kernel, dim3(hc[0] < 4096 ? hc[0] : 4096), bk, 0, s, p);
       LB_TRY(hipGetLastError());
     }
     int bits = 32;
@@ -579,16 +1025,22 @@ extern "C" int rt_lightbuf_build(const LBParams* in, RtLightBuf* out, LBDevice**
     }
     sb = tb;
     LB_TRY(rocprim::radix_sort_pairs(tmp, sb, k0, k1, v0, dev->prim, (size_t)total, 0, bits, s));
-    hipLaunchKernelGGL(key_kernel, dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, s, k1,
-                       (uint32_t)total, dev->key);
+    hipLaunchKernelGGL(key_kernel, dim3((uint32_t)((total + 255) / 256)), bk, 0, s, k1, (uint32_t)total,
+                       dev->key);
     LB_TRY(hipGetLastError());
-    hipLaunchKernelGGL(start_kernel, dim3((uint32_t)((ncell + 256) / 256)), dim3(256), 0, s, k1,
-                       (uint32_t)total, (uint32_t)ncell, dev->start);
+    hipLaunchKernelGGL(start_kernel, dim3((uint32_t)((ncell + 256) / 256)), bk, 0, s, k1, (uint32_t)total,
+                       (uint32_t)ncell, dev->start);
     LB_TRY(hipGetLastError());
   } else {
     LB_TRY(hipMemsetAsync(dev->start, 0, (ncell + 1) * sizeof(uint32_t), s));
   }
+  LB_TRY(hipMemcpyAsync(hc + 4, ctr + 4, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   LB_TRY(hipStreamSynchronize(s));
+  if (hc[4]) {
+    snprintf(err, errlen, "light buffer emission disagreed with its count");
+    rc = -1;
+    goto done;
+  }
   out->start = dev->start;
   out->prim = dev->prim;
   out->key = dev->key;
@@ -599,6 +1051,7 @@ done:
   (void)hipFree(off);
   (void)hipFree(ctr);
   (void)hipFree(big);
+  (void)hipFree(rmin);
   (void)hipFree(k0);
   (void)hipFree(k1);
   (void)hipFree(v0);

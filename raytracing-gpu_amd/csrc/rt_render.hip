@@ -1591,6 +1591,33 @@ __global__ __launch_bounds__(64, ACCEL == RT_ACCEL_FLAT_D ? RT_FLAT_SHADE_MIN_WA
   flush_counts(p, wc, lane, true);
 }
 
+// Shadow-query probe (tests, tools): the shadow ray of light li from each
+// given origin (cpu/light.c:53,78), answered through the light's buffer
+// (brute = 0) or by brute force over the nprim prim-order records (brute = 1,
+// cpu/hit.c:93-109).  One thread per origin; out[i] = shadowed.
+__global__ __launch_bounds__(256) void probe_shadow_kernel(KParams p, const float* __restrict__ org, uint32_t n,
+                                                           uint32_t li, uint32_t nprim, int brute,
+                                                           uint32_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float* L = p.light + RT_LIGHT_FLOATS_D * li;
+  const uint32_t type = __float_as_uint(L[0]);
+  const f3 o{org[3 * (size_t)i], org[3 * (size_t)i + 1], org[3 * (size_t)i + 2]};
+  const Ray r = make_ray(p, o, shadow_dir(type, f3{L[4], L[5], L[6]}, o), p.eps_rel);
+  bool hit = false;
+  if (brute) {
+    uint32_t risk = 0;
+    for (uint32_t k = 0; k < nprim && !hit; k++) {
+      const float4* t = p.tri_prim + 3 * (size_t)k;
+      hit = any_hit_rec(r, t[0], t[1], t[2], risk);
+    }
+  } else {
+    LaneCount lc = {0, 0, 0, 0, 0, 0, 0};
+    hit = lbuf_any<false>(p, p.lbuf[li], r, lc);
+  }
+  out[i] = hit ? 1u : 0u;
+}
+
 // A pixel's four samples (trace_kernel items 4t..4t+3): each sample's path
 // terms summed deepest-first, acc = color_add(reflected, term)
 // (cpu/raytracer.c:29-30), then acc = color_add(acc, color_mul(s, 0.25)) over
@@ -1903,6 +1930,14 @@ extern "C" hipError_t rt_launch_trace(const KParams* p, int accel, int count_wor
 extern "C" hipError_t rt_launch_shade(const KParams* p, int accel, int count_work, int policy,
                                       int grid, hipStream_t stream) {
   return launch_kernel(kernel_of<false>(accel, count_work, policy), grid, p, stream);
+}
+
+extern "C" hipError_t rt_launch_probe_shadow(const KParams* p, const float* org, uint32_t n, uint32_t li,
+                                             uint32_t nprim, int brute, uint32_t* out, hipStream_t stream) {
+  if (n == 0) return hipGetLastError();
+  hipLaunchKernelGGL(rt::probe_shadow_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, *p, org, n, li, nprim,
+                     brute, out);
+  return hipGetLastError();
 }
 
 extern "C" hipError_t rt_launch_fold(const KParams* p, hipStream_t stream) {

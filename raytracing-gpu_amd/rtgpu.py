@@ -108,7 +108,8 @@ class AccelInfo(C.Structure):
                 ("device_bytes", C.c_ulonglong), ("build_seconds", C.c_double),
                 ("max_leaf", C.c_ulonglong), ("shadow_global", C.c_ulonglong),
                 ("shadow_mu_max", C.c_double), ("lightbuf_entries", C.c_ulonglong),
-                ("lightbuf_global", C.c_ulonglong), ("lightbuf_seconds", C.c_double)]
+                ("lightbuf_global", C.c_ulonglong), ("lightbuf_seconds", C.c_double),
+                ("lightbuf_never", C.c_ulonglong), ("lightbuf_band", C.c_ulonglong)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -156,6 +157,7 @@ _PROTOS = [
     ("rt_hip_set_policy", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_set_exact_shadows", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_set_light_buffers", C.c_int, [C.c_void_p, C.c_int]),
+    ("rt_hip_probe_shadows", C.c_int, [C.c_void_p, C.c_uint, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]),
     ("rt_hip_tile_cycles", C.c_int, [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_size_t]),
     ("rt_hip_tile_phase_cycles", C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_ulonglong),
                                            C.c_size_t]),
@@ -445,6 +447,16 @@ class Context:
     def set_light_buffers(self, on=True):
         """Light buffers for the default shadow queries (rt_hip_set_light_buffers)."""
         _check(lib().rt_hip_set_light_buffers(self.h, 1 if on else 0), "light_buffers")
+
+    def probe_shadows(self, light, origins, brute=False):
+        """Shadow rays of light `light` from (n, 3) origins: shadowed flags
+        through the light buffer, or brute force (rt_hip_probe_shadows)."""
+        o = np.ascontiguousarray(origins, dtype=np.float32).reshape(-1, 3)
+        out = np.zeros(len(o), np.uint8)
+        _check(lib().rt_hip_probe_shadows(self.h, int(light), o.ctypes.data_as(C.c_void_p), len(o),
+                                          1 if brute else 0, out.ctypes.data_as(C.c_void_p)),
+               "probe_shadows")
+        return out.astype(bool)
 
     def set_exact_shadows(self, on=True):
         """Proven shadow walk (rt_hip_set_exact_shadows; slow near terminators)."""

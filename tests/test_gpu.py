@@ -8,6 +8,7 @@ bit-exact equality (0 ULP) and report the ULP histogram when it fails.
 import hashlib
 import os
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -372,9 +373,11 @@ def test_shadow_queries_match_brute_force(gpu, accel, policy, exact, lbuf):
         assert ctx.info()["lightbuf_entries"] > 0
     ctx.set_light_buffers(lbuf)
     ctx.set_policy(policy)
-    if exact:  # the proven shadow walk (csrc/rt_shadow.hip)
+    if exact:  # proven light buffers, or (staged policies) the proven walk
         ctx.set_exact_shadows(True)
         assert ctx.info()["shadow_mu_max"] >= 1.0
+        if lbuf:
+            assert ctx.info()["lightbuf_entries"] > 0
     img, _ = ctx.render_image(s.frame())
     v = ctx.verify_shadows(1)
     assert v["records"] > 100000 and v["queries"] == 2 * v["records"], v
@@ -399,8 +402,9 @@ def test_no_camera_lists_with_light_buffers(gpu, exact_shadows):
     assert_bitexact(img_nc, img, "without camera candidate lists")
 
 
-@pytest.mark.parametrize("height", [0.02, 0.5])
-def test_light_buffer_point_light_near_surface(gpu, height):
+@pytest.mark.parametrize("height,exact", [(0.02, False), (0.5, False), (0.02, True), (0.5, True),
+                                          (0.0, True)])
+def test_light_buffer_point_light_near_surface(gpu, height, exact):
     """A point light just above a sphere: triangles around it span wide
     angles of the light's cube map (or go to its global list); every shadow
     query still equals brute force, and the image equals the walk's."""
@@ -413,12 +417,18 @@ def test_light_buffer_point_light_near_surface(gpu, height):
     L.v.x, L.v.y, L.v.z = float(top[k, 0]), float(top[k, 1]) + height, float(top[k, 2])
     f = s.frame()
     ctx = gpu.Context(s, "octree_gpu")
+    if exact:  # proven footprints (a light on the sphere: its tangent plane)
+        ctx.set_exact_shadows(True)
     img, _ = ctx.render_image(f)
     v = ctx.verify_shadows(1)
     assert v["records"] > 10000 and v["records_differ"] == 0 and v["walk_lit_brute_shadowed"] == 0, v
-    ctx.set_light_buffers(False)
-    img_w, _ = ctx.render_image(f)
-    assert_bitexact(img, img_w, f"light buffers vs walk, light {height} above a sphere")
+    if exact:  # brute force is the reference for the proven mode
+        img_w, _ = gpu.Context(s, "flat").render_image(f)
+    else:
+        ctx.set_light_buffers(False)
+        img_w, _ = ctx.render_image(f)
+    assert_bitexact(img, img_w, f"light buffers (exact={exact}) vs {'flat' if exact else 'walk'}, "
+                                f"light {height} above a sphere")
 
 
 def test_exact_camera_rank_split(gpu):
@@ -530,3 +540,28 @@ def test_rt_gpu_cli_png(gpu, scene_dir, tmp_path):
     s = gpu.Scene.load_svati(str(src))
     ref, _ = orc.render_gpu(s.ptr, 80, 45, threads=8)
     assert np.array_equal(decode_png(str(out)), ref)
+
+
+@pytest.mark.parametrize("exact", [True, False])
+@pytest.mark.parametrize("li", [1, 2])
+def test_light_buffer_probe_grazing(gpu, li, exact):
+    """Shadow rays built to graze triangles (module helper grazing_origins):
+    the light buffer's answer equals brute force over every triangle for
+    every origin when its footprints are proven (rt_hip_set_exact_shadows);
+    the slack-grown default is reported, and must agree on this scene too."""
+    s = gpu.Scene.synthetic(3, 3, 9776, seed=0x5EED, width=96, height=54)
+    tri = s.triangles_array()
+    L = s.s.lights[li]
+    lv = np.array([L.v.x, L.v.y, L.v.z], np.float64)
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    from grazing import grazing_origins
+    o = grazing_origins(tri, int(L.type), lv, 4000, 40)
+    assert len(o) > 50000
+    ctx = gpu.Context(s, "octree_gpu")
+    ctx.set_exact_shadows(exact)
+    got = ctx.probe_shadows(li, o)
+    ref = ctx.probe_shadows(li, o, brute=True)
+    bad = np.flatnonzero(got != ref)
+    assert 0.01 < ref.mean() < 0.99, ref.mean()
+    assert len(bad) == 0, (f"{len(bad)} of {len(o)} grazing shadow rays differ from brute force "
+                           f"(buffer lit, brute shadowed: {int((~got & ref).sum())}); first {bad[:5].tolist()}")
