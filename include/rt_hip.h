@@ -226,6 +226,14 @@ int rt_hip_set_exact_camera(rt_hip_ctx *ctx, int enable);
  * Both are exact in the same sense (DESIGN.md §2 "Shadow rays"). */
 int rt_hip_set_light_buffers(rt_hip_ctx *ctx, int enable);
 int rt_hip_set_exact_shadows(rt_hip_ctx *ctx, int enable);
+/* Host-only survey (no device) of light `light`'s buffer as rt_hip_create
+ * builds it for this scene (exact = proven footprints), every stride-th
+ * triangle: out[0] entries, [1] triangles never accepted, [2] global, [3] band
+ * triangles, [4] big footprints, [5] triangles surveyed, [6] band-row entries,
+ * [7] largest per-triangle count, [8] its triangle (prim order), [9] entries of
+ * triangles with more than 1024, [10] with 65..1024, [11] triangles with more than 64. */
+int rt_lightbuf_survey(const rt_scene *scene, unsigned light, int exact, unsigned stride,
+                       unsigned long long out[12]);
 /* Shadow-query probe (tests, tools): light `light`'s shadow ray
  * (cpu/light.c:53,78) from each of n origins (x, y, z floats), answered
  * through the context's light buffer (brute = 0) or by brute force over every

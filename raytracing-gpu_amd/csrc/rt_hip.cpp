@@ -66,6 +66,7 @@ struct rt_hip_ctx {
   uint32_t nrec = 0, nlight = 0;
   rt_accel_info info{};
   float scene_c[3]{}, scene_r = 0;
+  float scene_lo[3]{}, scene_hi[3]{};  // the triangles' bounding box
   float eps_ulps = RT_EPS_ULPS_DEFAULT;
   float cam_eps_ulps = RT_CAM_EPS_ULPS_DEFAULT;
   int policy = RT_POLICY_DEFAULT;  // traversal policy (tests / A/B only: rt_hip_set_policy)
@@ -301,6 +302,55 @@ static void lbuf_release(rt_hip_ctx* c) {
   c->lb_ulps = -1.0f;
 }
 
+// The build parameters of one light's buffer for a scene of nprim triangles
+// in the box (scene_c, scene_r) and the culling slack eps_ulps.
+static void lb_fill(LBParams& lp, const float scene_c[3], float scene_r, const float aabb_lo[3],
+                    const float aabb_hi[3], float eps_ulps, uint32_t type, const float lv[3], uint32_t nprim,
+                    int proven) {
+  std::memset(&lp, 0, sizeof lp);
+  // a shadow ray leaves a hit point: inside the scene cube up to the float
+  // error of the hit, so its slack eps(o) (host/rt_cull.h, float) is at most
+  const double R = scene_r, eps_rel = (double)(eps_ulps * 5.9604645e-8f);
+  const double cmag = std::fmax(std::fabs(scene_c[0]), std::fmax(std::fabs(scene_c[1]), std::fabs(scene_c[2])));
+  const double slack = (eps_rel * (2.0 * R * 1.001 + 1e-3) + (double)RT_CULL_PLANE * (cmag + R) + 1e-6) * 1.01;
+  double lo[3], hi[3], s1 = 0.0;
+  for (int a = 0; a < 3; a++) {
+    if (proven) {
+      // the proof's origin box: the triangles' box grown by 1 + 1 % of the
+      // scene (hit points off it -- float garbage hits beyond that -- are
+      // counted by the shade pass, never assumed)
+      const double g = 1.0 + 0.02 * R;
+      lo[a] = (double)aabb_lo[a] - g;
+      hi[a] = (double)aabb_hi[a] + g;
+    } else {
+      lo[a] = scene_c[a] - R * 1.001 - 1e-3;
+      hi[a] = scene_c[a] + R * 1.001 + 1e-3;
+    }
+    s1 += std::fmax(std::fabs(lo[a]), std::fabs(hi[a]));
+  }
+  lp.nprim = nprim;
+  lp.kind = type == 1 ? RT_LB_DIR : RT_LB_POINT;
+  double dmax = 0.0;
+  for (int a = 0; a < 3; a++) {
+    lp.lv[a] = lv[a];
+    lp.box_lo[a] = lo[a];
+    lp.box_hi[a] = hi[a];
+  }
+  for (int k = 0; k < 8; k++) {
+    double d2 = 0.0;
+    for (int a = 0; a < 3; a++) {
+      const double x = ((k >> a) & 1 ? hi[a] : lo[a]) - lp.lv[a];
+      d2 += x * x;
+    }
+    dmax = std::fmax(dmax, std::sqrt(d2));
+  }
+  lp.slack = slack;
+  lp.s1 = s1;
+  lp.dmax = dmax * 1.01 + 1.0;
+  lp.target_cells = nprim < 4096u ? 4096u : (nprim > (1u << 24) ? (1u << 24) : nprim);
+  lp.proven = proven ? 1u : 0u;
+}
+
 static int lbuf_prepare(rt_hip_ctx* c, hipStream_t s) {
   if (!c->light_buffers || c->accel != RT_ACCEL_OCTREE || !c->d_node || !c->nlight) return RT_OK;
   if (c->d_lbuf && c->lb_ulps == c->eps_ulps && c->lb_proven == c->exact_shadows) return RT_OK;
@@ -308,46 +358,14 @@ static int lbuf_prepare(rt_hip_ctx* c, hipStream_t s) {
   c->lb_dev.assign(c->nlight, nullptr);
   std::vector<RtLightBuf> hb(c->nlight);
   std::memset(hb.data(), 0, hb.size() * sizeof(RtLightBuf));
-  // a shadow ray leaves a hit point: inside the scene cube up to the float
-  // error of the hit, so its slack eps(o) (host/rt_cull.h, float) is at most
-  const double R = c->scene_r, eps_rel = (double)(c->eps_ulps * 5.9604645e-8f);
-  const double cmag = std::fmax(std::fabs(c->scene_c[0]), std::fmax(std::fabs(c->scene_c[1]),
-                                                                  std::fabs(c->scene_c[2])));
-  const double slack = (eps_rel * (2.0 * R * 1.001 + 1e-3) + (double)RT_CULL_PLANE * (cmag + R) + 1e-6) * 1.01;
-  double lo[3], hi[3], s1 = 0.0;
-  for (int a = 0; a < 3; a++) {
-    lo[a] = c->scene_c[a] - R * 1.001 - 1e-3;
-    hi[a] = c->scene_c[a] + R * 1.001 + 1e-3;
-    s1 += std::fmax(std::fabs(lo[a]), std::fabs(hi[a]));
-  }
   char err[256] = {0};
   for (uint32_t li = 0; li < c->nlight; li++) {
     const uint32_t t = c->light_type[li];
     if (t != 1 && t != 2) continue;
     LBParams lp;
-    std::memset(&lp, 0, sizeof lp);
+    lb_fill(lp, c->scene_c, c->scene_r, c->scene_lo, c->scene_hi, c->eps_ulps, t, &c->light_v[3 * li], c->nprim,
+            c->exact_shadows);
     lp.tri = c->d_tri_prim;
-    lp.nprim = c->nprim;
-    lp.kind = t == 1 ? RT_LB_DIR : RT_LB_POINT;
-    double dmax = 0.0;
-    for (int a = 0; a < 3; a++) {
-      lp.lv[a] = c->light_v[3 * li + a];
-      lp.box_lo[a] = lo[a];
-      lp.box_hi[a] = hi[a];
-    }
-    for (int k = 0; k < 8; k++) {
-      double d2 = 0.0;
-      for (int a = 0; a < 3; a++) {
-        const double x = ((k >> a) & 1 ? hi[a] : lo[a]) - lp.lv[a];
-        d2 += x * x;
-      }
-      dmax = std::fmax(dmax, std::sqrt(d2));
-    }
-    lp.slack = slack;
-    lp.s1 = s1;
-    lp.dmax = dmax * 1.01 + 1.0;
-    lp.target_cells = c->nprim < 4096u ? 4096u : (c->nprim > (1u << 24) ? (1u << 24) : c->nprim);
-    lp.proven = c->exact_shadows ? 1u : 0u;
     if (rt_lightbuf_build(&lp, &hb[li], &c->lb_dev[li], s, err, sizeof err)) {
       lbuf_release(c);
       return rt_set_error(RT_EHIP, "light buffer of light %u: %s", li, err);
@@ -371,6 +389,36 @@ static int lbuf_prepare(rt_hip_ctx* c, hipStream_t s) {
   c->info.lightbuf_never = tnv;
   c->info.lightbuf_band = tbd;
   return RT_OK;
+}
+
+// Host-only survey of a light's buffer as rt_hip_create would build it for
+// this scene (prim-order records, the scene's box, the default culling
+// slack): rt_lightbuf_survey_host's counts (csrc/rt_lightbuf.h).
+extern "C" int rt_lightbuf_survey(const rt_scene* scene, unsigned light, int exact, unsigned stride,
+                                  unsigned long long out[12]) {
+  if (!scene || !out) return rt_set_error(RT_EINVAL, "null argument");
+  if (light >= scene->light_count || (scene->lights[light].type != 1 && scene->lights[light].type != 2))
+    return rt_set_error(RT_EINVAL, "light %u is not a directional or point light", light);
+  rt_flat_scene fs;
+  int rc = rt_flatten(scene, RT_ACCEL_FLAT, &fs);
+  if (rc) return rc;
+  float sc[3], sr = 0.0f, blo[3], bhi[3];
+  for (int a = 0; a < 3; a++) {
+    const float lo = fs.ntri ? fs.scene_lo[a] : 0.0f, hi = fs.ntri ? fs.scene_hi[a] : 0.0f;
+    sc[a] = 0.5f * (lo + hi);
+    sr = std::fmax(sr, 0.5f * (hi - lo));
+    blo[a] = lo;
+    bhi[a] = hi;
+  }
+  const float lv[3] = {scene->lights[light].v.x, scene->lights[light].v.y, scene->lights[light].v.z};
+  LBParams lp;
+  lb_fill(lp, sc, sr, blo, bhi, (float)RT_EPS_ULPS_DEFAULT, (uint32_t)scene->lights[light].type, lv,
+          (uint32_t)fs.ntri, exact);
+  lp.tri = (const float4*)fs.tri;
+  char err[256] = {0};
+  if (rt_lightbuf_survey_host(&lp, stride, out, err, sizeof err)) rc = rt_set_error(RT_EINVAL, "%s", err);
+  rt_flat_free(&fs);
+  return rc;
 }
 
 extern "C" int rt_hip_set_light_buffers(rt_hip_ctx* c, int enable) {
@@ -465,6 +513,8 @@ extern "C" int rt_hip_create(int device, const rt_scene* scene, int accel, rt_hi
   }
   for (int a = 0; a < 3; a++) {
     float lo = fs.ntri ? fs.scene_lo[a] : 0.0f, hi = fs.ntri ? fs.scene_hi[a] : 0.0f;
+    c->scene_lo[a] = lo;
+    c->scene_hi[a] = hi;
     c->scene_c[a] = 0.5f * (lo + hi);
     c->scene_r = std::fmax(c->scene_r, 0.5f * (hi - lo));
   }
@@ -1388,8 +1438,8 @@ extern "C" int rt_hip_stats(rt_hip_ctx* c, rt_stats* out) {
                         out->shadow_zero_risk);
   if (out->shadow_unproven)
     return rt_set_error(RT_EINEXACT,
-                        "%llu point-light shadow rays left from beyond the extent the shadow "
-                        "walk's exactness bound assumes (csrc/rt_shadow.hip)",
+                        "%llu shadow rays left from beyond the extent the exact shadow mode's "
+                        "bound assumes (csrc/rt_shadow.hip, csrc/rt_lightbuf.hip)",
                         out->shadow_unproven);
   // tuning knobs that give up the parity guarantee (A/B measurements only):
   // the image is complete, but not promised to equal cpu/rt's

@@ -32,6 +32,11 @@ struct RtLightBuf {
   const float* key;        // per entry, ascending within a cell: a query stops at key > its limit
   const uint32_t* global;  // prims every query of this light tests (footprint unbounded)
   uint32_t nglobal;
+  // proven footprints (LBParams::proven) hold for shadow rays leaving this
+  // box (floats inside the build's box); the shade pass counts the others
+  // (rt_stats.shadow_unproven -> RT_EINEXACT)
+  uint32_t proven;
+  float olo[3], ohi[3];
 };
 
 // Build parameters (host -> rt_lightbuf_build).
@@ -61,6 +66,12 @@ extern "C" void rt_lightbuf_free(LBDevice* dev);
 // entries and cells of a built buffer (bench / info)
 extern "C" void rt_lightbuf_sizes(const LBDevice* dev, unsigned long long* entries,
                                   unsigned long long* cells, unsigned long long* global);
+// The same footprints counted on the host (in->tri = host prim-order
+// records), every stride-th prim: out[0] entries, [1] never accepted, [2]
+// global, [3] band prims, [4] big prims, [5] prims surveyed, [6] band-row
+// entries, [7] largest per-prim count, [8] its prim.
+extern "C" int rt_lightbuf_survey_host(const LBParams* in, uint32_t stride, unsigned long long out[12],
+                                       char* err, size_t errlen);
 // proven mode: triangles no ray of the light can make the float test accept
 // (skipped), and triangles listed along a band of the cube map (point lights)
 extern "C" void rt_lightbuf_proof_counts(const LBDevice* dev, unsigned long long* never,

@@ -57,6 +57,8 @@
 
 namespace rtl {
 
+#define RTL_FN __host__ __device__
+
 constexpr double kEps = 0x1p-24;
 constexpr double kInvSqrt3 = 0.57735026918962573;
 constexpr double kSqrt3 = 1.7320508075688772;
@@ -79,7 +81,7 @@ struct BP {
   double olo[3], ohi[3];    // the origin box (LBParams::box_lo/hi)
   double d[3], dlen;        // DIR: the rays' direction -l.v (float) and its length
   double skew;              // DIR: max |u.d^|, |v.d^| (the float axes vs the exact direction)
-  const uint32_t* rmin_bits;  // POINT proven: float bits of a lower bound of |o - l.v| over origins
+  double rmin_o;             // POINT proven: a lower bound of |o - l.v| over shadow-ray origins
   uint32_t* count;
   uint32_t* off;
   unsigned long long* keys;
@@ -113,9 +115,9 @@ struct Foot {
   double bn[3], bB;
 };
 
-__device__ inline double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
-__device__ inline double norm3(const double* a) { return sqrt(dot3(a, a)); }
-__device__ inline void cross3d(const double* a, const double* b, double* o) {
+RTL_FN inline double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+RTL_FN inline double norm3(const double* a) { return sqrt(dot3(a, a)); }
+RTL_FN inline void cross3d(const double* a, const double* b, double* o) {
   o[0] = a[1] * b[2] - a[2] * b[1];
   o[1] = a[2] * b[0] - a[0] * b[2];
   o[2] = a[0] * b[1] - a[1] * b[0];
@@ -129,13 +131,13 @@ __device__ inline float unorder(uint32_t b) {
   return __uint_as_float((b & 0x80000000u) ? (b & 0x7fffffffu) : ~b);
 }
 
-__device__ inline int clampi(double x, int hi) {
+RTL_FN inline int clampi(double x, int hi) {
   if (!(x > 0.0)) return 0;  // NaN -> 0
   if (x >= (double)hi) return hi;
   return (int)x;
 }
 
-__device__ inline void foot_init(Foot& f) {
+RTL_FN inline void foot_init(Foot& f) {
   f.n = 0;
   f.global = false;
   f.never = false;
@@ -148,7 +150,7 @@ __device__ inline void foot_init(Foot& f) {
 
 // DIR: rect and image of the points P[0..2] (the triangle, or T_D) projected
 // on (u, v) with margin m; the plane of the triangle for the per-cell keys
-__device__ inline void dir_rect(const BP& p, const double P[3][3], const double* v0, const double* e1,
+RTL_FN inline void dir_rect(const BP& p, const double P[3][3], const double* v0, const double* e1,
                                 const double* e2, double m, Foot& f, double& hw) {
   double lu = 1e300, hu = -1e300, lvv = 1e300, hvv = -1e300;
   hw = -1e300;
@@ -184,7 +186,7 @@ __device__ inline void dir_rect(const BP& p, const double P[3][3], const double*
 // POINT: the cube-map rects of the cone from the light around the ball
 // (C, rb), widened by alpha, and the central projection of V grown by beta
 // for the overlap test.  false: the cone is too wide (global list).
-__device__ inline bool point_cone(const BP& p, const double V[3][3], const double C[3], double rb, double& rmin,
+RTL_FN inline bool point_cone(const BP& p, const double V[3][3], const double C[3], double rb, double& rmin,
                                   double grow, Foot& f) {
   const double D[3] = {C[0] - p.lv[0], C[1] - p.lv[1], C[2] - p.lv[2]};
   const double dc = norm3(D);
@@ -243,7 +245,7 @@ __device__ inline bool point_cone(const BP& p, const double V[3][3], const doubl
 }
 
 // ---- slack-grown footprints (default) ----
-__device__ void footprint_slack(const BP& p, const double V[3][3], const double* v0, const double* e1,
+RTL_FN void footprint_slack(const BP& p, const double V[3][3], const double* v0, const double* e1,
                                 const double* e2, Foot& f) {
   if (p.kind == RT_LB_DIR) {
     // the query's float projection of its origin is within 3 eps s1 of the
@@ -282,30 +284,21 @@ __device__ void footprint_slack(const BP& p, const double V[3][3], const double*
 }
 
 // ---- proven footprints (module comment) ----
-__device__ void footprint_dir_proven(const BP& p, const double* v0, const double* e1, const double* e2, Foot& f) {
+RTL_FN void footprint_dir_proven(const BP& p, const double* v0, const double* e1, const double* e2, Foot& f) {
   const double* d = p.d;
   double n[3];
   cross3d(e1, e2, n);
   const double A = fabs(dot3(n, d));  // |a| exact: a = e1.(d x e2) = -d.n, every ray alike
-  double M[3], S[3], N[3];
+  double M[3], S[3];
   for (int i = 0; i < 3; i++) S[i] = fmax(fabs(p.olo[i] - v0[i]), fabs(p.ohi[i] - v0[i]));
+  double Ea = 0.0;
   for (int i = 0; i < 3; i++) {
     const int j = (i + 1) % 3, k = (i + 2) % 3;
     M[i] = fabs(d[j]) * fabs(e2[k]) + fabs(d[k]) * fabs(e2[j]);
-    N[i] = S[j] * fabs(e1[k]) + S[k] * fabs(e1[j]);
-  }
-  double Ea = 0.0, Esh = 0.0, Edq = 0.0, Eeq = 0.0;
-  for (int i = 0; i < 3; i++) {
     Ea += fabs(e1[i]) * M[i];
-    Esh += S[i] * M[i];
-    Edq += fabs(d[i]) * N[i];
-    Eeq += fabs(e2[i]) * N[i];
   }
   const double r1 = 1.0 + 1e-6;
   Ea *= kCWA * kEps * r1;
-  Esh *= kCW * kEps * r1;
-  Edq *= kCW * kEps * r1;
-  Eeq *= kCW * kEps * r1;
   if (A + Ea < kAMin * (1.0 - 1e-9)) {  // |a_f| < 1e-7 for every ray: rejected (cpu/hit.c:19)
     f.never = true;
     return;
@@ -316,13 +309,54 @@ __device__ void footprint_dir_proven(const BP& p, const double* v0, const double
     f.global = true;
     return;
   }
-  const double du = Esh / (alb * (1.0 - rho)), dv = Edq / (alb * (1.0 - rho));
-  const double dw = (4.0 * kEps + (Esh + Edq) / alb + rho) / (1.0 - rho);
-  // T_D's corners (U, V) = (-du, -dv), (1 + dw + dv, -dv), (-du, 1 + dw + du)
-  const double cU[3] = {-du, 1.0 + dw + dv, -du}, cV[3] = {-dv, -dv, 1.0 + dw + du};
+  const double C[3] = {v0[0] + (e1[0] + e2[0]) / 3.0, v0[1] + (e1[1] + e2[1]) / 3.0, v0[2] + (e1[2] + e2[2]) / 3.0};
+  const double ud[3] = {-d[0] / p.dlen, -d[1] / p.dlen, -d[2] / p.dlen};  // from X back toward the origin
+  double du = 0.0, dv = 0.0, dw = 0.0, Eeq = 0.0;
   double P[3][3];
-  for (int k = 0; k < 3; k++)
-    for (int a = 0; a < 3; a++) P[k][a] = v0[a] + cU[k] * e1[a] + cV[k] * e2[a];
+  // T_D with |S_i| <= the box bound, then again with the origins' own bound:
+  // an accepting ray's origin o = X - t d (t >= 0) lies in the box, X in T_D
+  // (every step valid for every accepting ray, so each bound is)
+  for (int pass = 0; pass < 3; pass++) {
+    double N[3], Esh = 0.0, Edq = 0.0;
+    Eeq = 0.0;
+    for (int i = 0; i < 3; i++) {
+      const int j = (i + 1) % 3, k = (i + 2) % 3;
+      N[i] = S[j] * fabs(e1[k]) + S[k] * fabs(e1[j]);
+    }
+    for (int i = 0; i < 3; i++) {
+      Esh += S[i] * M[i];
+      Edq += fabs(d[i]) * N[i];
+      Eeq += fabs(e2[i]) * N[i];
+    }
+    Esh *= kCW * kEps * r1;
+    Edq *= kCW * kEps * r1;
+    Eeq *= kCW * kEps * r1;
+    du = Esh / (alb * (1.0 - rho));
+    dv = Edq / (alb * (1.0 - rho));
+    dw = (4.0 * kEps + (Esh + Edq) / alb + rho) / (1.0 - rho);
+    // T_D's corners (U, V) = (-du, -dv), (1 + dw + dv, -dv), (-du, 1 + dw + du)
+    const double cU[3] = {-du, 1.0 + dw + dv, -du}, cV[3] = {-dv, -dv, 1.0 + dw + du};
+    double rX = 0.0;
+    for (int k = 0; k < 3; k++) {
+      double w[3];
+      for (int a = 0; a < 3; a++) {
+        P[k][a] = v0[a] + cU[k] * e1[a] + cV[k] * e2[a];
+        w[a] = P[k][a] - C[a];
+      }
+      rX = fmax(rX, norm3(w));
+    }
+    rX = rX * (1.0 + 1e-9) + 1e-9;
+    if (pass == 2) break;
+    // the origin lies on the line behind X: t <= the box exit along ud
+    double tex = 1e300;
+    for (int a = 0; a < 3; a++) {
+      if (ud[a] > 0.0) tex = fmin(tex, (p.ohi[a] - (C[a] - rX)) / ud[a]);
+      if (ud[a] < 0.0) tex = fmin(tex, ((C[a] + rX) - p.olo[a]) / -ud[a]);
+    }
+    tex = fmax(tex, 0.0) * (1.0 + 1e-9);
+    for (int i = 0; i < 3; i++)
+      S[i] = fmin(S[i], (fabs(C[i] - v0[i]) + rX + tex * fabs(ud[i])) * (1.0 + 1e-9));
+  }
   const double Smax = sqrt(S[0] * S[0] + S[1] * S[1] + S[2] * S[2]);
   const double ext = (1.0 + du + dv + dw) * (norm3(e1) + norm3(e2));
   // the query's float projection (3 eps s1), and X - o along d seen through
@@ -338,7 +372,7 @@ __device__ void footprint_dir_proven(const BP& p, const double* v0, const double
 
 // reach of T_D beyond T for rays at cosine c (|d| cancels), Cauchy-Schwarz
 // form as csrc/rt_shadow.hip; > 1e300: no bound
-__device__ inline double reach_at(double c, double nl, double ea, double l1, double l2, double Smax) {
+RTL_FN inline double reach_at(double c, double nl, double ea, double l1, double l2, double Smax) {
   const double den = nl * c - ea;
   if (!(den > 2.0001 * ea) || !(den > 0.0)) return 1e301;
   const double rho = ea / den, kap = kCDot * kEps / den;
@@ -346,8 +380,40 @@ __device__ inline double reach_at(double c, double nl, double ea, double l1, dou
   return (kap * ls * (lmax + ls) * Smax / (1.0 - rho) + (4.0 * kEps + rho) * lmax / (1.0 - rho)) * (1.0 + 1e-6);
 }
 
-__device__ void footprint_point_proven(const BP& p, const double V[3][3], const double* v0, const double* e1,
-                                       const double* e2, Foot& f) {
+// |o - v0| over the origins of accepting shadow rays of a point light that
+// cross T's plane within rX of T's centroid C: o lies on a line through X
+// (|X - C| <= rX) passing within dline of the light, either beyond X (o = X +
+// lam u, u = (X - l.v) / |X - l.v|, the crossing between o and the light) or
+// beyond the light (o = l.v - mu u, the crossing past the light); every such
+// o is in the origin box, so lam, mu <= the box's exit along u's cone.
+RTL_FN double point_smax(const BP& p, const double* C, const double* v0, double rX, double dline, double sbox) {
+  const double D[3] = {C[0] - p.lv[0], C[1] - p.lv[1], C[2] - p.lv[2]};
+  const double dc = norm3(D);
+  if (!(dc > 2.0 * (rX + dline) + 1e-9)) return sbox;
+  // |u - c^| <= the cone's half-angle (plus the line's offset from the light)
+  const double th = asin(fmin(1.0, (rX + dline) / dc)) + (rX + dline) / (dc - rX - dline) * 1e-6 + 1e-12;
+  const double sp = fmin(2.0, th * 1.001);
+  double lam = 1e300, mu = 1e300;
+  for (int a = 0; a < 3; a++) {
+    const double ulo = D[a] / dc - sp, uhi = D[a] / dc + sp;
+    if (ulo > 0.0) lam = fmin(lam, (p.ohi[a] - (C[a] - rX)) / ulo);
+    if (uhi < 0.0) lam = fmin(lam, ((C[a] + rX) - p.olo[a]) / -uhi);
+    // beyond the light along -u
+    // (from the line's point nearest the light, within dline of it)
+    if (-uhi > 0.0) mu = fmin(mu, (p.ohi[a] - p.lv[a] + dline) / -uhi);
+    if (-ulo < 0.0) mu = fmin(mu, (p.lv[a] + dline - p.olo[a]) / ulo);
+  }
+  lam = fmax(lam, 0.0);
+  // mu < 0: the line beyond the light never reaches the box (no such origin)
+  const double far = mu < 0.0 ? 0.0 : dc + rX + mu;
+  const double ox = fmax(lam, far) + 2.0 * dline;
+  double cv[3];
+  for (int a = 0; a < 3; a++) cv[a] = C[a] - v0[a];
+  return fmin(sbox, (norm3(cv) + rX + ox) * (1.0 + 1e-9) + 1e-9);
+}
+
+RTL_FN void footprint_point_proven(const BP& p, const double V[3][3], const double* v0, const double* e1,
+                                   const double* e2, Foot& f) {
   double n[3];
   cross3d(e1, e2, n);
   const double nl = norm3(n), l1 = norm3(e1), l2 = norm3(e2);
@@ -371,33 +437,42 @@ __device__ void footprint_point_proven(const BP& p, const double V[3][3], const 
     const double X[3] = {V[k][0] - p.lv[0], V[k][1] - p.lv[1], V[k][2] - p.lv[2]};
     vmax = fmax(vmax, norm3(X));
   }
+  double C[3];
+  for (int a = 0; a < 3; a++) C[a] = (V[0][a] + V[1][a] + V[2][a]) / 3.0;
+  double rc = 0.0;
+  for (int k = 0; k < 3; k++) {
+    const double d[3] = {V[k][0] - C[0], V[k][1] - C[1], V[k][2] - C[2]};
+    rc = fmax(rc, norm3(d));
+  }
+  rc *= 1.0 + 1e-12;
   for (int i = 0; i < 3; i++) S[i] = fmax(fabs(p.olo[i] - v0[i]), fabs(p.ohi[i] - v0[i]));
-  const double Smax = sqrt(S[0] * S[0] + S[1] * S[1] + S[2] * S[2]) * (1.0 + 1e-9);
+  const double Sbox = sqrt(S[0] * S[0] + S[1] * S[1] + S[2] * S[2]) * (1.0 + 1e-9);
   const double dline = 2.0 * kSqrt3 * kEps * Dmax;  // fl(l.v - o) from o passes this close to l.v
   const double a_ = sL - dline, b_ = vmax * (1.0 + 1e-12) + dline;
   // rays crossing within r of T: cosine >= c(r) = a_ / (b_ + r); R = a point
   // past the smallest fixed point of g(r) = reach_at(c(r)) (g(R) <= R)
-  double R = 1e301;
-  if (a_ > 0.0) {
+  auto fixed_point = [&](double Sm) {
     double r = 0.0;
+    if (!(a_ > 0.0)) return 1e301;
     for (int it = 0; it < 64; it++) {
-      const double g = reach_at(a_ / (b_ + r), nl, ea, l1, l2, Smax);
-      if (!(g < 1e300)) break;
-      if (g <= r) {
-        R = r;
-        break;
-      }
+      const double g = reach_at(a_ / (b_ + r), nl, ea, l1, l2, Sm);
+      if (!(g < 1e300)) return 1e301;
+      if (g <= r) return r;
       r = g * (1.0 + 1e-9) + 1e-300;
     }
-  }
+    return 1e301;
+  };
+  double Smax = Sbox;
+  double R = fixed_point(Smax);
   bool band = true;
   double clo = 0.0;
   if (R < 1e300) {
     // H_o(c) + Dmax c + dline: how close to the plane the light must be for a
-    // ray at cosine < c to be accepted at all (module comment)
+    // ray at cosine < c to be accepted at all (module comment); any origin
+    // in the box, so the box's |S|
     auto q = [&](double c) {
       return ls / (nl * (1.0 - c)) *
-                 ((nl * c + ea) * (1.0 + 4.0 * kEps) + kCDot * kEps * Smax * lmax + c * Smax * lmax) *
+                 ((nl * c + ea) * (1.0 + 4.0 * kEps) + kCDot * kEps * Sbox * lmax + c * Sbox * lmax) *
                  (1.0 + 1e-6) +
              Dmax * c * (1.0 + 4.0 * kEps) + dline;
     };
@@ -417,40 +492,64 @@ __device__ void footprint_point_proven(const BP& p, const double V[3][3], const 
       const double cst = lo;  // q(cst) <= sL: no accepted ray below cst
       if (cst > 0.0) {
         const double rhi = a_ / cst - b_;
-        const double hc = reach_at(cst, nl, ea, l1, l2, Smax);
+        const double hc = reach_at(cst, nl, ea, l1, l2, Sbox);
         if (hc < rhi) {  // rays at c >= cst cross within R (convexity of g)
           band = false;
+          // every accepting ray crosses within R: its origin's |S| is bounded
+          // by point_smax, and the fixed point again with that bound (each
+          // step valid for every accepting ray)
+          for (int it = 0; it < 2; it++) {
+            Smax = point_smax(p, C, v0, rc + R, dline, Sbox);
+            const double R2 = fixed_point(Smax);
+            if (!(R2 < 1e300)) break;
+            R = fmin(R, R2);
+          }
           clo = a_ / (b_ + R);
         }
       }
     }
   }
-  if (band) {
-    // rays at c >= cst: within reach_at(cst) of T; rays below: origins in the
-    // band of directions within asin(cst + dline / rmin_o) of the plane through
-    // the light parallel to T's
-    const double rmin_o = p.rmin_bits ? (double)__uint_as_float(*p.rmin_bits) : 0.0;
-    const double cst = fmax(1e-3, 8.0 * ea / nl);
-    R = reach_at(cst, nl, ea, l1, l2, Smax);
+  // the band alternative (valid for every triangle): rays at c >= cst
+  // cross within reach_at(cst) of T; rays below leave origins in the band of
+  // directions within asin(cst + dline / rmin_o) of the plane through the
+  // light parallel to T's.  Taken when the bound above fails, or when its
+  // cone would cover more cells than the band and a small cone (a plane
+  // passing close to the light: R grows like 1 / s_L).
+  {
+    const double Dc[3] = {C[0] - p.lv[0], C[1] - p.lv[1], C[2] - p.lv[2]};
+    const double dc = norm3(Dc), hn = 0.5 * (double)p.n;
+    auto cone_cells = [&](double Rr) {
+      if (!(dc > (rc + Rr) * 1.001)) return 1e300;
+      const double th = asin(fmin(1.0, (rc + Rr) / dc)) * hn;
+      return 3.2 * th * th + 4.0 * th + 1.0;
+    };
+    const double rmin_o = p.rmin_o;
+    const double cst = fmax(2.0 / (double)p.n, 8.0 * ea / nl);
+    double Sb = Sbox, Rb = reach_at(cst, nl, ea, l1, l2, Sb);
+    if (Rb < 1e300) {
+      Sb = point_smax(p, C, v0, rc + Rb, dline, Sbox);
+      Rb = fmin(Rb, reach_at(cst, nl, ea, l1, l2, Sb));
+    }
     const double bs = cst * (1.0 + 1e-6) + (rmin_o > 0.0 ? dline / rmin_o : 1e300) + 4.0 * kEps;
-    if (!(cst < 0.25) || !(R < 1e300) || !(bs < 0.3)) {
+    const bool bok = cst < 0.25 && Rb < 1e300 && bs < 0.3;
+    const double band_cells = bok ? 4.0 * (double)p.n * (bs * kSqrt3 * hn * 2.0 + 3.0) + cone_cells(Rb) : 1e300;
+    if (!band && !(cone_cells(R) > band_cells)) {
+      // keep the cone alone
+    } else if (bok) {
+      band = true;
+      R = Rb;
+      Smax = Sb;
+      clo = cst;
+      f.band = true;
+      for (int a = 0; a < 3; a++) f.bn[a] = nh[a];
+      // a face cell holds directions x = (s, t, +-1): |x| <= sqrt 3
+      f.bB = bs * kSqrt3 * (1.0 + 1e-9) + 1e-12;
+    } else if (band) {
       f.global = true;
       return;
     }
-    clo = cst;
-    f.band = true;
-    for (int a = 0; a < 3; a++) f.bn[a] = nh[a];
-    // a face cell holds directions x = (s, t, +-1): |x| <= sqrt 3
-    f.bB = bs * kSqrt3 * (1.0 + 1e-9) + 1e-12;
   }
-  double C[3];
-  for (int a = 0; a < 3; a++) C[a] = (V[0][a] + V[1][a] + V[2][a]) / 3.0;
-  double rb = 0.0;
-  for (int k = 0; k < 3; k++) {
-    const double d[3] = {V[k][0] - C[0], V[k][1] - C[1], V[k][2] - C[2]};
-    rb = fmax(rb, norm3(d));
-  }
-  rb = rb * (1.0 + 1e-12) + R + 1e-12;
+  const double rb = rc + R + 1e-12;
   double rmin = 0.0;
   if (!point_cone(p, V, C, rb, rmin, R, f)) {
     f.n = 0;
@@ -465,7 +564,7 @@ __device__ void footprint_point_proven(const BP& p, const double V[3][3], const 
   f.key = rmin - derr - 2.0 * dline - 1e-9 * p.dmax;
 }
 
-__device__ void footprint(const BP& p, uint32_t prim, Foot& f) {
+RTL_FN void footprint(const BP& p, uint32_t prim, Foot& f) {
   const float* r = (const float*)(p.tri + 3 * (size_t)prim);
   const double v0[3] = {r[0], r[1], r[2]}, e1[3] = {r[3], r[4], r[5]}, e2[3] = {r[6], r[7], r[8]};
   const double V[3][3] = {{v0[0], v0[1], v0[2]},
@@ -480,7 +579,7 @@ __device__ void footprint(const BP& p, uint32_t prim, Foot& f) {
     footprint_point_proven(p, V, v0, e1, e2, f);
 }
 
-__device__ inline uint64_t foot_cells(const BP& p, const Foot& f) {
+RTL_FN inline uint64_t foot_cells(const BP& p, const Foot& f) {
   uint64_t c = 0;
   for (int q = 0; q < f.n; q++)
     c += (uint64_t)(f.x1[q] - f.x0[q] + 1) * (uint64_t)(f.y1[q] - f.y0[q] + 1);
@@ -509,7 +608,7 @@ __device__ inline float cell_key(const BP& p, const Foot& f, int x, int y) {
 // Can the triangle's grown image in rect q reach cell (x, y)?  Separating
 // axis test of the cell square (grown by the margin) against the image's edge
 // lines; conservative (true when unsure: degenerate images, rect-only).
-__device__ inline bool cell_overlaps(const BP& p, const Foot& f, int q, int x, int y) {
+RTL_FN inline bool cell_overlaps(const BP& p, const Foot& f, int q, int x, int y) {
   if (!f.tri_ok[q]) return true;
   double ox, oy, cs;
   if (p.kind == RT_LB_DIR) {
@@ -547,7 +646,7 @@ __device__ inline bool cell_overlaps(const BP& p, const Foot& f, int q, int x, i
   return true;
 }
 
-__device__ inline uint32_t cell_index(const BP& p, const Foot& f, int q, int x, int y) {
+RTL_FN inline uint32_t cell_index(const BP& p, const Foot& f, int q, int x, int y) {
   if (p.kind == RT_LB_DIR) return (uint32_t)y * p.nx + (uint32_t)x;
   return f.face[q] * p.n * p.n + (uint32_t)y * p.n + (uint32_t)x;
 }
@@ -556,7 +655,7 @@ __device__ inline uint32_t cell_index(const BP& p, const Foot& f, int q, int x, 
 // direction x = (s, t, sigma) (face frame: s along axis a+1, t along a+2, as
 // the query maps them) with |x.bn| <= bB; false: none.  Widened by 0.02 cells
 // for the query's rounding.
-__device__ inline bool band_row(const BP& p, const Foot& f, uint32_t face, uint32_t y, int& xa, int& xb) {
+RTL_FN inline bool band_row(const BP& p, const Foot& f, uint32_t face, uint32_t y, int& xa, int& xb) {
   const int a = (int)(face >> 1), j = (a + 1) % 3, k = (a + 2) % 3;
   const double sigma = (face & 1) ? -1.0 : 1.0;
   const double cs = 2.0 / (double)p.n, pad = 0.02 * cs;
@@ -583,7 +682,7 @@ __device__ inline bool band_row(const BP& p, const Foot& f, uint32_t face, uint3
 }
 
 // A footprint as rows: each rect's rows, then (band) the 6 n rows of the cube map.
-__device__ inline uint32_t foot_rows(const BP& p, const Foot& f) {
+RTL_FN inline uint32_t foot_rows(const BP& p, const Foot& f) {
   uint32_t r = 0;
   for (int q = 0; q < f.n; q++) r += (uint32_t)(f.y1[q] - f.y0[q] + 1);
   if (f.band) r += 6u * p.n;
@@ -594,7 +693,7 @@ __device__ inline uint32_t foot_rows(const BP& p, const Foot& f) {
 // `lim` (the prim's own range: a count/emission mismatch is flagged in
 // ctr[4], not written out of bounds)
 template <bool EMIT>
-__device__ inline uint32_t row_entries(const BP& p, const Foot& f, uint32_t prim, uint32_t row, uint64_t at,
+RTL_FN inline uint32_t row_entries(const BP& p, const Foot& f, uint32_t prim, uint32_t row, uint64_t at,
                                        uint64_t lim) {
   for (int q = 0; q < f.n; q++) {
     const uint32_t nr = (uint32_t)(f.y1[q] - f.y0[q] + 1);
@@ -606,7 +705,7 @@ __device__ inline uint32_t row_entries(const BP& p, const Foot& f, uint32_t prim
     uint32_t c = 0;
     for (int x = f.x0[q]; x <= f.x1[q]; x++)
       if (cell_overlaps(p, f, q, x, y)) {
-        if (EMIT) {
+        if constexpr (EMIT) {
           if (at + c >= lim) {
             p.ctr[4] = 1u;
             return c;
@@ -622,7 +721,7 @@ __device__ inline uint32_t row_entries(const BP& p, const Foot& f, uint32_t prim
   const uint32_t face = row / p.n, y = row % p.n;
   int xa = 0, xb = -1;
   if (!band_row(p, f, face, y, xa, xb)) return 0;
-  if (EMIT) {
+  if constexpr (EMIT) {
     const uint32_t kb = orderable(-__builtin_inff());
     for (int x = xa; x <= xb; x++) {
       const uint64_t i = at + (uint64_t)(x - xa);
@@ -637,23 +736,61 @@ __device__ inline uint32_t row_entries(const BP& p, const Foot& f, uint32_t prim
   return (uint32_t)(xb - xa + 1);
 }
 
-__device__ inline bool foot_is_big(const BP& p, const Foot& f) { return f.band || foot_cells(p, f) > kSmallCells; }
+RTL_FN inline bool foot_is_big(const BP& p, const Foot& f) { return f.band || foot_cells(p, f) > kSmallCells; }
+
+// distance from x to the triangle (a, b, c), double: the closest point by the
+// interior / edge cases
+RTL_FN double pt_tri_dist(const double* x, const double* a, const double* b, const double* c) {
+  double ab[3], ac[3], ax[3];
+  for (int i = 0; i < 3; i++) {
+    ab[i] = b[i] - a[i];
+    ac[i] = c[i] - a[i];
+    ax[i] = x[i] - a[i];
+  }
+  double n[3];
+  cross3d(ab, ac, n);
+  const double nn = dot3(n, n);
+  if (nn > 0.0) {
+    double t[3], s[3];
+    cross3d(ab, ax, t);
+    cross3d(ax, ac, s);
+    const double v = dot3(t, n) / nn, u = dot3(s, n) / nn;
+    if (u >= 0.0 && v >= 0.0 && u + v <= 1.0) return fabs(dot3(ax, n)) / sqrt(nn);
+  }
+  double best = 1e300;
+  const double* P[3] = {a, b, c};
+  for (int e = 0; e < 3; e++) {
+    const double* p0 = P[e];
+    const double* p1 = P[(e + 1) % 3];
+    double d[3], w[3];
+    for (int i = 0; i < 3; i++) {
+      d[i] = p1[i] - p0[i];
+      w[i] = x[i] - p0[i];
+    }
+    const double dd = dot3(d, d);
+    double t = dd > 0.0 ? dot3(w, d) / dd : 0.0;
+    t = t < 0.0 ? 0.0 : (t > 1.0 ? 1.0 : t);
+    const double z[3] = {w[0] - t * d[0], w[1] - t * d[1], w[2] - t * d[2]};
+    best = fmin(best, norm3(z));
+  }
+  return best;
+}
+
+// a lower bound of the distance from the light to the shadow-ray origins on
+// this triangle (hit points: on it up to their float rounding, 1e-6 s1)
+RTL_FN double prim_rmin(const BP& p, uint32_t prim) {
+  const float* r = (const float*)(p.tri + 3 * (size_t)prim);
+  const double v0[3] = {r[0], r[1], r[2]};
+  const double v1[3] = {v0[0] + r[3], v0[1] + r[4], v0[2] + r[5]};
+  const double v2[3] = {v0[0] + r[6], v0[1] + r[7], v0[2] + r[8]};
+  const double d = pt_tri_dist(p.lv, v0, v1, v2) * (1.0 - 1e-9) - 1e-6 * p.s1;
+  return d > 0.0 ? d : 0.0;
+}
 
 __global__ __launch_bounds__(256) void rmin_kernel(BP p, uint32_t* bits) {
   const uint32_t prim = blockIdx.x * blockDim.x + threadIdx.x;
   if (prim >= p.nprim) return;
-  const float* r = (const float*)(p.tri + 3 * (size_t)prim);
-  const double v0[3] = {r[0], r[1], r[2]}, e1[3] = {r[3], r[4], r[5]}, e2[3] = {r[6], r[7], r[8]};
-  double C[3], rc = 0.0;
-  for (int a = 0; a < 3; a++) C[a] = v0[a] + (e1[a] + e2[a]) / 3.0;
-  for (int k = 0; k < 3; k++) {
-    double X[3];
-    for (int a = 0; a < 3; a++) X[a] = v0[a] + (k == 1 ? e1[a] : 0.0) + (k == 2 ? e2[a] : 0.0) - C[a];
-    rc = fmax(rc, norm3(X));
-  }
-  const double D[3] = {C[0] - p.lv[0], C[1] - p.lv[1], C[2] - p.lv[2]};
-  // a hit point lies on a triangle up to its float rounding (1e-6 s1 covers it)
-  const double dist = norm3(D) - rc * (1.0 + 1e-12) - 1e-6 * p.s1;
+  const double dist = prim_rmin(p, prim);
   const float fd = dist > 0.0 ? __double2float_rd(dist) : 0.0f;
   atomicMin(bits, __float_as_uint(fd));  // non-negative floats order as their bits
 }
@@ -821,29 +958,14 @@ extern "C" void rt_lightbuf_proof_counts(const LBDevice* d, unsigned long long* 
     }                                                                                 \
   } while (0)
 
-extern "C" int rt_lightbuf_build(const LBParams* in, RtLightBuf* out, LBDevice** devp, hipStream_t s,
-                                 char* err, size_t errlen) {
+// The build's parameters (shared by the device build and the host survey):
+// the DIR grid's float axes and extent, the POINT cube map's side.
+static int bp_setup(const LBParams* in, rtl::BP& p, RtLightBuf* out, uint64_t& ncell, char* err, size_t errlen) {
   using namespace rtl;
-  int rc = 0;
-  BP p;
   std::memset(&p, 0, sizeof p);
   std::memset(out, 0, sizeof *out);
-  LBDevice* dev = new LBDevice();
-  uint32_t* count = nullptr;
-  uint32_t* off = nullptr;
-  uint32_t* ctr = nullptr;
-  uint32_t* big = nullptr;
-  uint32_t* rmin = nullptr;
-  unsigned long long *k0 = nullptr, *k1 = nullptr;
-  uint32_t* v0 = nullptr;
-  void* tmp = nullptr;
-  size_t tb = 0;
-  uint32_t hc[5] = {0, 0, 0, 0, 0}, last_off = 0, last_cnt = 0;
-  uint64_t total = 0, ncell = 0;
-  const uint32_t np = in->nprim;
-  const dim3 gp((np + 255) / 256), bk(256);
   p.tri = in->tri;
-  p.nprim = np;
+  p.nprim = in->nprim;
   p.kind = in->kind;
   p.proven = in->proven ? 1u : 0u;
   for (int a = 0; a < 3; a++) {
@@ -861,7 +983,6 @@ extern "C" int rt_lightbuf_build(const LBParams* in, RtLightBuf* out, LBDevice**
     const double wl = sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
     if (!(wl > 0.0)) {
       snprintf(err, errlen, "directional light with a zero vector");
-      delete dev;
       return -1;
     }
     for (int a = 0; a < 3; a++) {
@@ -937,11 +1058,41 @@ extern "C" int rt_lightbuf_build(const LBParams* in, RtLightBuf* out, LBDevice**
     ncell = 6ull * n * n;
   }
   out->kind = in->kind;
+  out->proven = p.proven;
+  for (int a = 0; a < 3; a++) {  // rounded inward: a float inside is inside the build's box
+    float lo = (float)in->box_lo[a], hi = (float)in->box_hi[a];
+    if ((double)lo < in->box_lo[a]) lo = std::nextafter(lo, 3.0e38f);
+    if ((double)hi > in->box_hi[a]) hi = std::nextafter(hi, -3.0e38f);
+    out->olo[a] = lo;
+    out->ohi[a] = hi;
+  }
   if (ncell >= (1ull << 31)) {
     snprintf(err, errlen, "light buffer of %llu cells", (unsigned long long)ncell);
-    delete dev;
     return -1;
   }
+  return 0;
+}
+
+extern "C" int rt_lightbuf_build(const LBParams* in, RtLightBuf* out, LBDevice** devp, hipStream_t s,
+                                 char* err, size_t errlen) {
+  using namespace rtl;
+  int rc = 0;
+  BP p;
+  uint64_t total = 0, ncell = 0;
+  if (bp_setup(in, p, out, ncell, err, errlen)) return -1;
+  LBDevice* dev = new LBDevice();
+  uint32_t* count = nullptr;
+  uint32_t* off = nullptr;
+  uint32_t* ctr = nullptr;
+  uint32_t* big = nullptr;
+  uint32_t* rmin = nullptr;
+  unsigned long long *k0 = nullptr, *k1 = nullptr;
+  uint32_t* v0 = nullptr;
+  void* tmp = nullptr;
+  size_t tb = 0;
+  uint32_t hc[5] = {0, 0, 0, 0, 0}, last_off = 0, last_cnt = 0;
+  const uint32_t np = in->nprim;
+  const dim3 gp((np + 255) / 256), bk(256);
   LB_TRY(hipMalloc((void**)&count, ((size_t)np + 1) * sizeof(uint32_t)));
   LB_TRY(hipMalloc((void**)&off, ((size_t)np + 1) * sizeof(uint32_t)));
   LB_TRY(hipMalloc((void**)&ctr, 5 * sizeof(uint32_t)));
@@ -961,7 +1112,12 @@ extern "C" int rt_lightbuf_build(const LBParams* in, RtLightBuf* out, LBDevice**
     LB_TRY(hipMemsetAsync(rmin, 0x7f, sizeof(uint32_t), s));  // 0x7f7f7f7f: a large float
     if (np) hipLaunchKernelGGL(rmin_kernel, gp, bk, 0, s, p, rmin);
     LB_TRY(hipGetLastError());
-    p.rmin_bits = rmin;
+    uint32_t rb = 0;
+    LB_TRY(hipMemcpyAsync(&rb, rmin, sizeof rb, hipMemcpyDeviceToHost, s));
+    LB_TRY(hipStreamSynchronize(s));
+    float rf;
+    std::memcpy(&rf, &rb, sizeof rf);
+    p.rmin_o = (double)rf;
   }
   if (np) hipLaunchKernelGGL(count_kernel, gp, bk, 0, s, p);
   LB_TRY(hipGetLastError());
@@ -1064,4 +1220,58 @@ done:
     *devp = dev;
   }
   return rc;
+}
+
+// Host survey of a build (tests, tools; no device): the same footprints,
+// counted on the CPU for every stride-th prim of in->tri (HOST prim-order
+// records).  out: [0] entries, [1] never accepted, [2] global, [3] band
+// prims, [4] big prims, [5] prims surveyed, [6] entries in band rows,
+// [7] largest per-prim count, [8] its prim, [9] entries of prims with > 1024,
+// [10] entries of prims with 65..1024, [11] prims with > 64.
+extern "C" int rt_lightbuf_survey_host(const LBParams* in, uint32_t stride, unsigned long long out[12], char* err,
+                                       size_t errlen) {
+  using namespace rtl;
+  BP p;
+  RtLightBuf lb;
+  uint64_t ncell = 0;
+  if (bp_setup(in, p, &lb, ncell, err, errlen)) return -1;
+  if (p.proven && p.kind == RT_LB_POINT) {
+    double m = 1e300;
+    for (uint32_t i = 0; i < p.nprim; i++) m = fmin(m, prim_rmin(p, i));
+    p.rmin_o = p.nprim ? (double)(float)m : 0.0;
+    if (p.rmin_o > m) p.rmin_o = std::nextafter((float)m, 0.0f);  // rounded down, as the device does
+  }
+  for (int k = 0; k < 12; k++) out[k] = 0;
+  if (!stride) stride = 1;
+  for (uint32_t prim = 0; prim < p.nprim; prim += stride) {
+    Foot f;
+    footprint(p, prim, f);
+    out[5]++;
+    if (f.never) {
+      out[1]++;
+      continue;
+    }
+    if (f.global) {
+      out[2]++;
+      continue;
+    }
+    if (f.band) out[3]++;
+    if (foot_is_big(p, f)) out[4]++;
+    const uint32_t rows = foot_rows(p, f);
+    uint64_t c = 0;
+    for (uint32_t r = 0; r < rows; r++) {
+      const uint32_t e = row_entries<false>(p, f, prim, r, 0, 0);
+      c += e;
+      if (f.band && r >= rows - 6u * p.n) out[6] += e;
+    }
+    out[0] += c;
+    if (c > 1024) out[9] += c;
+    if (c > 64 && c <= 1024) out[10] += c;
+    if (c > 64) out[11]++;
+    if (c > out[7]) {
+      out[7] = c;
+      out[8] = prim;
+    }
+  }
+  return 0;
 }

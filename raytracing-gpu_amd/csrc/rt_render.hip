@@ -1095,9 +1095,22 @@ __device__ __forceinline__ bool shadow_q(const KParams& p, f3 o, f3 d, uint32_t 
   if (staged) {
     hit = staged_any<COUNT>(p, r, act, w, wc);
   } else if (p.lbuf && p.lbuf[li].kind != RT_LB_NONE) {
+    const RtLightBuf& L = p.lbuf[li];
     LaneCount lc = {0, 0, 0, 0, 0, 0, 0};
-    hit = act && lbuf_any<COUNT>(p, p.lbuf[li], r, lc);
+    hit = act && lbuf_any<COUNT>(p, L, r, lc);
     absorb<COUNT>(wc, lc, true);
+    if (L.proven) {
+      // the proof assumed origins in its box; the rare others (hit points of
+      // float garbage hits far past a triangle, e.g. camera rays grazing a
+      // ground plane at the horizon) take brute force over every record,
+      // the wave's lanes over the triangles (cpu/hit.c:93-109)
+      const bool out = act && !(o.x >= L.olo[0] && o.x <= L.ohi[0] && o.y >= L.olo[1] && o.y <= L.ohi[1] &&
+                                o.z >= L.olo[2] && o.z <= L.ohi[2]);
+      if (__ballot(out)) {
+        const bool h2 = flat_any_tp<COUNT>(p, r, out, wc);
+        if (out) hit = h2;
+      }
+    }
   } else {
     LaneCount lc = {0, 0, 0, 0, 0, 0, 0};
     hit = act && oct_any<COUNT>(p, r, s, lc);

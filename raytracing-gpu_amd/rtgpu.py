@@ -157,6 +157,7 @@ _PROTOS = [
     ("rt_hip_set_policy", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_set_exact_shadows", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_set_light_buffers", C.c_int, [C.c_void_p, C.c_int]),
+    ("rt_lightbuf_survey", C.c_int, [C.c_void_p, C.c_uint, C.c_int, C.c_uint, C.c_void_p]),
     ("rt_hip_probe_shadows", C.c_int, [C.c_void_p, C.c_uint, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]),
     ("rt_hip_tile_cycles", C.c_int, [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_size_t]),
     ("rt_hip_tile_phase_cycles", C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_ulonglong),
@@ -277,6 +278,15 @@ class Scene:
 
     def materials_array(self):
         return scene_materials(self.ptr)
+
+    def lightbuf_survey(self, light, exact=False, stride=1):
+        """Host-only count of light `light`'s buffer (rt_lightbuf_survey)."""
+        out = (C.c_ulonglong * 12)()
+        _check(lib().rt_lightbuf_survey(self.ptr, int(light), 1 if exact else 0, int(stride), out),
+               "lightbuf_survey")
+        keys = ("entries", "never", "global", "band", "big", "surveyed", "band_entries", "max_count",
+                "max_prim", "entries_gt1024", "entries_65_1024", "prims_gt64")
+        return dict(zip(keys, (int(x) for x in out)))
 
     def frame(self):
         f = Frame()

@@ -565,3 +565,21 @@ def test_light_buffer_probe_grazing(gpu, li, exact):
     assert 0.01 < ref.mean() < 0.99, ref.mean()
     assert len(bad) == 0, (f"{len(bad)} of {len(o)} grazing shadow rays differ from brute force "
                            f"(buffer lit, brute shadowed: {int((~got & ref).sum())}); first {bad[:5].tolist()}")
+
+
+@pytest.mark.parametrize("exact", [False, True])
+def test_light_buffer_entries_match_host_survey(gpu, exact):
+    """The device build of the light buffers (count -> scan -> emit, small and
+    workgroup footprints, band rows) lists exactly the entries the host survey
+    of the same footprint code counts (rt_lightbuf_survey), light by light."""
+    s = gpu.Scene.synthetic(4, 4, 9776, seed=0x5EED, width=96, height=54)
+    ctx = gpu.Context(s, "octree_gpu")
+    ctx.set_exact_shadows(exact)
+    info = ctx.info()
+    host = [s.lightbuf_survey(li, exact, 1) for li in range(s.s.light_count)
+            if int(s.s.lights[li].type) in (1, 2)]
+    assert info["lightbuf_entries"] == sum(h["entries"] for h in host), (info, host)
+    assert info["lightbuf_global"] == sum(h["global"] for h in host)
+    if exact:
+        assert info["lightbuf_band"] == sum(h["band"] for h in host)
+        assert info["lightbuf_never"] == sum(h["never"] for h in host)

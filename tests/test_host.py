@@ -392,3 +392,19 @@ def test_scene_lifecycle_asan(tmp_path, scene_dir):
                        timeout=600)
     assert r.returncode == 0, r.stderr[-4000:]
     assert "asan scene lifecycle ok" in r.stdout
+
+
+def test_lightbuf_survey_host(built):
+    """Host survey of the light buffers (no device): slack-grown and proven
+    footprints of a small synthetic scene, both lights; the proven ones list
+    every triangle somewhere (none is edge-on enough to be never accepted
+    here) and are deterministic."""
+    import rtgpu
+    s = rtgpu.Scene.synthetic(2, 2, 9776, seed=0x5EED, width=96, height=54)
+    for li in (1, 2):
+        a = s.lightbuf_survey(li, False, 1)
+        b = s.lightbuf_survey(li, True, 1)
+        assert a["surveyed"] == b["surveyed"] == s.triangle_count
+        assert a["entries"] >= a["surveyed"] - a["global"]
+        assert b["entries"] >= b["surveyed"] - b["global"] - b["never"]
+        assert b == s.lightbuf_survey(li, True, 1)
