@@ -86,6 +86,10 @@ typedef struct rt_stats {
   /* point-light shadow rays whose origin lies beyond the extent the exact
    * shadow walk assumes (csrc/rt_shadow.hip; must be 0, RT_EINEXACT) */
   unsigned long long shadow_unproven;
+  /* exact-shadow mode: shadow queries from origins off the proof box (float
+   * garbage hits far past a triangle), decided by brute force after the
+   * shade pass (rt_hip_set_exact_shadows) */
+  unsigned long long shadow_deferred;
 } rt_stats;
 
 /* Sizes of the device-side scene image, for the roofline accounting. */
@@ -276,6 +280,9 @@ int rt_hip_cand_verify(rt_hip_ctx *ctx, const rt_frame *frame, int rank, int nra
  * outcomes differ, queries the walk found lit and brute force shadowed}.
  * The render's image and stats are untouched. */
 int rt_hip_verify_shadows(rt_hip_ctx *ctx, unsigned stride, unsigned long long out[4]);
+/* The same from the first-th record of each region on (first < stride: the
+ * calls for first = 0 .. stride-1 cover every record once). */
+int rt_hip_verify_shadows_from(rt_hip_ctx *ctx, unsigned stride, unsigned first, unsigned long long out[4]);
 
 /* Diagnostic: candidate-list entries of each of the first n rank-local tiles
  * of the last render (n <= that rank's tile count). */

@@ -30,6 +30,7 @@ extern "C" {
 
 #ifndef RT_EPS_ULPS_DEFAULT
 #define RT_EPS_ULPS_DEFAULT 64
+#define RT_OOB_CAP (1u << 20)  // deferred shadow queries per render (exact-shadow mode)
 #endif
 // camera rays (bounce depth 0): a wider slack lets the walk itself find most
 // triangles whose float-MT error region is beyond the secondary rays' slack,
@@ -94,6 +95,8 @@ struct rt_hip_ctx {
   // exact shadow rays (csrc/rt_shadow.hip), built for the slack sh_ulps
   float2* d_prim_mu = nullptr;
   float2* d_node_mu = nullptr;
+  uint4* d_oob = nullptr;       // exact-shadow mode: deferred off-box shadow queries
+  uint32_t* d_oob_count = nullptr;
   uint32_t* d_sh_global = nullptr;
   uint32_t n_sh_global = 0;
   float sh_ulps = -1.0f;
@@ -201,6 +204,8 @@ extern "C" void rt_hip_destroy(rt_hip_ctx* c) {
   (void)hipFree(c->d_last);
   (void)hipFree(c->d_prim_mu);
   (void)hipFree(c->d_node_mu);
+  (void)hipFree(c->d_oob);
+  (void)hipFree(c->d_oob_count);
   (void)hipFree(c->d_sh_global);
   for (LBDevice* d : c->lb_dev) rt_lightbuf_free(d);
   (void)hipFree(c->d_lbuf);
@@ -1196,6 +1201,16 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
     if (rc) return rc;
     if (c->policy == RT_POLICY_DEFAULT || c->policy == RT_POLICY_LANE) p.lbuf = c->d_lbuf;
   }
+  if (p.lbuf && c->exact_shadows) {  // proven buffers: the off-box queries' queue
+    if (!c->d_oob) {
+      HIP_TRY(hipMalloc((void**)&c->d_oob_count, sizeof(uint32_t)));
+      HIP_TRY(hipMalloc((void**)&c->d_oob, (size_t)RT_OOB_CAP * sizeof(uint4)));
+    }
+    p.oob = c->d_oob;
+    p.oob_count = c->d_oob_count;
+    p.oob_cap = RT_OOB_CAP;
+    HIP_TRY(hipMemsetAsync(c->d_oob_count, 0, sizeof(uint32_t), s));
+  }
   if (c->exact_shadows && !p.lbuf) {  // the proven walk
     p.node_mu = c->d_node_mu;
     p.sh_global = c->d_sh_global;
@@ -1228,6 +1243,7 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
   HIP_TRY(rt_launch_trace(&p, dacc, c->count_work, pol, gt, s));
   if (c->timing) HIP_TRY(hipEventRecord(ev[2], s));
   HIP_TRY(rt_launch_shade(&p, dacc, c->count_work, pol, gs, s));
+  HIP_TRY(rt_launch_shade_fixup(&p, c->nprim, s));
   if (c->timing) HIP_TRY(hipEventRecord(ev[3], s));
   HIP_TRY(rt_launch_fold(&p, s));
   c->last_p = p;
@@ -1247,7 +1263,14 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
 // are left as they were.  out = {records compared, shadow queries compared,
 // records whose masks differ, queries the walk called lit and brute force
 // shadowed}.
+extern "C" int rt_hip_verify_shadows_from(rt_hip_ctx* c, unsigned stride, unsigned first,
+                                          unsigned long long out[4]);
 extern "C" int rt_hip_verify_shadows(rt_hip_ctx* c, unsigned stride, unsigned long long out[4]) {
+  return rt_hip_verify_shadows_from(c, stride, 0, out);
+}
+
+extern "C" int rt_hip_verify_shadows_from(rt_hip_ctx* c, unsigned stride, unsigned first,
+                                          unsigned long long out[4]) {
   if (!c || !out) return rt_set_error(RT_EINVAL, "null argument");
   if (!c->d_hit || !c->last_p.hit) return rt_set_error(RT_EINVAL, "no hit records (render a frame first)");
   if (c->nlight > 32) return rt_set_error(RT_EINVAL, "shadow verification covers at most 32 lights");
@@ -1276,6 +1299,7 @@ extern "C" int rt_hip_verify_shadows(rt_hip_ctx* c, unsigned stride, unsigned lo
     p.hit_term = term;
     p.hit_lit = lit[pass];
     p.shade_stride = stride ? stride : 1;
+    p.shade_first = first;
     p.shade_counter = ctr;
     p.stats = st;
     int dacc = c->accel == RT_ACCEL_FLAT || !c->d_node ? RT_ACCEL_FLAT_D : RT_ACCEL_OCTREE_D;
@@ -1287,9 +1311,12 @@ extern "C" int rt_hip_verify_shadows(rt_hip_ctx* c, unsigned stride, unsigned lo
       dacc = RT_ACCEL_FLAT_D;
       if (rt_render_grid(0, RT_ACCEL_FLAT_D, 0, 0, c->cus, &g) != hipSuccess) g = c->grid;
     }
+    if (pass == 1) p.oob = nullptr;
     if (hipMemsetAsync(lit[pass], 0xff, n * sizeof(uint32_t), s) != hipSuccess ||
         hipMemsetAsync(ctr, 0, RT_HIT_REGIONS * 32 * sizeof(uint32_t), s) != hipSuccess ||
+        (p.oob && hipMemsetAsync(p.oob_count, 0, sizeof(uint32_t), s) != hipSuccess) ||
         rt_launch_shade(&p, dacc, 0, dacc == RT_ACCEL_FLAT_D ? 0 : c->policy, g, s) != hipSuccess ||
+        rt_launch_shade_fixup(&p, c->nprim, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
       rc = rt_set_error(RT_EHIP, "shadow verification pass %d: %s", pass,
                         hipGetErrorString(hipGetLastError()));
@@ -1306,7 +1333,7 @@ extern "C" int rt_hip_verify_shadows(rt_hip_ctx* c, unsigned stride, unsigned lo
   std::memset(out, 0, 4 * sizeof *out);
   for (int x = 0; x < RT_HIT_REGIONS; x++) {
     const size_t cnt = hc[32 * x] < c->hit_cap ? hc[32 * x] : c->hit_cap;
-    for (size_t k = 0; k < cnt; k += (stride ? stride : 1)) {
+    for (size_t k = first; k < cnt; k += (stride ? stride : 1)) {
       const size_t a = (size_t)x * c->hit_cap + k;
       out[0]++;
       if (la[a] != lb[a]) {
@@ -1436,6 +1463,14 @@ extern "C" int rt_hip_stats(rt_hip_ctx* c, rt_stats* out) {
                         "%llu shadow rays hit an object whose interpolated normal can vanish "
                         "(cpu/hit.c:99 may skip it; early any-hit exit not proven exact)",
                         out->shadow_zero_risk);
+  if (c->last_p.oob) {
+    uint32_t q = 0;
+    HIP_TRY(hipMemcpy(&q, c->d_oob_count, sizeof q, hipMemcpyDeviceToHost));
+    out->shadow_deferred = q;
+    if (q > RT_OOB_CAP)
+      return rt_set_error(RT_EINEXACT, "%u shadow queries from off the exact mode's proof box, %u decided",
+                          q, RT_OOB_CAP);
+  }
   if (out->shadow_unproven)
     return rt_set_error(RT_EINEXACT,
                         "%llu shadow rays left from beyond the extent the exact shadow mode's "

@@ -101,6 +101,7 @@ struct KParams {
   // 0..31) and shades only every shade_stride-th record of each region
   uint32_t* hit_lit;
   uint32_t shade_stride;
+  uint32_t shade_first;  // ... starting with the shade_first-th
   // exact shadow rays (csrc/rt_shadow.hip): per-node (mu, nu) multipliers of
   // the shadow walk's slack, and the prims every unshadowed shadow ray tests
   // light buffers (csrc/rt_lightbuf.hip), per light; NULL: every shadow query walks
@@ -109,6 +110,13 @@ struct KParams {
   const uint32_t* sh_global;
   uint32_t n_sh_global;
   float sh_omax;  // point-light shadow origins with |o - c|_max beyond this are counted unproven
+  // exact-shadow mode (proven light buffers): shadow queries of lights 0..31
+  // from origins off the proof box are deferred -- shade_kernel appends
+  // (record, pending lights, lit lights, 0) and shades with them lit;
+  // rt_launch_shade_fixup decides them by brute force and re-shades the record
+  uint4* oob;
+  uint32_t* oob_count;
+  uint32_t oob_cap;
   uint32_t* tile_counter;       // 8 item-stream counters, 32 words apart; zeroed before launch
   unsigned long long* stats;    // RT_NSTATS counters, zeroed before launch
   uint2* spill;                 // grid*64 lanes x RT_SPILL_STACK stack entries
@@ -135,6 +143,9 @@ extern "C" hipError_t rt_launch_trace(const KParams* p, int accel, int count_wor
                                       int grid, hipStream_t stream);
 extern "C" hipError_t rt_launch_shade(const KParams* p, int accel, int count_work, int policy,
                                       int grid, hipStream_t stream);
+// exact-shadow mode: the deferred queries of shade_kernel (p->oob), brute
+// force over the nprim prim-order records, then their records re-shaded
+extern "C" hipError_t rt_launch_shade_fixup(const KParams* p, uint32_t nprim, hipStream_t stream);
 extern "C" hipError_t rt_launch_fold(const KParams* p, hipStream_t stream);
 // shadow-query probe: light li's shadow ray from each of n origins through
 // the light buffer p->lbuf[li] (brute = 0) or brute force over nprim

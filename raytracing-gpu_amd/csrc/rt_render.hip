@@ -1083,7 +1083,7 @@ __device__ bool lbuf_any(const KParams& p, const RtLightBuf& L, const Ray& r, La
 // given type; converged call.
 template <int ACCEL, bool COUNT, int POL>
 __device__ __forceinline__ bool shadow_q(const KParams& p, f3 o, f3 d, uint32_t type, uint32_t li,
-                                         bool act, Stack& s, WaveCtx& w, WorkCount& wc) {
+                                         bool act, Stack& s, WaveCtx& w, WorkCount& wc, bool* defer = nullptr) {
   uint64_t am = __ballot(act);
   wc.shadow += (uint32_t)__popcll(am);
   Ray r = make_ray(p, o, d, p.eps_rel);
@@ -1107,8 +1107,13 @@ __device__ __forceinline__ bool shadow_q(const KParams& p, f3 o, f3 d, uint32_t 
       const bool out = act && !(o.x >= L.olo[0] && o.x <= L.ohi[0] && o.y >= L.olo[1] && o.y <= L.ohi[1] &&
                                 o.z >= L.olo[2] && o.z <= L.ohi[2]);
       if (__ballot(out)) {
-        const bool h2 = flat_any_tp<COUNT>(p, r, out, wc);
-        if (out) hit = h2;
+        if (defer && p.oob) {  // decided GPU-wide after the pass (rt_launch_shade_fixup)
+          *defer = out;
+          if (out) hit = false;
+        } else {
+          const bool h2 = flat_any_tp<COUNT>(p, r, out, wc);
+          if (out) hit = h2;
+        }
       }
     }
   } else {
@@ -1509,6 +1514,7 @@ template <int ACCEL, bool COUNT, int POL>
 __device__ __forceinline__ col shade_record(const KParams& p, bool valid, size_t a, Stack& s,
                                             WaveCtx& w, WorkCount& wc, uint32_t& lit0) {
   col acc = init_color(0.0f, 0.0f, 0.0f);
+  uint32_t pend = 0;  // lights 0..31 whose query was deferred (p.oob)
   for (uint32_t l0 = 0; l0 < p.nlight; l0 += 32) {
     const uint32_t l1 = p.nlight - l0 < 32u ? p.nlight : l0 + 32u;
     uint32_t lit = 0;  // bit k: light l0 + k does not shadow the point
@@ -1524,16 +1530,23 @@ __device__ __forceinline__ col shade_record(const KParams& p, bool valid, size_t
         if (type != 1 && type != 2) continue;
         const f3 lv = f3{L[4], L[5], L[6]};
         const uint64_t c0 = COUNT ? __builtin_readcyclecounter() : 0ull;
-        const bool sh = shadow_q<ACCEL, COUNT, POL>(p, P, shadow_dir(type, lv, P), type, li, valid, s, w, wc);
+        bool df = false;
+        const bool sh = shadow_q<ACCEL, COUNT, POL>(p, P, shadow_dir(type, lv, P), type, li, valid, s, w, wc,
+                                                    l0 == 0 ? &df : nullptr);
         if (COUNT) {
           const uint32_t dc = (uint32_t)(__builtin_readcyclecounter() - c0);
           wc.cy_shadow += dc;
           if (type == 1) wc.cy_shadow_dir += dc;
         }
+        if (df) pend |= 1u << li;
         if (!sh) lit |= 1u << (li - l0);
       }
     }
     if (l0 == 0) lit0 = lit;
+    if (valid && pend && l0 == 0) {  // deferred: queued with the lit bits so far
+      const uint32_t q = atomicAdd(p.oob_count, 1u);
+      if (q < p.oob_cap) p.oob[q] = make_uint4((uint32_t)a, pend, lit & ~pend, 0u);
+    }
     if (!valid) continue;
     const float4 r0 = p.hit[2 * a], r1 = p.hit[2 * a + 1];
     const f3 P{r0.x, r0.y, r0.z}, N{r0.w, r1.x, r1.y};
@@ -1582,7 +1595,8 @@ __global__ __launch_bounds__(64, ACCEL == RT_ACCEL_FLAT_D ? RT_FLAT_SHADE_MIN_WA
     const uint32_t hc = p.hit_count[32u * x];
     const uint32_t n = hc < p.hit_cap ? hc : p.hit_cap;
     const uint32_t stride = p.shade_stride > 1u ? p.shade_stride : 1u;  // verification only
-    const uint32_t ns = (n + stride - 1u) / stride;  // records shaded
+    const uint32_t first = p.shade_first;
+    const uint32_t ns = n > first ? (n - first + stride - 1u) / stride : 0u;  // records shaded
     uint32_t q = 0;
     if (lane == 0) q = atomicAdd(p.shade_counter + 32u * x, 1u);
     q = uni(q);
@@ -1592,7 +1606,7 @@ __global__ __launch_bounds__(64, ACCEL == RT_ACCEL_FLAT_D ? RT_FLAT_SHADE_MIN_WA
     }
     const uint32_t k = q * 64u + (uint32_t)lane;
     const bool valid = k < ns;
-    const size_t a = (size_t)x * p.hit_cap + (size_t)k * stride;
+    const size_t a = (size_t)x * p.hit_cap + (size_t)k * stride + first;
     uint32_t lit = 0;
     const col local = shade_record<ACCEL, COUNT, POL>(p, valid, a, stk, w, wc, lit);
     if (valid) {
@@ -1602,6 +1616,78 @@ __global__ __launch_bounds__(64, ACCEL == RT_ACCEL_FLAT_D ? RT_FLAT_SHADE_MIN_WA
     }
   }
   flush_counts(p, wc, lane, true);
+}
+
+// Exact-shadow mode, deferred queries (shade_kernel, p.oob): entry e's
+// pending lights' shadow rays from its record's hit point by brute force over
+// the nprim prim-order records (cpu/hit.c:93-109), a workgroup per
+// (entry, chunk of kFixChunk records); hits ORed into the entry's w.
+static constexpr uint32_t kFixChunk = 16384;
+__global__ __launch_bounds__(256) void oob_fix_kernel(KParams p, uint32_t nprim) {
+  __shared__ uint32_t bits, skip;
+  const uint32_t n = min(*p.oob_count, p.oob_cap);
+  const uint32_t chunks = (nprim + kFixChunk - 1) / kFixChunk;
+  for (uint64_t item = blockIdx.x; item < (uint64_t)n * chunks; item += gridDim.x) {
+    const uint32_t e = (uint32_t)(item / chunks), c = (uint32_t)(item % chunks);
+    const uint4 q = p.oob[e];
+    if (threadIdx.x == 0) {  // one decision for the block: every lane reaches the barriers
+      bits = 0;
+      skip = (__atomic_load_n(&p.oob[e].w, __ATOMIC_RELAXED) & q.y) == q.y;  // all already shadowed
+    }
+    __syncthreads();
+    if (skip) {
+      __syncthreads();
+      continue;
+    }
+    const float4 r0 = p.hit[2 * (size_t)q.x];
+    const f3 P{r0.x, r0.y, r0.z};
+    uint32_t mine = 0, risk = 0;
+    for (uint32_t li = 0; li < 32 && li < p.nlight; li++) {
+      if (!((q.y >> li) & 1u)) continue;
+      const float* L = p.light + RT_LIGHT_FLOATS_D * li;
+      const uint32_t type = __float_as_uint(L[0]);
+      const Ray r = make_ray(p, P, shadow_dir(type, f3{L[4], L[5], L[6]}, P), p.eps_rel);
+      bool h = false;
+      const uint32_t end = min(nprim, (c + 1) * kFixChunk);
+      for (uint32_t k = c * kFixChunk + threadIdx.x; k < end && !h; k += blockDim.x) {
+        const float4* t = p.tri_prim + 3 * (size_t)k;
+        h = any_hit_rec(r, t[0], t[1], t[2], risk);
+      }
+      if (h) mine |= 1u << li;
+    }
+    if (mine) atomicOr(&bits, mine);
+    if (risk) atomicAdd(p.stats + 18, 1ull);  // shadow_zero_risk
+    __syncthreads();
+    if (threadIdx.x == 0 && bits) atomicOr(&p.oob[e].w, bits);
+    __syncthreads();
+  }
+}
+
+// ... then each entry's record shaded again with the decided lights
+// (cpu/light.c:33-100, cpu/raytracer.c:30), as shade_kernel would have.
+__global__ __launch_bounds__(64) void oob_reshade_kernel(KParams p) {
+  const uint32_t n = min(*p.oob_count, p.oob_cap);
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+    const uint4 q = p.oob[e];
+    const size_t a = q.x;
+    const uint32_t lit0 = q.z | (q.y & ~q.w);
+    const float4 r0 = p.hit[2 * a], r1 = p.hit[2 * a + 1];
+    const f3 P{r0.x, r0.y, r0.z}, N{r0.w, r1.x, r1.y};
+    const float* m = p.mat + RT_MAT_FLOATS_D * (size_t)__float_as_uint(r1.w);
+    col acc = init_color(0.0f, 0.0f, 0.0f);
+    for (uint32_t li = 0; li < p.nlight && li < 32; li++) {
+      const float* L = p.light + RT_LIGHT_FLOATS_D * li;
+      const uint32_t type = __float_as_uint(L[0]);
+      const col lc = init_color(L[1], L[2], L[3]);
+      if (type == 0)  // AMBIENT
+        acc = color_add(acc, color_mul2(lc, init_color(m[0], m[1], m[2])));
+      else if ((type == 1 || type == 2) && ((lit0 >> li) & 1u))
+        acc = color_add(acc, light_lit(type, lc, f3{L[4], L[5], L[6]}, m, P, N));
+    }
+    const col tm = color_mul(acc, r1.z);  // coef
+    p.hit_term[a] = make_float4(tm.r, tm.g, tm.b, 0.0f);
+    if (p.hit_lit) p.hit_lit[a] = lit0;
+  }
 }
 
 // Shadow-query probe (tests, tools): the shadow ray of light li from each
@@ -1943,6 +2029,13 @@ extern "C" hipError_t rt_launch_trace(const KParams* p, int accel, int count_wor
 extern "C" hipError_t rt_launch_shade(const KParams* p, int accel, int count_work, int policy,
                                       int grid, hipStream_t stream) {
   return launch_kernel(kernel_of<false>(accel, count_work, policy), grid, p, stream);
+}
+
+extern "C" hipError_t rt_launch_shade_fixup(const KParams* p, uint32_t nprim, hipStream_t stream) {
+  if (!p->oob) return hipGetLastError();
+  hipLaunchKernelGGL(rt::oob_fix_kernel, dim3(4096), dim3(256), 0, stream, *p, nprim);
+  hipLaunchKernelGGL(rt::oob_reshade_kernel, dim3(64), dim3(64), 0, stream, *p);
+  return hipGetLastError();
 }
 
 extern "C" hipError_t rt_launch_probe_shadow(const KParams* p, const float* org, uint32_t n, uint32_t li,

@@ -95,7 +95,7 @@ class Stats(C.Structure):
                 ("cycles_shadow_directional", C.c_ulonglong), ("stack_spills", C.c_ulonglong),
                 ("shadow_zero_risk", C.c_ulonglong), ("hit_records", C.c_ulonglong),
                 ("shadow_node_visits", C.c_ulonglong), ("shadow_tri_tests", C.c_ulonglong),
-                ("shadow_unproven", C.c_ulonglong)]
+                ("shadow_unproven", C.c_ulonglong), ("shadow_deferred", C.c_ulonglong)]
 
     def as_dict(self):
         return {k: int(getattr(self, k)) for k, _ in self._fields_}
@@ -153,6 +153,7 @@ _PROTOS = [
     ("rt_hip_cand_verify", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
     ("rt_hip_cand_tile_entries", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
     ("rt_hip_verify_shadows", C.c_int, [C.c_void_p, C.c_uint, C.POINTER(C.c_ulonglong)]),
+    ("rt_hip_verify_shadows_from", C.c_int, [C.c_void_p, C.c_uint, C.c_uint, C.POINTER(C.c_ulonglong)]),
     ("rt_hip_set_exact_camera", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_set_policy", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_set_exact_shadows", C.c_int, [C.c_void_p, C.c_int]),
@@ -495,11 +496,12 @@ class Context:
         return dict(zip(("listed", "entries", "fp_mismatch", "tile_mismatch", "global",
                          "filter_violation", "filtered"), (int(x) for x in out)))
 
-    def verify_shadows(self, stride=1):
+    def verify_shadows(self, stride=1, first=0):
         """Shadow outcomes of the last render's hit records (every stride-th
-        per region): the walk vs brute force (rt_hip_verify_shadows)."""
+        per region, from the first-th): the walk vs brute force
+        (rt_hip_verify_shadows_from)."""
         out = (C.c_ulonglong * 4)()
-        _check(lib().rt_hip_verify_shadows(self.h, stride, out), "verify_shadows")
+        _check(lib().rt_hip_verify_shadows_from(self.h, stride, first, out), "verify_shadows")
         return dict(zip(("records", "queries", "records_differ", "walk_lit_brute_shadowed"),
                         (int(x) for x in out)))
 

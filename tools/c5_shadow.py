@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--stride", type=int, default=16)
     ap.add_argument("--policy", type=int, default=0)
     ap.add_argument("--tag", default="c5")
+    ap.add_argument("--all", action="store_true", help="every record: --stride calls, one per offset")
     ap.add_argument("--exact", type=int, default=0, help="proven light buffers (rt_hip_set_exact_shadows)")
     ap.add_argument("--probe", type=int, default=0,
                     help="also this many grazing triangles x 50 adversarial origins per light (tools/grazing.py), "
@@ -41,12 +42,20 @@ def main():
     info = ctx.info()
     img, st = ctx.render_image(s.frame())
     t = time.perf_counter()
-    v = ctx.verify_shadows(a.stride)
+    if a.all:
+        v = {}
+        for first in range(a.stride):
+            w = ctx.verify_shadows(a.stride, first)
+            for k, x in w.items():
+                v[k] = v.get(k, 0) + x
+            print(f"offset {first}/{a.stride}: {w}", flush=True)
+    else:
+        v = ctx.verify_shadows(a.stride)
     out = {"scene_triangles": s.triangle_count, "W": a.W, "H": a.H, "stride": a.stride,
            "policy": a.policy, "shadow_queries_in_frame": st["shadow"],
            "hit_records_in_frame": st["hit_records"], "shadow_global_prims": info["shadow_global"],
            "shadow_mu_max": info["shadow_mu_max"], "verify_seconds": time.perf_counter() - t,
-           "exact_shadows": a.exact, "lightbuf": {k: info[k] for k in info if k.startswith("lightbuf")}, **v}
+           "exact_shadows": a.exact, "shadow_deferred": st.get("shadow_deferred", 0), "lightbuf": {k: info[k] for k in info if k.startswith("lightbuf")}, **v}
     if a.probe:
         sys.path.insert(0, os.path.join(REPO, "tools"))
         from grazing import grazing_origins

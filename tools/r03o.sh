@@ -10,3 +10,7 @@ for x in 0 1; do
 done
 timeout -k 10 300 python -u tools/c5_shadow.py --stride 16 --exact 1 --probe 4000 --tag r03o_e1 > gpurun_out/r03o/c5_shadow_e1.log 2>&1 || { tail -5 gpurun_out/r03o/c5_shadow_e1.log; exit 1; }
 cut -c1-2000 gpurun_out/r03o/c5_shadow_e1.log
+for wl in c1 c2 c3 c4; do
+  timeout -k 10 300 python3 bench.py --workload $wl --steps 10 --warmup 2 --cpu-seconds 12 > gpurun_out/r03o/bench_$wl.json 2> gpurun_out/r03o/bench_$wl.err || { tail -5 gpurun_out/r03o/bench_$wl.err; exit 1; }
+  python3 -c "import json; d=json.load(open('gpurun_out/r03o/bench_$wl.json')); print('$wl', d['value'], d['ms_per_step'], d['config'].get('accel'), (d.get('cpu_baseline') or {}).get('value'))"
+done
