@@ -28,8 +28,11 @@ struct RtLightBuf {
   float u0, v0, inv_cs;    // DIR: grid origin and 1 / cell size
   float half_n;            // POINT: nx / 2
   const uint32_t* start;   // per cell: first entry; [ncell] = total
-  const uint32_t* prim;    // per entry: prim index (prim-order records)
-  const float* key;        // per entry, ascending within a cell: a query stops at key > its limit
+  // per entry: the triangle's record (3 float4, as the prim-order records)
+  // with its prim slot (rec[3k+2].y) holding the entry's key; ascending
+  // within a cell, a query stops at key > its limit.  One contiguous 48 B
+  // load per test: no prim -> record indirection on the query's chain.
+  const float4* rec;
   const uint32_t* global;  // prims every query of this light tests (footprint unbounded)
   uint32_t nglobal;
   // proven footprints (LBParams::proven) hold for shadow rays leaving this

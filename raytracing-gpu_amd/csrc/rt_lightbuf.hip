@@ -888,10 +888,18 @@ __global__ __launch_bounds__(256) void big_emit_kernel(BP p) {
   }
 }
 
-// sorted (cell, key) pairs -> per-entry keys
-__global__ __launch_bounds__(256) void key_kernel(const unsigned long long* keys, uint32_t n, float* key) {
+// sorted (cell, key) pairs and prims -> per-entry records with the key in
+// the prim slot
+__global__ __launch_bounds__(256) void rec_kernel(const unsigned long long* keys, const uint32_t* prim,
+                                                  const float4* tri, uint32_t n, float4* rec) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) key[i] = unorder((uint32_t)keys[i]);
+  if (i >= n) return;
+  const float4* t = tri + 3 * (size_t)prim[i];
+  float4 q2 = t[2];
+  q2.y = unorder((uint32_t)keys[i]);
+  rec[3 * (size_t)i] = t[0];
+  rec[3 * (size_t)i + 1] = t[1];
+  rec[3 * (size_t)i + 2] = q2;
 }
 
 // start[c] = the first entry of a cell >= c (binary search; empty cells get
@@ -917,6 +925,7 @@ struct LBDevice {
   uint32_t* start = nullptr;
   uint32_t* prim = nullptr;
   float* key = nullptr;
+  float4* rec = nullptr;
   uint32_t* global = nullptr;
   unsigned long long entries = 0, cells = 0, nglobal = 0, never = 0, band = 0;
 };
@@ -932,6 +941,7 @@ extern "C" void rt_lightbuf_free(LBDevice* d) {
   (void)hipFree(d->start);
   (void)hipFree(d->prim);
   (void)hipFree(d->key);
+  (void)hipFree(d->rec);
   (void)hipFree(d->global);
   delete d;
 }
@@ -1156,7 +1166,7 @@ extern "C" int rt_lightbuf_build(const LBParams* in, RtLightBuf* out, LBDevice**
   dev->never = hc[2];
   dev->band = hc[3];
   LB_TRY(hipMalloc((void**)&dev->prim, (total + 1) * sizeof(uint32_t)));
-  LB_TRY(hipMalloc((void**)&dev->key, (total + 1) * sizeof(float)));
+  LB_TRY(hipMalloc((void**)&dev->rec, (total + 1) * 3 * sizeof(float4)));
   if (total) {
     LB_TRY(hipMalloc((void**)&k0, total * sizeof(unsigned long long)));
     LB_TRY(hipMalloc((void**)&k1, total * sizeof(unsigned long long)));
@@ -1181,8 +1191,8 @@ extern "C" int rt_lightbuf_build(const LBParams* in, RtLightBuf* out, LBDevice**
     }
     sb = tb;
     LB_TRY(rocprim::radix_sort_pairs(tmp, sb, k0, k1, v0, dev->prim, (size_t)total, 0, bits, s));
-    hipLaunchKernelGGL(key_kernel, dim3((uint32_t)((total + 255) / 256)), bk, 0, s, k1, (uint32_t)total,
-                       dev->key);
+    hipLaunchKernelGGL(rec_kernel, dim3((uint32_t)((total + 255) / 256)), bk, 0, s, k1, dev->prim, p.tri,
+                       (uint32_t)total, dev->rec);
     LB_TRY(hipGetLastError());
     hipLaunchKernelGGL(start_kernel, dim3((uint32_t)((ncell + 256) / 256)), bk, 0, s, k1, (uint32_t)total,
                        (uint32_t)ncell, dev->start);
@@ -1198,8 +1208,7 @@ extern "C" int rt_lightbuf_build(const LBParams* in, RtLightBuf* out, LBDevice**
     goto done;
   }
   out->start = dev->start;
-  out->prim = dev->prim;
-  out->key = dev->key;
+  out->rec = dev->rec;
   out->global = dev->global;
   out->nglobal = hc[1];
 done:

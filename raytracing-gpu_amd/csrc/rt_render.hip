@@ -1053,19 +1053,28 @@ __device__ bool lbuf_any(const KParams& p, const RtLightBuf& L, const Ray& r, La
       lim = length(x) * (1.0f + 1e-6f);  // keys: nearest distance from the light
     }
   }
+  // both cells' entry ranges first (independent loads); then each cell's
+  // entries -- the record inline, its key in the prim slot: one contiguous
+  // load per test, no prim -> record indirection.  (Loading the next entry's
+  // record ahead measured slower: its registers spill, shade 1.86 -> 2.72 ms
+  // on C5, profiles/r03t_lbuf_inline/.)
+  uint32_t rs[2] = {0u, 0u}, re[2] = {0u, 0u};
+  for (int h = 0; h < 2; h++)
+    if (cell[h] != 0xffffffffu) {
+      rs[h] = L.start[cell[h]];
+      re[h] = L.start[cell[h] + 1];
+    }
   for (int h = 0; h < 2; h++) {
-    if (cell[h] == 0xffffffffu) continue;
     const float q = h == 0 ? lim : __builtin_inff();
-    const uint32_t e = L.start[cell[h] + 1];
-    for (uint32_t k = L.start[cell[h]]; k < e; k++) {
-      if (L.key[k] > q) break;
-      const uint32_t prim = L.prim[k];
-      const float4* t = p.tri_prim + 3 * (size_t)prim;
+    for (uint32_t k = rs[h]; k < re[h]; k++) {
+      const float4* t = L.rec + 3 * (size_t)k;
+      const float4 a0 = t[0], a1 = t[1], a2 = t[2];
+      if (a2.y > q) break;
       if (COUNT) {
-        lc.tris += lanes_distinct(prim);
+        lc.tris += lanes_distinct(k);
         lc.ltris++;
       }
-      if (any_hit_rec(r, t[0], t[1], t[2], lc.risk)) return true;
+      if (any_hit_rec(r, a0, a1, a2, lc.risk)) return true;
     }
   }
   for (uint32_t k = 0; k < L.nglobal; k++) {
@@ -1102,18 +1111,15 @@ __device__ __forceinline__ bool shadow_q(const KParams& p, f3 o, f3 d, uint32_t 
     if (L.proven) {
       // the proof assumed origins in its box; the rare others (hit points of
       // float garbage hits far past a triangle, e.g. camera rays grazing a
-      // ground plane at the horizon) take brute force over every record,
-      // the wave's lanes over the triangles (cpu/hit.c:93-109)
+      // ground plane at the horizon) are decided by brute force over every
+      // record after the pass (cpu/hit.c:93-109)
       const bool out = act && !(o.x >= L.olo[0] && o.x <= L.ohi[0] && o.y >= L.olo[1] && o.y <= L.ohi[1] &&
                                 o.z >= L.olo[2] && o.z <= L.ohi[2]);
-      if (__ballot(out)) {
-        if (defer && p.oob) {  // decided GPU-wide after the pass (rt_launch_shade_fixup)
-          *defer = out;
-          if (out) hit = false;
-        } else {
-          const bool h2 = flat_any_tp<COUNT>(p, r, out, wc);
-          if (out) hit = h2;
-        }
+      if (defer && p.oob) {  // decided GPU-wide after the pass (rt_launch_shade_fixup)
+        *defer = out;
+        if (out) hit = false;
+      } else {  // (lights past the 32nd) counted, never assumed: RT_EINEXACT
+        wc.sh_unproven += (uint32_t)__popcll(__ballot(out));
       }
     }
   } else {
