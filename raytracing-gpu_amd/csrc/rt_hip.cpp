@@ -324,7 +324,10 @@ static void lb_fill(LBParams& lp, const float scene_c[3], float scene_r, const f
       // the proof's origin box: the triangles' box grown by 1 + 1 % of the
       // scene (hit points off it -- float garbage hits beyond that -- are
       // counted by the shade pass, never assumed)
-      const double g = 1.0 + 0.02 * R;
+#ifndef RT_LB_PROOF_BOX
+#define RT_LB_PROOF_BOX 1.0  // the proof box: the triangles' box grown by g = RT_LB_PROOF_BOX (1 + 0.02 R)
+#endif
+      const double g = RT_LB_PROOF_BOX * (1.0 + 0.02 * R);
       lo[a] = (double)aabb_lo[a] - g;
       hi[a] = (double)aabb_hi[a] + g;
     } else {

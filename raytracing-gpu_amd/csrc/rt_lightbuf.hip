@@ -524,7 +524,10 @@ RTL_FN void footprint_point_proven(const BP& p, const double V[3][3], const doub
       return 3.2 * th * th + 4.0 * th + 1.0;
     };
     const double rmin_o = p.rmin_o;
-    const double cst = fmax(2.0 / (double)p.n, 8.0 * ea / nl);
+#ifndef RT_LB_BAND_C
+#define RT_LB_BAND_C 0.5  // the band's cosine split c* = RT_LB_BAND_C / n (cells of the cube map's side n)
+#endif
+    const double cst = fmax(RT_LB_BAND_C / (double)p.n, 8.0 * ea / nl);
     double Sb = Sbox, Rb = reach_at(cst, nl, ea, l1, l2, Sb);
     if (Rb < 1e300) {
       Sb = point_smax(p, C, v0, rc + Rb, dline, Sbox);
