@@ -1006,8 +1006,14 @@ __device__ __forceinline__ void closest_q(const KParams& p, const Ray& r, bool a
 // up to the first any-hit -- for a point light also the opposite cell, whose
 // triangles lie beyond the light (cpu/rt's shadow ray does not stop there,
 // cpu/hit.c:93-109) -- then the light's global list.  Per lane.
-template <bool COUNT>
-__device__ bool lbuf_any(const KParams& p, const RtLightBuf& L, const Ray& r, LaneCount& lc) {
+// The cells a shadow ray's query scans and their entry ranges (the first
+// memory round trip of a query; shade_record can issue it early).
+struct LbRange {
+  uint32_t rs[2], re[2];
+  float lim;  // key limit of the first range (the second: none)
+};
+
+__device__ __forceinline__ LbRange lbuf_range(const RtLightBuf& L, const Ray& r) {
   uint32_t cell[2] = {0xffffffffu, 0xffffffffu};
   float lim = __builtin_inff();  // key limit of cell[0] (cell[1]: none)
   if (L.kind == RT_LB_DIR) {
@@ -1053,20 +1059,29 @@ __device__ bool lbuf_any(const KParams& p, const RtLightBuf& L, const Ray& r, La
       lim = length(x) * (1.0f + 1e-6f);  // keys: nearest distance from the light
     }
   }
-  // both cells' entry ranges first (independent loads); then each cell's
-  // entries -- the record inline, its key in the prim slot: one contiguous
-  // load per test, no prim -> record indirection.  (Loading the next entry's
-  // record ahead measured slower: its registers spill, shade 1.86 -> 2.72 ms
-  // on C5, profiles/r03t_lbuf_inline/.)
-  uint32_t rs[2] = {0u, 0u}, re[2] = {0u, 0u};
-  for (int h = 0; h < 2; h++)
-    if (cell[h] != 0xffffffffu) {
-      rs[h] = L.start[cell[h]];
-      re[h] = L.start[cell[h] + 1];
-    }
+  // both cells' entry ranges (independent loads)
+  LbRange g;
+  g.lim = lim;
   for (int h = 0; h < 2; h++) {
-    const float q = h == 0 ? lim : __builtin_inff();
-    for (uint32_t k = rs[h]; k < re[h]; k++) {
+    g.rs[h] = 0u;
+    g.re[h] = 0u;
+    if (cell[h] != 0xffffffffu) {
+      g.rs[h] = L.start[cell[h]];
+      g.re[h] = L.start[cell[h] + 1];
+    }
+  }
+  return g;
+}
+
+// Each range's entries -- the record inline, its key in the prim slot: one
+// contiguous load per test, no prim -> record indirection.  (Loading the next
+// entry's record ahead measured slower: its registers spill, shade 1.86 ->
+// 2.72 ms on C5, profiles/r03t_lbuf_inline/.)  Then the global list.
+template <bool COUNT>
+__device__ bool lbuf_scan(const KParams& p, const RtLightBuf& L, const Ray& r, const LbRange& g, LaneCount& lc) {
+  for (int h = 0; h < 2; h++) {
+    const float q = h == 0 ? g.lim : __builtin_inff();
+    for (uint32_t k = g.rs[h]; k < g.re[h]; k++) {
       const float4* t = L.rec + 3 * (size_t)k;
       const float4 a0 = t[0], a1 = t[1], a2 = t[2];
       if (a2.y > q) break;
@@ -1088,11 +1103,17 @@ __device__ bool lbuf_any(const KParams& p, const RtLightBuf& L, const Ray& r, La
   return false;
 }
 
+template <bool COUNT>
+__device__ bool lbuf_any(const KParams& p, const RtLightBuf& L, const Ray& r, LaneCount& lc) {
+  return lbuf_scan<COUNT>(p, L, r, lbuf_range(L, r), lc);
+}
+
 // Shadow query (collide_dist > 0.01, cpu/light.c:24-31) of a light of the
 // given type; converged call.
 template <int ACCEL, bool COUNT, int POL>
 __device__ __forceinline__ bool shadow_q(const KParams& p, f3 o, f3 d, uint32_t type, uint32_t li,
-                                         bool act, Stack& s, WaveCtx& w, WorkCount& wc, bool* defer = nullptr) {
+                                         bool act, Stack& s, WaveCtx& w, WorkCount& wc, bool* defer = nullptr,
+                                         const LbRange* pre = nullptr) {
   uint64_t am = __ballot(act);
   wc.shadow += (uint32_t)__popcll(am);
   Ray r = make_ray(p, o, d, p.eps_rel);
@@ -1106,7 +1127,7 @@ __device__ __forceinline__ bool shadow_q(const KParams& p, f3 o, f3 d, uint32_t 
   } else if (p.lbuf && p.lbuf[li].kind != RT_LB_NONE) {
     const RtLightBuf& L = p.lbuf[li];
     LaneCount lc = {0, 0, 0, 0, 0, 0, 0};
-    hit = act && lbuf_any<COUNT>(p, L, r, lc);
+    hit = act && (pre ? lbuf_scan<COUNT>(p, L, r, *pre, lc) : lbuf_any<COUNT>(p, L, r, lc));
     absorb<COUNT>(wc, lc, true);
     if (L.proven) {
       // the proof assumed origins in its box; the rare others (hit points of
@@ -1537,6 +1558,9 @@ __device__ __forceinline__ col shade_record(const KParams& p, bool valid, size_t
         const f3 lv = f3{L[4], L[5], L[6]};
         const uint64_t c0 = COUNT ? __builtin_readcyclecounter() : 0ull;
         bool df = false;
+        // (issuing the first two lights' cell-range loads before either
+        // query, through shadow_q's `pre`, measured slower: shade 1.92 ->
+        // 2.16 ms on C5, profiles/r04b_shade_pre/)
         const bool sh = shadow_q<ACCEL, COUNT, POL>(p, P, shadow_dir(type, lv, P), type, li, valid, s, w, wc,
                                                     l0 == 0 ? &df : nullptr);
         if (COUNT) {
