@@ -34,12 +34,21 @@
 // occupancy targets of the wavefront split's kernels (waves per SIMD):
 // trace_kernel (closest-hit walks, candidate tests) needs 104 registers left
 // alone, 96 at 5 waves (C5 trace 7.35 -> 6.34 ms, profiles/r03d/); shade_kernel
-// (shadow queries + Phong per hit record) fits 64 at 8 (7.19 -> 6.89 ms)
+// (shadow queries + Phong per hit record) fits 64 at 8 (7.19 -> 6.89 ms).
+// Re-measured with light buffers (profiles/r04c_validate/ab.log, C5): shade
+// 1.92 ms at 8, 1.99 at 7, 2.01 at 6; trace 6.22 ms at 5, 7.12 at 4
 #ifndef RT_TRACE_MIN_WAVES
 #define RT_TRACE_MIN_WAVES 5
 #endif
 #ifndef RT_SHADE_MIN_WAVES
 #define RT_SHADE_MIN_WAVES 8
+#endif
+// camera candidate tests two records per packed-float instruction
+// (rt_render.hip mt_candidate_pk); 0: one record per scalar test.  Measured
+// slower (C5 trace 6.27 -> 6.51 ms, profiles/r04e_pk/ab.log): the phase is
+// not VALU-issue bound, and the pairs cost registers (7 -> 17 spills)
+#ifndef RT_CAND_PK
+#define RT_CAND_PK 0
 #endif
 // the brute-force (FLAT) shade kernel streams records through LDS, two at a
 // time (mt_candidate2): at 8 waves it spilled 96 B per lane

@@ -139,6 +139,39 @@ __device__ __forceinline__ void mt_candidate2(f3 o, f3 d, const float4* qa, cons
   cb = cb && !(tb < kEps * (1.0f - m) || tb > t_cut);
 }
 
+// Two records per instruction: a pair of staged records held component-wise,
+// P[c] = (record A's c-th float, record B's), c = 0 .. 11 in the record's own
+// order (v0, e1, e2, then q2.yzw).  float2 arithmetic lowers to v_pk_mul_f32 /
+// v_pk_add_f32 -- per half the same IEEE operation as the scalar
+// instruction, so every value below has the bits mt_candidate computes.
+typedef float pf2 __attribute__((ext_vector_type(2)));
+
+// mt_candidate of both records of a staged pair (hasb false: A only).  Same
+// operations in the same order (cross, dot as rt_device.h), same decisions,
+// about half the VALU instructions of two scalar calls.
+__device__ __forceinline__ void mt_candidate_pk(f3 o, f3 d, const pf2* P, bool hasb, float t_cut,
+                                                bool& ca, bool& cb) {
+  const float m = 1e-5f;
+  const pf2 v0x = P[0], v0y = P[1], v0z = P[2], e1x = P[3], e1y = P[4], e1z = P[5];
+  const pf2 e2x = P[6], e2y = P[7], e2z = P[8];
+  const pf2 hx = d.y * e2z - d.z * e2y, hy = d.z * e2x - d.x * e2z, hz = d.x * e2y - d.y * e2x;
+  const pf2 a = e1x * hx + e1y * hy + e1z * hz;
+  const pf2 r = {__builtin_amdgcn_rcpf(a.x), __builtin_amdgcn_rcpf(a.y)};
+  const pf2 sx = o.x - v0x, sy = o.y - v0y, sz = o.z - v0z;
+  const pf2 u = (sx * hx + sy * hy + sz * hz) * r;
+  ca = !(a.x > -kEps && a.x < kEps) && !(u.x < -1e-30f || u.x > 1.0f + m);
+  cb = hasb && !(a.y > -kEps && a.y < kEps) && !(u.y < -1e-30f || u.y > 1.0f + m);
+  if (__ballot(ca || cb) == 0) return;
+  const pf2 qx = sy * e1z - sz * e1y, qy = sz * e1x - sx * e1z, qz = sx * e1y - sy * e1x;
+  const pf2 v = (d.x * qx + d.y * qy + d.z * qz) * r;
+  ca = ca && !(v.x < -1e-30f || u.x + v.x > 1.0f + m);
+  cb = cb && !(v.y < -1e-30f || u.y + v.y > 1.0f + m);
+  if (__ballot(ca || cb) == 0) return;
+  const pf2 t = (e2x * qx + e2y * qy + e2z * qz) * r;
+  ca = ca && !(t.x < kEps * (1.0f - m) || t.x > t_cut);
+  cb = cb && !(t.y < kEps * (1.0f - m) || t.y > t_cut);
+}
+
 struct Best {
   float dist;  // +inf = none
   float t_cut; // parametric bound beyond which no triangle can win (+inf = none)
@@ -1293,18 +1326,42 @@ __device__ __forceinline__ void cand_closest(const KParams& p, const Ray& r, boo
       g2 = q[2];
     }
     wave_sync();  // after the previous readers of stage
+#if RT_CAND_PK
+    // pairs of survivors, component-wise (mt_candidate_pk): slot s is half
+    // s & 1 of pair s >> 1, whose 12 float2 take 6 ds_read_b128
+    if (keep) {
+      float* sf = (float*)w.stage + (slot >> 1) * 24 + (slot & 1);
+      const float c[12] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w, g2.x, g2.y, g2.z, g2.w};
+#pragma unroll
+      for (int i = 0; i < 12; i++) sf[2 * i] = c[i];
+    }
+    wave_sync();
+    for (uint32_t k = 0; k < n; k += 2) {
+      const pf2* P = (const pf2*)w.stage + (k >> 1) * 12;
+      bool ca = false, cb = false;
+      if (act) mt_candidate_pk(r.o, r.d, P, k + 1 < n, b.t_cut, ca, cb);
+      if (ca)
+        consider_exact(r, float4{P[0].x, P[1].x, P[2].x, P[3].x}, float4{P[4].x, P[5].x, P[6].x, P[7].x},
+                       float4{P[8].x, P[9].x, P[10].x, P[11].x}, b);
+      if (cb)
+        consider_exact(r, float4{P[0].y, P[1].y, P[2].y, P[3].y}, float4{P[4].y, P[5].y, P[6].y, P[7].y},
+                       float4{P[8].y, P[9].y, P[10].y, P[11].y}, b);
+    }
+#else
     if (keep) {
       w.stage[3 * slot] = g0;
       w.stage[3 * slot + 1] = g1;
       w.stage[3 * slot + 2] = g2;
     }
     wave_sync();
-    // (two candidates per step, as the brute-force loops do, measured
-    // slower here: C5 frame 15.96 -> 16.10 ms, profiles/r03f_bench/ab.log)
+    // (two candidates per step as two scalar chains, as the brute-force loops
+    // do, measured slower here: C5 frame 15.96 -> 16.10 ms,
+    // profiles/r03f_bench/ab.log)
     for (uint32_t k = 0; k < n; k++) {
       float4 q0 = w.stage[3 * k], q1 = w.stage[3 * k + 1], q2 = w.stage[3 * k + 2];
       if (act) consider(r, q0, q1, q2, b);
     }
+#endif
     tested += n;
   }
   for (uint32_t k = 0; k < p.n_cand_global; k++) {
