@@ -288,6 +288,11 @@ int rt_hip_verify_shadows_from(rt_hip_ctx *ctx, unsigned stride, unsigned first,
  * of the last render (n <= that rank's tile count). */
 int rt_hip_cand_tile_entries(rt_hip_ctx *ctx, unsigned int *out, size_t n);
 
+/* Test hook: at most cap work items for the entry-parallel emission of the
+ * big candidate footprints (default 2^20); a frame needing more emits them
+ * one wave per footprint instead (the same lists). */
+int rt_hip_set_cand_item_cap(rt_hip_ctx *ctx, unsigned cap);
+
 /* d_gathered = nranks consecutive tile buffers (rank-major, as an RCCL gather
  * delivers them); writes the PPM-order image (W*H*3 floats) to d_rgb. */
 int rt_hip_assemble(rt_hip_ctx *ctx, const rt_frame *frame, const float *d_gathered, int nranks,

@@ -44,11 +44,16 @@ struct CandParams {
   uint32_t* keys;         // entries: local tile index (pass 2)
   uint32_t* vals;         // entries: prim
   uint32_t* global;       // nprim: prims whose footprint is unbounded
-  uint32_t* ctr;          // [1] global prims, [2] big footprints, [3] list length
+  uint32_t* ctr;          // [1] global prims, [2] big footprints, [3] list length,
+                          // [5] 1 = more than item_cap items (big_kernel emits instead)
   uint32_t* big;          // nprim: list entries with big footprints (rt_cand.hip kSmallRows)
   float* skip;            // nprim: depth-skip bound of each listed prim
   uint32_t* big_lane;     // big_cap x 64: per big footprint, each lane's row-count subtotal
   uint32_t big_cap;       // (big_count_kernel -> big_kernel; beyond it big_kernel recounts)
+  uint2* items;           // item_cap: (big footprint, chunk of its entries), big_item_kernel's waves
+  uint32_t item_cap;
+  uint32_t* wave_items;   // rt_cand_big_waves() + 1: items of each big_count wave ([last] = 0)
+  const uint32_t* wave_base;  // its exclusive scan ([last] = all items)
 };
 
 // Host mirror for surveys (same classify/raster code): safe / footprint /
@@ -79,6 +84,12 @@ extern "C" size_t rt_cand_footprint_bytes(void);
 extern "C" hipError_t rt_cand_big_count(const CandParams* p, hipStream_t s);
 extern "C" hipError_t rt_cand_emit(const CandParams* p, hipStream_t s);
 extern "C" hipError_t rt_cand_big(const CandParams* p, uint32_t nbig, hipStream_t s);
+// big emission work items: wave_items (big_count_kernel) -> scan -> wave_base
+// -> rt_cand_items writes them; pass 2b, entry-parallel: one wave per
+// (big footprint, chunk of its entries) item (used when ctr[5] == 0)
+extern "C" uint32_t rt_cand_big_waves(void);
+extern "C" hipError_t rt_cand_items(const CandParams* p, hipStream_t s);
+extern "C" hipError_t rt_cand_big_items(const CandParams* p, uint32_t nitems, hipStream_t s);
 extern "C" hipError_t rt_cand_scan(const uint32_t* in, uint32_t* out, uint32_t n, void* temp,
                                    size_t* temp_bytes, hipStream_t s);
 extern "C" hipError_t rt_cand_sort(uint32_t* keys_in, uint32_t* keys_out, uint32_t* vals_in,

@@ -585,6 +585,38 @@ __host__ __device__ inline uint32_t count_row(const CandParams& p, const Footpri
   return c;
 }
 
+// raster_row's tiles of row ty as three disjoint column intervals, in
+// emission order: x[0..1] = [a0, a1], then the parts of [b0, b1] left and
+// right of it (x[2..3], x[4..5]; empty: x0 > x1); c[i] = this rank's tiles in
+// interval i, f[i] = its first block column (rt_rank_row_tiles).  c[0] + c[1]
+// + c[2] == count_row (the rank's tiles of a column set add up over disjoint
+// parts).
+__host__ __device__ inline void row_ivs(const CandParams& p, const Footprint& fp, int ty, int r0, int r1,
+                                        int* x, int* f, uint32_t* c) {
+  int a0, a1, b0, b1;
+  row_tiles(p, fp, ty, r0, r1, a0, a1, b0, b1);
+  x[0] = a0;
+  x[1] = a1;
+  if (a0 > a1) {
+    x[2] = b0;
+    x[3] = b1;
+    x[4] = 1;
+    x[5] = 0;
+  } else {
+    x[2] = b0;
+    x[3] = b1 < a0 - 1 ? b1 : a0 - 1;
+    x[4] = b0 > a1 + 1 ? b0 : a1 + 1;
+    x[5] = b1;
+  }
+  for (int i = 0; i < 3; i++) {
+    f[i] = 0;
+    c[i] = x[2 * i] > x[2 * i + 1]
+               ? 0u
+               : rt_rank_row_tiles(ty, x[2 * i], x[2 * i + 1], (uint32_t)p.nranks, (uint32_t)p.rank,
+                                   (uint32_t)p.blocks_x, (uint32_t)p.tb, &f[i]);
+  }
+}
+
 // Tiles of this rank whose camera samples can be candidates for the
 // triangle.  Pixel (r, c) samples k in [W/2 - c, W/2 - c + 1/2], l in
 // [H/2 - r, H/2 - r + 1/2] (cpu/raytracer.c:55-58 with i = W/2 - c, j = H/2 -
@@ -615,6 +647,11 @@ constexpr uint32_t kSmallEntries = 32;
 // persistent waves of the big-footprint passes (they loop over the big list,
 // whose length only the device knows before the scan)
 constexpr int kBigWaves = 4096;
+// entries per big_item_kernel wave.  One wave per footprint (big_kernel) left
+// the chip idle behind a few long ones: C5's largest footprint has 53,789
+// entries in rows of ~200 tiles, each lane writing its row alone, and the
+// kernel ran at 0.42 resident waves per SIMD (profiles/r03w_c5/pmc_sq.json).
+constexpr uint32_t kChunk = 1024;
 
 // Pass 0: the float fast path over every prim; flags the prims it cannot
 // prove safe (visits[prim] = 1), which an exclusive scan and scatter_kernel
@@ -693,6 +730,7 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, int lane) {
 __global__ __launch_bounds__(64) void big_count_kernel(CandParams p) {
   const int lane = threadIdx.x;
   const uint32_t nbig = p.ctr[2];
+  uint32_t witems = 0;
   for (uint32_t b = blockIdx.x; b < nbig; b += gridDim.x) {
     const uint32_t j = p.big[b];
     const Footprint fp = p.fp[j];
@@ -703,6 +741,29 @@ __global__ __launch_bounds__(64) void big_count_kernel(CandParams p) {
     if (b < p.big_cap) p.big_lane[(size_t)b * 64 + lane] = cnt;  // big_kernel's offsets
     cnt = wave_sum(cnt);
     if (lane == 0) p.visits[j] = cnt;
+    witems += (cnt + kChunk - 1) / kChunk;
+  }
+  // this wave's big_item_kernel items (one per kChunk entries of each of its
+  // footprints), placed by a scan over the waves: one atomic per footprint
+  // on a shared counter serialised at L2 (big_count 0.16 -> 1.5 ms on C5)
+  if (lane == 0) p.wave_items[blockIdx.x] = witems;
+}
+
+// After the scan of wave_items: each big_count wave's footprints, in the same
+// order, write their items from the wave's offset; past item_cap, ctr[5] = 1
+// and the host emits with big_kernel instead.
+__global__ __launch_bounds__(64) void item_kernel(CandParams p) {
+  const int lane = threadIdx.x;
+  const uint32_t nbig = p.ctr[2];
+  uint32_t at = p.wave_base[blockIdx.x];
+  for (uint32_t b = blockIdx.x; b < nbig; b += gridDim.x) {
+    const uint32_t ni = (p.visits[p.big[b]] + kChunk - 1) / kChunk;
+    if (at + ni <= p.item_cap) {
+      for (uint32_t c = (uint32_t)lane; c < ni; c += 64) p.items[at + c] = make_uint2(b, c);
+    } else if (lane == 0) {
+      p.ctr[5] = 1u;
+    }
+    at += ni;
   }
 }
 
@@ -781,6 +842,91 @@ __global__ __launch_bounds__(64) void big_kernel(CandParams p) {
     uint32_t o = p.off[j] + wave_excl_scan(cnt, lane);
     if (rows)
       for (int ty = ty0 + lane; ty <= ty1; ty += 64) o += emit_row(p, fp, ty, r0, r1, o, prim);
+  }
+}
+
+// Column of the k-th of this rank's tiles in [x0, x1] of tile row ty (f =
+// the first of the rank's block columns there, rt_rank_row_tiles): the first
+// block may be cut on the left, the ones after it hold tb tiles each, n
+// blocks apart.  tb is 1 or RT_TB (a power of two).
+__device__ __forceinline__ int kth_rank_col(const CandParams& p, int x0, int x1, int f, uint32_t k) {
+  const int tb = p.tb;
+  const int s0 = x0 > f * tb ? x0 : f * tb;
+  const int e0 = x1 < f * tb + tb - 1 ? x1 : f * tb + tb - 1;
+  const uint32_t c0 = (uint32_t)(e0 - s0 + 1);
+  if (k < c0) return s0 + (int)k;
+  const uint32_t kk = k - c0, sh = (uint32_t)(__ffs(tb) - 1);
+  const int m = 1 + (int)(kk >> sh);
+  return (f + m * p.nranks) * tb + (int)(kk & (uint32_t)(tb - 1));
+}
+
+// Pass 2b, entry-parallel (big_count_kernel's items): the wave writes entries
+// [c kChunk, (c + 1) kChunk) of big footprint b, lane-consecutive (coalesced
+// stores).  Row by row in row-major order, each row's intervals in
+// raster_row's order; the rows are taken 64 at a time -- the lanes compute
+// their intervals and counts (row_ivs), a wave scan places them, and each
+// entry of the chunk finds its row by binary search over the 64 prefixes in
+// LDS.  Same (tile, prim) set as big_kernel; the sort orders it.
+__global__ __launch_bounds__(64) void big_item_kernel(CandParams p) {
+  __shared__ uint32_t pre[65];
+  __shared__ int rx[64][6], rf[64][3];
+  __shared__ uint32_t rc[64][2];
+  __shared__ int rty[64];
+  const int lane = threadIdx.x;
+  const uint2 it = p.items[blockIdx.x];
+  const uint32_t j = p.big[it.x], prim = p.list[j];
+  const uint32_t base = p.off[j], total = p.off[j + 1] - base;
+  const uint32_t c0 = it.y * kChunk, c1 = c0 + kChunk < total ? c0 + kChunk : total;
+  const Footprint fp = p.fp[j];
+  int r0, r1;
+  if (!raster_rows(p, fp, r0, r1)) return;  // no entries, no items
+  uint32_t g0 = 0;  // entries of the footprint before this group of rows
+  for (int gy = r0 >> 3; gy <= (r1 >> 3) && g0 < c1; gy += 64) {
+    const int ty = gy + lane;
+    int x[6] = {1, 0, 1, 0, 1, 0}, f[3] = {0, 0, 0};
+    uint32_t c[3] = {0u, 0u, 0u};
+    if (ty <= (r1 >> 3)) row_ivs(p, fp, ty, r0, r1, x, f, c);
+    const uint32_t n = c[0] + c[1] + c[2];
+    const uint32_t ex = wave_excl_scan(n, lane);
+    const uint32_t gt = __shfl(ex + n, 63, 64);
+    if (g0 + gt > c0) {
+      __syncthreads();  // after the previous group's readers
+      pre[lane] = g0 + ex;
+      if (lane == 63) pre[64] = g0 + gt;
+#pragma unroll
+      for (int i = 0; i < 6; i++) rx[lane][i] = x[i];
+#pragma unroll
+      for (int i = 0; i < 3; i++) rf[lane][i] = f[i];
+      rc[lane][0] = c[0];
+      rc[lane][1] = c[1];
+      rty[lane] = ty;
+      __syncthreads();
+      const uint32_t e0 = c0 > g0 ? c0 : g0, e1 = c1 < g0 + gt ? c1 : g0 + gt;
+      for (uint32_t e = e0 + (uint32_t)lane; e < e1; e += 64) {
+        // the last row whose prefix is <= e (it holds e: e < pre[64], and a
+        // row without entries shares its prefix with the next one)
+        int r = 0;
+#pragma unroll
+        for (int s = 32; s > 0; s >>= 1)
+          if (pre[r + s] <= e) r += s;
+        uint32_t k = e - pre[r];
+        int iv = 0;
+        if (k >= rc[r][0]) {
+          k -= rc[r][0];
+          iv = 1;
+          if (k >= rc[r][1]) {
+            k -= rc[r][1];
+            iv = 2;
+          }
+        }
+        const int tx = kth_rank_col(p, rx[r][2 * iv], rx[r][2 * iv + 1], rf[r][iv], k);
+        uint32_t rk;
+        p.keys[base + e] = rt_tile_local(tx, rty[r], (uint32_t)p.nranks, (uint32_t)p.blocks_x,
+                                         (uint32_t)p.tb, &rk);
+        p.vals[base + e] = prim;
+      }
+    }
+    g0 += gt;
   }
 }
 
@@ -881,7 +1027,17 @@ extern "C" int rt_cand_survey_host(const CandParams* p, const float* tri, const 
         if (c == rtc::FOOTPRINT) {
           unsigned long long v = 0;
           rtc::raster(*p, fp, [&](uint32_t) { v++; });
-          if (v != rtc::raster_count(*p, fp)) {
+          // big_count_kernel counts rows through row_ivs (big_item_kernel's intervals)
+          unsigned long long vi = 0;
+          int q0, q1;
+          if (rtc::raster_rows(*p, fp, q0, q1))
+            for (int ty = q0 >> 3; ty <= (q1 >> 3); ty++) {
+              int x[6], fb[3];
+              uint32_t cn[3];
+              rtc::row_ivs(*p, fp, ty, q0, q1, x, fb, cn);
+              vi += cn[0] + cn[1] + cn[2];
+            }
+          if (v != rtc::raster_count(*p, fp) || vi != v) {
             bad[t]++;  // the device count pass must agree
 #ifdef RT_SURVEY_DEBUG
             int r0, r1;
@@ -1047,6 +1203,19 @@ extern "C" hipError_t rt_cand_big(const CandParams* p, uint32_t nbig, hipStream_
   if (nbig == 0) return hipSuccess;
   const uint32_t g = nbig < (uint32_t)rtc::kBigWaves ? nbig : (uint32_t)rtc::kBigWaves;
   hipLaunchKernelGGL(rtc::big_kernel, dim3(g), dim3(64), 0, s, *p);
+  return hipGetLastError();
+}
+
+extern "C" uint32_t rt_cand_big_waves(void) { return (uint32_t)rtc::kBigWaves; }
+
+extern "C" hipError_t rt_cand_items(const CandParams* p, hipStream_t s) {
+  hipLaunchKernelGGL(rtc::item_kernel, dim3(rtc::kBigWaves), dim3(64), 0, s, *p);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t rt_cand_big_items(const CandParams* p, uint32_t nitems, hipStream_t s) {
+  if (nitems == 0) return hipSuccess;
+  hipLaunchKernelGGL(rtc::big_item_kernel, dim3(nitems), dim3(64), 0, s, *p);
   return hipGetLastError();
 }
 

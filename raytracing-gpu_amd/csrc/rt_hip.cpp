@@ -122,6 +122,10 @@ struct rt_hip_ctx {
   uint32_t* d_cand_ctr = nullptr;     // 4
   float* d_cand_skip = nullptr;       // nprim
   uint32_t* d_cand_big_lane = nullptr;  // kBigLaneCap x 64 lane subtotals of big footprints
+  uint2* d_cand_items = nullptr;        // kItemCap big-emission work items
+  uint32_t* d_cand_wave_items = nullptr;  // rt_cand_big_waves() + 1 each: items per big_count wave,
+  uint32_t* d_cand_wave_base = nullptr;   // and their exclusive scan
+  uint32_t cand_item_cap = 0xffffffffu;  // test hook: fewer items (min with kItemCap)
   uint32_t* d_prim_leaf = nullptr;    // nprim: a leaf holding each prim (camera-independent)
   uint32_t* d_cand = nullptr;
   uint32_t* d_order = nullptr;        // 3 x (ntiles + 1): heavy flags, their scan, the work order
@@ -222,6 +226,9 @@ extern "C" void rt_hip_destroy(rt_hip_ctx* c) {
   (void)hipFree(c->d_cand_big);
   (void)hipFree(c->d_cand_ctr);
   (void)hipFree(c->d_cand_big_lane);
+  (void)hipFree(c->d_cand_items);
+  (void)hipFree(c->d_cand_wave_items);
+  (void)hipFree(c->d_cand_wave_base);
   (void)hipFree(c->d_cand_skip);
   (void)hipFree(c->d_prim_leaf);
   (void)hipFree(c->d_cand);
@@ -858,6 +865,18 @@ static double d3dot(const double* a, const double* b) { return a[0] * b[0] + a[1
 // big footprints whose per-lane row counts big_count_kernel keeps for
 // big_kernel (C5: ~5e4 per frame; beyond this big_kernel recounts)
 static constexpr uint32_t kBigLaneCap = 1u << 17;
+// (big footprint, chunk) work items of the entry-parallel big emission (C5:
+// ~5e4 per frame; beyond this the frame's big footprints go to big_kernel)
+#ifndef RT_CAND_ITEM_CAP
+#define RT_CAND_ITEM_CAP (1u << 20)
+#endif
+static constexpr uint32_t kItemCap = RT_CAND_ITEM_CAP;
+
+extern "C" int rt_hip_set_cand_item_cap(rt_hip_ctx* c, unsigned cap) {
+  if (!c) return rt_set_error(RT_EINVAL, "null context");
+  c->cand_item_cap = cap;
+  return RT_OK;
+}
 
 // Frame constants of the candidate lists for rank/nranks (no device work).
 static int cand_params(const rt_frame* f, const float scene_c[3], float scene_r, float eps_ulps,
@@ -981,7 +1000,8 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
     // freed here, never allocated over
     for (void** b : {(void**)&c->d_cand_list, &c->d_cand_fp, (void**)&c->d_cand_visits, (void**)&c->d_cand_off,
                      (void**)&c->d_cand_global, (void**)&c->d_cand_big, (void**)&c->d_cand_ctr,
-                     (void**)&c->d_cand_skip, (void**)&c->d_cand_big_lane}) {
+                     (void**)&c->d_cand_skip, (void**)&c->d_cand_big_lane, (void**)&c->d_cand_items,
+                     (void**)&c->d_cand_wave_items, (void**)&c->d_cand_wave_base}) {
       (void)hipFree(*b);
       *b = nullptr;
     }
@@ -991,10 +1011,15 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
     HIP_TRY(hipMalloc((void**)&c->d_cand_off, (np + 1) * sizeof(uint32_t)));
     HIP_TRY(hipMalloc((void**)&c->d_cand_global, (np + 1) * sizeof(uint32_t)));
     HIP_TRY(hipMalloc((void**)&c->d_cand_big, (np + 1) * sizeof(uint32_t)));
-    HIP_TRY(hipMalloc((void**)&c->d_cand_ctr, 4 * sizeof(uint32_t)));
+    HIP_TRY(hipMalloc((void**)&c->d_cand_ctr, 8 * sizeof(uint32_t)));
     HIP_TRY(hipMalloc((void**)&c->d_cand_skip, (np + 1) * sizeof(float)));
     HIP_TRY(hipMalloc((void**)&c->d_cand_big_lane, (size_t)kBigLaneCap * 64 * sizeof(uint32_t)));
-    HIP_TRY(hipHostMalloc((void**)&c->h_cand, 4 * sizeof(uint32_t), hipHostMallocDefault));
+    HIP_TRY(hipMalloc((void**)&c->d_cand_items, ((size_t)kItemCap + 1) * sizeof(uint2)));
+    const size_t nw = (size_t)rt_cand_big_waves() + 1;
+    HIP_TRY(hipMalloc((void**)&c->d_cand_wave_items, nw * sizeof(uint32_t)));
+    HIP_TRY(hipMemset(c->d_cand_wave_items, 0, nw * sizeof(uint32_t)));  // [last] stays 0
+    HIP_TRY(hipMalloc((void**)&c->d_cand_wave_base, nw * sizeof(uint32_t)));
+    HIP_TRY(hipHostMalloc((void**)&c->h_cand, 8 * sizeof(uint32_t), hipHostMallocDefault));
   }
   if (nt + 1 > c->cand_tiles_cap) {
     size_t cap = c->cand_tiles_cap;
@@ -1012,10 +1037,18 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
   cp.skip = c->d_cand_skip;
   cp.big_lane = c->d_cand_big_lane;
   cp.big_cap = kBigLaneCap;
+  cp.items = c->d_cand_items;
+  cp.item_cap = c->cand_item_cap < kItemCap ? c->cand_item_cap : kItemCap;
+  cp.wave_items = c->d_cand_wave_items;
+  cp.wave_base = c->d_cand_wave_base;
   HIP_TRY(hipMemsetAsync(c->d_cand_visits + np, 0, sizeof(uint32_t), s));
-  HIP_TRY(hipMemsetAsync(c->d_cand_ctr, 0, 4 * sizeof(uint32_t), s));
+  HIP_TRY(hipMemsetAsync(c->d_cand_ctr, 0, 8 * sizeof(uint32_t), s));
   size_t tb = 0;
   HIP_TRY(rt_cand_scan(c->d_cand_visits, c->d_cand_off, (uint32_t)np, nullptr, &tb, s));
+  rc = ensure_tmp(c, tb);
+  if (rc) return rc;
+  tb = 0;
+  HIP_TRY(rt_cand_scan(c->d_cand_wave_items, c->d_cand_wave_base, rt_cand_big_waves(), nullptr, &tb, s));
   rc = ensure_tmp(c, tb);
   if (rc) return rc;
   // pass 0: flags -> compact list of the prims the float fast path leaves
@@ -1027,12 +1060,19 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
   // pass 1: footprints and tile counts of the listed prims
   HIP_TRY(rt_cand_count(&cp, s));
   HIP_TRY(rt_cand_big_count(&cp, s));
+  // the big footprints' emission items (a scan over the big_count waves)
+  tb = c->scan_tmp_bytes;
+  HIP_TRY(rt_cand_scan(c->d_cand_wave_items, c->d_cand_wave_base, rt_cand_big_waves(), c->d_scan_tmp, &tb, s));
+  HIP_TRY(rt_cand_items(&cp, s));
   tb = c->scan_tmp_bytes;
   HIP_TRY(rt_cand_scan(c->d_cand_visits, c->d_cand_off, (uint32_t)np, c->d_scan_tmp, &tb, s));
   HIP_TRY(hipMemcpyAsync(c->h_cand, c->d_cand_off + np, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(c->h_cand + 1, c->d_cand_ctr + 1, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(c->h_cand + 1, c->d_cand_ctr + 1, 5 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(c->h_cand + 4, c->d_cand_wave_base + rt_cand_big_waves(), sizeof(uint32_t),
+                         hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   const uint32_t total = c->h_cand[0], nglobal = c->h_cand[1], nbig = c->h_cand[2];
+  const uint32_t nitems = c->h_cand[4], items_over = c->h_cand[5];
   if (total + 1 > c->cand_cap) {
     for (uint32_t** b : {&c->d_cand_keys, &c->d_cand_vals, &c->d_cand_keys2, &c->d_cand}) {
       (void)hipFree(*b);
@@ -1050,7 +1090,10 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
   cp.keys = c->d_cand_keys;
   cp.vals = c->d_cand_vals;
   HIP_TRY(rt_cand_emit(&cp, s));
-  HIP_TRY(rt_cand_big(&cp, nbig, s));
+  if (items_over)
+    HIP_TRY(rt_cand_big(&cp, nbig, s));
+  else
+    HIP_TRY(rt_cand_big_items(&cp, nitems, s));
   int bits = 1;
   while ((1ull << bits) <= nt) bits++;
   tb = 0;

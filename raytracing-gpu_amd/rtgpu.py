@@ -152,6 +152,7 @@ _PROTOS = [
     ("rt_hip_set_camera_slack", C.c_int, [C.c_void_p, C.c_float]),
     ("rt_hip_cand_verify", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
     ("rt_hip_cand_tile_entries", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
+    ("rt_hip_set_cand_item_cap", C.c_int, [C.c_void_p, C.c_uint]),
     ("rt_hip_verify_shadows", C.c_int, [C.c_void_p, C.c_uint, C.POINTER(C.c_ulonglong)]),
     ("rt_hip_verify_shadows_from", C.c_int, [C.c_void_p, C.c_uint, C.c_uint, C.POINTER(C.c_ulonglong)]),
     ("rt_hip_set_exact_camera", C.c_int, [C.c_void_p, C.c_int]),
@@ -511,6 +512,11 @@ class Context:
         _check(lib().rt_hip_cand_tile_entries(self.h, out.ctypes.data_as(C.c_void_p), ntiles),
                "cand_tile_entries")
         return out
+
+    def set_cand_item_cap(self, cap):
+        """Test hook: cap the big footprints' emission work items (0: one
+        wave per footprint, the fallback path)."""
+        _check(lib().rt_hip_set_cand_item_cap(self.h, int(cap)), "cand_item_cap")
 
     def set_camera_slack(self, ulps):
         _check(lib().rt_hip_set_camera_slack(self.h, float(ulps)), "camera_slack")

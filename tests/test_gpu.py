@@ -444,20 +444,26 @@ def test_exact_camera_rank_split(gpu):
         assert_bitexact(t, ref[: len(t)], f"rank {rank}/3")
 
 
-@pytest.mark.parametrize("accel,nranks,ranks", [("octree_gpu", 1, (0,)), ("octree", 1, (0,)),
-                                               ("octree_gpu", 3, (0, 1, 2)),
-                                               ("octree_gpu", 7, (0, 6))])
-def test_candidate_lists_match_host(gpu, accel, nranks, ranks):
+@pytest.mark.parametrize("accel,nranks,ranks,item_cap", [("octree_gpu", 1, (0,), None), ("octree", 1, (0,), None),
+                                                        ("octree_gpu", 3, (0, 1, 2), None),
+                                                        ("octree_gpu", 7, (0, 6), None),
+                                                        ("octree_gpu", 1, (0,), 0),
+                                                        ("octree_gpu", 3, (0, 2), 5)])
+def test_candidate_lists_match_host(gpu, accel, nranks, ranks, item_cap):
     """The device-built camera candidate lists (csrc/rt_cand.hip: float fast
     path, f64 classification, small/big footprint split, emission, radix
     sort, per-tile offsets) equal the host re-derivation from the same
     classify/raster code: every listed prim's footprint bit for bit, every
     tile's list as a multiset -- including the big footprints (hundreds of
-    tiles) emitted one wave each; 7 ranks exercise the rank filter's per-row
-    path (240 tile columns are not a multiple of 7)."""
+    tiles), emitted entry-parallel in chunks (big_item_kernel) or, when the
+    work items overflow their cap (item_cap 0, or 5: overflow part-way), one
+    wave per footprint (big_kernel); 7 ranks exercise the rank filter's
+    per-row path (240 tile columns are not a multiple of 7)."""
     s = gpu.Scene.synthetic(8, 6, 9776, seed=0x5EED, width=1920, height=1080)
     f = s.frame()
     ctx = gpu.Context(s, accel)
+    if item_cap is not None:
+        ctx.set_cand_item_cap(item_cap)
     for rank in ranks:
         _tiles_of_rank(ctx, f, rank, nranks)
         v = ctx.cand_verify(f, rank, nranks)
