@@ -393,12 +393,17 @@ RTC_FN int quick_class(const CandParams& p, const float* r) {
   float e_dq = (float)p.c_dot * fe * smax * l1 * 1.0001f;
   float e_eq = (float)p.c_dot * fe * smax * l1 * l2 * 1.0001f;
   const float dmin = 1.0f - 4.0f * fe;
-  // H(c) <= (du + dv + dw) (l1 + l2) with a = a_lb(c)
+  // H(c) <= (du + dv + dw) (l1 + l2) with a = a_lb(c).  The quotients share
+  // two IEEE reciprocals (this kernel is VALU-bound, a division is ~10
+  // instructions): each product adds one rounding of a positive term (rho <=
+  // 1/2 above), far inside the 1.0001 margin
   auto H = [&](float c, float& a_o, float& rho_o) {
     const float a = fmaxf(amin, (dmin * nlo * c - e_a) * 0.99999f);
-    const float rho = e_a / a;
-    const float du = e_sh / (a * (1.0f - rho)), dv = e_dq / (a * (1.0f - rho));
-    const float dw = (4.0f * fe + (e_sh + e_dq) / a + rho) / (1.0f - rho);
+    const float ra = 1.0f / a;
+    const float rho = e_a * ra;
+    const float rom = 1.0f / (1.0f - rho);
+    const float du = e_sh * ra * rom, dv = e_dq * ra * rom;
+    const float dw = (4.0f * fe + (e_sh + e_dq) * ra + rho) * rom;
     a_o = a;
     rho_o = rho;
     return (du + dv + dw) * (l1 + l2) * 1.0001f;
@@ -429,10 +434,11 @@ RTC_FN int quick_class(const CandParams& p, const float* r) {
     const float qx = cx - px, qy = cy - py, qz = cz - pz;  // centroid - pos
     const float R = sqrtf(qx * qx + qy * qy + qz * qz) * 0.99999f;
     if (R > 2.0f * rq) {
-      const float st = rq / R * 1.42f + 8.0f * fe + 1e-6f;
-      const float d0 = fminf(1.0f, fabsf(qx) / R + st) * 1.00001f;
-      const float d1 = fminf(1.0f, fabsf(qy) / R + st) * 1.00001f;
-      const float d2 = fminf(1.0f, fabsf(qz) / R + st) * 1.00001f;
+      const float rR = 1.0f / R;  // (one more rounding per quotient, inside the 1.00001 margins)
+      const float st = rq * rR * 1.42f + 8.0f * fe + 1e-6f;
+      const float d0 = fminf(1.0f, fabsf(qx) * rR + st) * 1.00001f;
+      const float d1 = fminf(1.0f, fabsf(qy) * rR + st) * 1.00001f;
+      const float d2 = fminf(1.0f, fabsf(qz) * rR + st) * 1.00001f;
       const float L = ((float)p.lmax + (float)p.dline) * 1.00001f, dl = (float)p.dline + 1e-6f;
       const float s0 = (L * d0 + fabsf(px) + dl) * 1.00001f;
       const float s1 = (L * d1 + fabsf(py) + dl) * 1.00001f;
