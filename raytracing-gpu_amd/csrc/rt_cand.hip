@@ -657,7 +657,10 @@ constexpr int kBigWaves = 4096;
 // the chip idle behind a few long ones: C5's largest footprint has 53,789
 // entries in rows of ~200 tiles, each lane writing its row alone, and the
 // kernel ran at 0.42 resident waves per SIMD (profiles/r03w_c5/pmc_sq.json).
-constexpr uint32_t kChunk = 1024;
+#ifndef RT_CAND_CHUNK
+#define RT_CAND_CHUNK 1024
+#endif
+constexpr uint32_t kChunk = RT_CAND_CHUNK;
 
 // Pass 0: the float fast path over every prim; flags the prims it cannot
 // prove safe (visits[prim] = 1), which an exclusive scan and scatter_kernel
