@@ -83,7 +83,8 @@ RTC_FN double pt_tri_dist(const double* x, const double* a, const double* b, con
                    ab[0] * ax[1] - ab[1] * ax[0]};
     double s[3] = {ax[1] * ac[2] - ax[2] * ac[1], ax[2] * ac[0] - ax[0] * ac[2],
                    ax[0] * ac[1] - ax[1] * ac[0]};
-    const double v = dot3(t, n) / nn, u = dot3(s, n) / nn;
+    const double inn = 1.0 / nn;  // (an ulp of the barycentrics: the edge cases take over)
+    const double v = dot3(t, n) * inn, u = dot3(s, n) * inn;
     if (u >= 0.0 && v >= 0.0 && u + v <= 1.0) return fabs(dot3(ax, n)) / sqrt(nn);
   }
   double best = 1e300;
@@ -120,7 +121,8 @@ RTC_FN int classify(const CandParams& p, const float* r, const float* leafbox, F
   const double nl = norm3(n);
   double e_a = p.c_a * kEps * l1 * l2 * kDMax;
   if (nl * kDMax + e_a < kAMin) return SAFE;  // |a| < 1e-7 for every ray: never accepted
-  const double nh[3] = {n[0] / nl, n[1] / nl, n[2] / nl};
+  const double inl = 1.0 / nl;  // (the unit normal to an ulp or two: inside every margin below)
+  const double nh[3] = {n[0] * inl, n[1] * inl, n[2] * inl};
   const double pv[3] = {p.pos[0] - v0[0], p.pos[1] - v0[1], p.pos[2] - v0[2]};
   const double deye = fabs(dot3(nh, pv));
   const double smax = p.lmax + norm3(pv);  // |o - v0| <= |o - pos| + |pos - v0|
@@ -181,10 +183,11 @@ RTC_FN int classify(const CandParams& p, const float* r, const float* leafbox, F
     for (int k = 0; k < 3; k++) qr = fmax(qr, dist3(P[k], q));
     const double R = dist3(q, p.pos);
     if (R > 2.0 * (qr + p.dline)) {
-      const double st = (qr + p.dline) / R * 1.42 + 8.0 * kEps;  // |d - q^| <= 2 sin(theta / 2)
+      const double iR = 1.0 / R;
+      const double st = (qr + p.dline) * iR * 1.42 + 8.0 * kEps;  // |d - q^| <= 2 sin(theta / 2)
       double dm[3], sm[3], ae1[3], ae2[3];
       for (int a = 0; a < 3; a++) {
-        dm[a] = fmin(1.0, fabs(q[a] - p.pos[a]) / R + st) * kDMax;
+        dm[a] = fmin(1.0, fabs(q[a] - p.pos[a]) * iR + st) * kDMax;
         sm[a] = ((p.lmax + p.dline) * dm[a] + fabs(pv[a]) + p.dline) * (1.0 + 1e-9);
         ae1[a] = fabs(e1[a]);
         ae2[a] = fabs(e2[a]);
@@ -695,9 +698,7 @@ __host__ __device__ inline bool small_count(const CandParams& p, const Footprint
 // Pass 1: classify the listed prims, keep each one's footprint and count the
 // tiles of the small ones (visits[j] for list entry j; visits is zero beyond
 // the list); big ones are queued for big_count_kernel.
-__global__ __launch_bounds__(256) void count_kernel(CandParams p) {
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= p.ctr[3]) return;
+__device__ __forceinline__ void count_one(const CandParams& p, uint32_t j) {
   const uint32_t prim = p.list[j];
   const float* rec = (const float*)(p.tri + 3 * (size_t)prim);
   uint32_t visits = 0;
@@ -718,6 +719,11 @@ __global__ __launch_bounds__(256) void count_kernel(CandParams p) {
     }
   }
   p.visits[j] = visits;
+}
+
+__global__ __launch_bounds__(256) void count_kernel(CandParams p) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < p.ctr[3]) count_one(p, j);
 }
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
