@@ -660,6 +660,11 @@ constexpr int kBigWaves = 4096;
 // the chip idle behind a few long ones: C5's largest footprint has 53,789
 // entries in rows of ~200 tiles, each lane writing its row alone, and the
 // kernel ran at 0.42 resident waves per SIMD (profiles/r03w_c5/pmc_sq.json).
+// threads per workgroup of the per-prim list passes (fast path,
+// classification, small emission)
+#ifndef RT_LIST_BLOCK
+#define RT_LIST_BLOCK 256
+#endif
 #ifndef RT_CAND_CHUNK
 #define RT_CAND_CHUNK 1024
 #endif
@@ -669,7 +674,7 @@ constexpr uint32_t kChunk = RT_CAND_CHUNK;
 // prove safe (visits[prim] = 1), which an exclusive scan and scatter_kernel
 // turn into a compact list, so the f64 classification of pass 1 runs on full
 // waves instead of on the scattered third of the lanes of every wave.
-__global__ __launch_bounds__(256) void quick_kernel(CandParams p) {
+__global__ __launch_bounds__(RT_LIST_BLOCK) void quick_kernel(CandParams p) {
   const uint32_t prim = blockIdx.x * blockDim.x + threadIdx.x;
   if (prim >= p.nprim) return;
   p.visits[prim] = quick_class(p, (const float*)(p.tri + 3 * (size_t)prim)) == Q_LIST ? 1u : 0u;
@@ -721,7 +726,7 @@ __device__ __forceinline__ void count_one(const CandParams& p, uint32_t j) {
   p.visits[j] = visits;
 }
 
-__global__ __launch_bounds__(256) void count_kernel(CandParams p) {
+__global__ __launch_bounds__(RT_LIST_BLOCK) void count_kernel(CandParams p) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j < p.ctr[3]) count_one(p, j);
 }
@@ -825,7 +830,7 @@ __device__ __forceinline__ uint32_t emit_row(const CandParams& p, const Footprin
 
 // Pass 2 (after the scan of visits): the small footprints write their
 // (tile, prim) pairs at their offsets.
-__global__ __launch_bounds__(256) void emit_kernel(CandParams p) {
+__global__ __launch_bounds__(RT_LIST_BLOCK) void emit_kernel(CandParams p) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= p.ctr[3]) return;
   uint32_t o = p.off[j];
@@ -1186,7 +1191,7 @@ extern "C" size_t rt_cand_footprint_bytes(void) { return sizeof(rtc::Footprint);
 
 extern "C" hipError_t rt_cand_quick(const CandParams* p, hipStream_t s) {
   if (p->nprim == 0) return hipSuccess;
-  hipLaunchKernelGGL(rtc::quick_kernel, dim3((p->nprim + 255) / 256), dim3(256), 0, s, *p);
+  hipLaunchKernelGGL(rtc::quick_kernel, dim3((p->nprim + RT_LIST_BLOCK - 1) / RT_LIST_BLOCK), dim3(RT_LIST_BLOCK), 0, s, *p);
   return hipGetLastError();
 }
 
@@ -1198,7 +1203,7 @@ extern "C" hipError_t rt_cand_scatter(const CandParams* p, hipStream_t s) {
 extern "C" hipError_t rt_cand_count(const CandParams* p, hipStream_t s) {
   if (p->nprim == 0) return hipSuccess;
   // sized for the worst case; threads beyond the list's length exit at once
-  hipLaunchKernelGGL(rtc::count_kernel, dim3((p->nprim + 255) / 256), dim3(256), 0, s, *p);
+  hipLaunchKernelGGL(rtc::count_kernel, dim3((p->nprim + RT_LIST_BLOCK - 1) / RT_LIST_BLOCK), dim3(RT_LIST_BLOCK), 0, s, *p);
   return hipGetLastError();
 }
 
@@ -1210,7 +1215,7 @@ extern "C" hipError_t rt_cand_big_count(const CandParams* p, hipStream_t s) {
 
 extern "C" hipError_t rt_cand_emit(const CandParams* p, hipStream_t s) {
   if (p->nprim == 0) return hipSuccess;
-  hipLaunchKernelGGL(rtc::emit_kernel, dim3((p->nprim + 255) / 256), dim3(256), 0, s, *p);
+  hipLaunchKernelGGL(rtc::emit_kernel, dim3((p->nprim + RT_LIST_BLOCK - 1) / RT_LIST_BLOCK), dim3(RT_LIST_BLOCK), 0, s, *p);
   return hipGetLastError();
 }
 
