@@ -665,6 +665,12 @@ constexpr int kBigWaves = 4096;
 #ifndef RT_LIST_BLOCK
 #define RT_LIST_BLOCK 256
 #endif
+// bits per radix place of the lists' sort (0: rocPRIM's tuned default, 8):
+// 9 sorts C5's 17-bit tile keys in two places instead of three (lists 2.13
+// -> 1.98 ms; 6 bits: 2.20; profiles/r04o_sort_bits/)
+#ifndef RT_SORT_BITS
+#define RT_SORT_BITS 9
+#endif
 #ifndef RT_CAND_CHUNK
 #define RT_CAND_CHUNK 1024
 #endif
@@ -1248,8 +1254,19 @@ extern "C" hipError_t rt_cand_scan(const uint32_t* in, uint32_t* out, uint32_t n
 extern "C" hipError_t rt_cand_sort(uint32_t* keys_in, uint32_t* keys_out, uint32_t* vals_in,
                                    uint32_t* vals_out, uint32_t n, int bits, void* temp,
                                    size_t* temp_bytes, hipStream_t s) {
+#if RT_SORT_BITS
+  // digits of RT_SORT_BITS bits per onesweep place (rocPRIM's gfx950 u32/u32
+  // tuning otherwise: 8 bits, so C5's 17-bit tile keys take three places)
+  using cfg = rocprim::radix_sort_config<
+      rocprim::default_config, rocprim::default_config,
+      rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 16>, rocprim::kernel_config<1024, 16>,
+                                          RT_SORT_BITS, rocprim::block_radix_rank_algorithm::match>>;
+  return rocprim::radix_sort_pairs<cfg>(temp, *temp_bytes, keys_in, keys_out, vals_in, vals_out, (size_t)n, 0,
+                                        bits, s);
+#else
   return rocprim::radix_sort_pairs(temp, *temp_bytes, keys_in, keys_out, vals_in, vals_out,
                                    (size_t)n, 0, bits, s);
+#endif
 }
 
 extern "C" hipError_t rt_cand_entry_skip(const uint32_t* cand, const float* skip, float* out,
