@@ -92,6 +92,12 @@ extern "C" hipError_t rt_cand_items(const CandParams* p, hipStream_t s);
 extern "C" hipError_t rt_cand_big_items(const CandParams* p, uint32_t nitems, hipStream_t s);
 extern "C" hipError_t rt_cand_scan(const uint32_t* in, uint32_t* out, uint32_t n, void* temp,
                                    size_t* temp_bytes, hipStream_t s);
+// exclusive scan of in[0 .. n], n = min(*n_dev, nmax) read on the device
+// (n_dev NULL: nmax): out[0 .. n], *total = out[n] (total may be NULL);
+// bsum: rt_cand_scan_dev_tiles(nmax) words of scratch
+extern "C" uint32_t rt_cand_scan_dev_tiles(uint32_t nmax);
+extern "C" hipError_t rt_cand_scan_dev(const uint32_t* in, uint32_t* out, uint32_t nmax, const uint32_t* n_dev,
+                                       uint32_t* total, uint32_t* bsum, hipStream_t s);
 extern "C" hipError_t rt_cand_sort(uint32_t* keys_in, uint32_t* keys_out, uint32_t* vals_in,
                                    uint32_t* vals_out, uint32_t n, int bits, void* temp,
                                    size_t* temp_bytes, hipStream_t s);

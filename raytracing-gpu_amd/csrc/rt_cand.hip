@@ -1013,6 +1013,103 @@ __global__ __launch_bounds__(256) void heavy_perm_kernel(const uint32_t* flags, 
   perm[flags[t] ? pos[t] : nheavy + t - pos[t]] = t;
 }
 
+
+// Exclusive scan of in[0 .. n] (n + 1 values: out[n] = the sum of in[0 ..
+// n - 1], also written to *total) with n read on the device (min(*n_dev,
+// nmax); n_dev NULL: nmax) -- the classification's scan runs over the listed
+// prims only, whose count the host does not know before its one
+// synchronisation.  Three passes over tiles of kScanTile values: tile sums,
+// one workgroup scanning them, tile-local scans through LDS (coalesced loads
+// and stores).  Deterministic (integer adds).
+constexpr int kScanThreads = 256, kScanPer = 16, kScanTile = kScanThreads * kScanPer;
+
+__device__ __forceinline__ uint32_t scan_len(uint32_t nmax, const uint32_t* n_dev) {
+  const uint32_t n = n_dev ? *n_dev : nmax;
+  return (n < nmax ? n : nmax) + 1u;
+}
+
+// exclusive scan of one value per thread over a 256-thread block; *sum = total
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* sh, uint32_t* sum) {
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  uint32_t inc = x;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) sh[wv] = inc;
+  __syncthreads();
+  uint32_t before = 0, tot = 0;
+  for (int k = 0; k < kScanThreads / 64; k++) {
+    if (k < wv) before += sh[k];
+    tot += sh[k];
+  }
+  __syncthreads();
+  *sum = tot;
+  return before + inc - x;
+}
+
+__global__ __launch_bounds__(kScanThreads) void scan_sums_kernel(const uint32_t* __restrict__ in, uint32_t nmax,
+                                                                 const uint32_t* n_dev, uint32_t* bsum) {
+  __shared__ uint32_t sh[kScanThreads / 64];
+  const uint32_t n1 = scan_len(nmax, n_dev), base = blockIdx.x * (uint32_t)kScanTile;
+  uint32_t x = 0;
+  if (base < n1)
+    for (int k = 0; k < kScanPer; k++) {
+      const uint32_t i = base + (uint32_t)(k * kScanThreads) + threadIdx.x;
+      if (i < n1) x += in[i];
+    }
+  uint32_t tot;
+  block_excl_scan(x, sh, &tot);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+
+// one workgroup: exclusive scan of the nb tile sums in place
+__global__ __launch_bounds__(kScanThreads) void scan_tops_kernel(uint32_t* bsum, uint32_t nb) {
+  __shared__ uint32_t sh[kScanThreads / 64];
+  uint32_t carry = 0;
+  for (uint32_t b0 = 0; b0 < nb; b0 += kScanThreads) {
+    const uint32_t i = b0 + threadIdx.x;
+    const uint32_t x = i < nb ? bsum[i] : 0u;
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan(x, sh, &tot);
+    if (i < nb) bsum[i] = carry + ex;
+    carry += tot;
+  }
+}
+
+__global__ __launch_bounds__(kScanThreads) void scan_apply_kernel(const uint32_t* __restrict__ in, uint32_t* out,
+                                                                  uint32_t nmax, const uint32_t* n_dev,
+                                                                  const uint32_t* bsum, uint32_t* total) {
+  __shared__ uint32_t v[kScanTile + kScanThreads];  // thread t's 16 values at t * 17 (no bank conflicts)
+  __shared__ uint32_t sh[kScanThreads / 64];
+  const uint32_t n1 = scan_len(nmax, n_dev), base = blockIdx.x * (uint32_t)kScanTile;
+  if (base >= n1) return;  // uniform per block
+  const int t = threadIdx.x;
+  for (int k = 0; k < kScanPer; k++) {
+    const uint32_t e = (uint32_t)(k * kScanThreads + t), i = base + e;
+    v[e + e / kScanPer] = i < n1 ? in[i] : 0u;
+  }
+  __syncthreads();
+  uint32_t run = 0;
+  for (int k = 0; k < kScanPer; k++) run += v[t * (kScanPer + 1) + k];
+  uint32_t tot;
+  uint32_t pre = bsum[blockIdx.x] + block_excl_scan(run, sh, &tot);
+  for (int k = 0; k < kScanPer; k++) {
+    const uint32_t x = v[t * (kScanPer + 1) + k];
+    v[t * (kScanPer + 1) + k] = pre;
+    pre += x;
+  }
+  __syncthreads();
+  for (int k = 0; k < kScanPer; k++) {
+    const uint32_t e = (uint32_t)(k * kScanThreads + t), i = base + e;
+    if (i < n1) {
+      const uint32_t o = v[e + e / kScanPer];
+      out[i] = o;
+      if (i == n1 - 1u && total) *total = o;
+    }
+  }
+}
+
 }  // namespace rtc
 
 #include <algorithm>
@@ -1242,6 +1339,20 @@ extern "C" hipError_t rt_cand_items(const CandParams* p, hipStream_t s) {
 extern "C" hipError_t rt_cand_big_items(const CandParams* p, uint32_t nitems, hipStream_t s) {
   if (nitems == 0) return hipSuccess;
   hipLaunchKernelGGL(rtc::big_item_kernel, dim3(nitems), dim3(64), 0, s, *p);
+  return hipGetLastError();
+}
+
+extern "C" uint32_t rt_cand_scan_dev_tiles(uint32_t nmax) {
+  return (nmax + 1u + (uint32_t)rtc::kScanTile - 1u) / (uint32_t)rtc::kScanTile;
+}
+
+extern "C" hipError_t rt_cand_scan_dev(const uint32_t* in, uint32_t* out, uint32_t nmax, const uint32_t* n_dev,
+                                       uint32_t* total, uint32_t* bsum, hipStream_t s) {
+  const uint32_t nb = rt_cand_scan_dev_tiles(nmax);
+  hipLaunchKernelGGL(rtc::scan_sums_kernel, dim3(nb), dim3(rtc::kScanThreads), 0, s, in, nmax, n_dev, bsum);
+  hipLaunchKernelGGL(rtc::scan_tops_kernel, dim3(1), dim3(rtc::kScanThreads), 0, s, bsum, nb);
+  hipLaunchKernelGGL(rtc::scan_apply_kernel, dim3(nb), dim3(rtc::kScanThreads), 0, s, in, out, nmax, n_dev,
+                     (const uint32_t*)bsum, total);
   return hipGetLastError();
 }
 

@@ -125,6 +125,7 @@ struct rt_hip_ctx {
   uint2* d_cand_items = nullptr;        // kItemCap big-emission work items
   uint32_t* d_cand_wave_items = nullptr;  // rt_cand_big_waves() + 1 each: items per big_count wave,
   uint32_t* d_cand_wave_base = nullptr;   // and their exclusive scan
+  uint32_t* d_scan_bsum = nullptr;        // rt_cand_scan_dev_tiles(nprim) tile sums of the device-length scans
   uint32_t cand_item_cap = 0xffffffffu;  // test hook: fewer items (min with kItemCap)
   uint32_t* d_prim_leaf = nullptr;    // nprim: a leaf holding each prim (camera-independent)
   uint32_t* d_cand = nullptr;
@@ -229,6 +230,7 @@ extern "C" void rt_hip_destroy(rt_hip_ctx* c) {
   (void)hipFree(c->d_cand_items);
   (void)hipFree(c->d_cand_wave_items);
   (void)hipFree(c->d_cand_wave_base);
+  (void)hipFree(c->d_scan_bsum);
   (void)hipFree(c->d_cand_skip);
   (void)hipFree(c->d_prim_leaf);
   (void)hipFree(c->d_cand);
@@ -871,6 +873,12 @@ static constexpr uint32_t kBigLaneCap = 1u << 17;
 #define RT_CAND_ITEM_CAP (1u << 20)
 #endif
 static constexpr uint32_t kItemCap = RT_CAND_ITEM_CAP;
+// the lists' two prim-length scans: the device-length scan of rt_cand.hip
+// (1; the classification's over the listed prims only, no zeroing pass) or
+// rocPRIM's over every prim (0)
+#ifndef RT_DEV_SCAN
+#define RT_DEV_SCAN 1
+#endif
 
 extern "C" int rt_hip_set_cand_item_cap(rt_hip_ctx* c, unsigned cap) {
   if (!c) return rt_set_error(RT_EINVAL, "null context");
@@ -1001,7 +1009,7 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
     for (void** b : {(void**)&c->d_cand_list, &c->d_cand_fp, (void**)&c->d_cand_visits, (void**)&c->d_cand_off,
                      (void**)&c->d_cand_global, (void**)&c->d_cand_big, (void**)&c->d_cand_ctr,
                      (void**)&c->d_cand_skip, (void**)&c->d_cand_big_lane, (void**)&c->d_cand_items,
-                     (void**)&c->d_cand_wave_items, (void**)&c->d_cand_wave_base}) {
+                     (void**)&c->d_cand_wave_items, (void**)&c->d_cand_wave_base, (void**)&c->d_scan_bsum}) {
       (void)hipFree(*b);
       *b = nullptr;
     }
@@ -1019,6 +1027,7 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
     HIP_TRY(hipMalloc((void**)&c->d_cand_wave_items, nw * sizeof(uint32_t)));
     HIP_TRY(hipMemset(c->d_cand_wave_items, 0, nw * sizeof(uint32_t)));  // [last] stays 0
     HIP_TRY(hipMalloc((void**)&c->d_cand_wave_base, nw * sizeof(uint32_t)));
+    HIP_TRY(hipMalloc((void**)&c->d_scan_bsum, (size_t)rt_cand_scan_dev_tiles((uint32_t)np) * sizeof(uint32_t)));
     HIP_TRY(hipHostMalloc((void**)&c->h_cand, 8 * sizeof(uint32_t), hipHostMallocDefault));
   }
   if (nt + 1 > c->cand_tiles_cap) {
@@ -1053,10 +1062,15 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
   if (rc) return rc;
   // pass 0: flags -> compact list of the prims the float fast path leaves
   HIP_TRY(rt_cand_quick(&cp, s));
+#if RT_DEV_SCAN
+  HIP_TRY(rt_cand_scan_dev(c->d_cand_visits, c->d_cand_off, (uint32_t)np, nullptr, nullptr, c->d_scan_bsum, s));
+  HIP_TRY(rt_cand_scatter(&cp, s));
+#else
   tb = c->scan_tmp_bytes;
   HIP_TRY(rt_cand_scan(c->d_cand_visits, c->d_cand_off, (uint32_t)np, c->d_scan_tmp, &tb, s));
   HIP_TRY(rt_cand_scatter(&cp, s));
   HIP_TRY(hipMemsetAsync(c->d_cand_visits, 0, (np + 1) * sizeof(uint32_t), s));
+#endif
   // pass 1: footprints and tile counts of the listed prims
   HIP_TRY(rt_cand_count(&cp, s));
   HIP_TRY(rt_cand_big_count(&cp, s));
@@ -1064,9 +1078,16 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
   tb = c->scan_tmp_bytes;
   HIP_TRY(rt_cand_scan(c->d_cand_wave_items, c->d_cand_wave_base, rt_cand_big_waves(), c->d_scan_tmp, &tb, s));
   HIP_TRY(rt_cand_items(&cp, s));
+#if RT_DEV_SCAN
+  // over the list's length only (ctr[3], on the device); the entry total -> ctr[6]
+  HIP_TRY(rt_cand_scan_dev(c->d_cand_visits, c->d_cand_off, (uint32_t)np, c->d_cand_ctr + 3, c->d_cand_ctr + 6,
+                           c->d_scan_bsum, s));
+  HIP_TRY(hipMemcpyAsync(c->h_cand, c->d_cand_ctr + 6, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+#else
   tb = c->scan_tmp_bytes;
   HIP_TRY(rt_cand_scan(c->d_cand_visits, c->d_cand_off, (uint32_t)np, c->d_scan_tmp, &tb, s));
   HIP_TRY(hipMemcpyAsync(c->h_cand, c->d_cand_off + np, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+#endif
   HIP_TRY(hipMemcpyAsync(c->h_cand + 1, c->d_cand_ctr + 1, 5 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(c->h_cand + 4, c->d_cand_wave_base + rt_cand_big_waves(), sizeof(uint32_t),
                          hipMemcpyDeviceToHost, s));
