@@ -38,7 +38,11 @@ struct CandParams {
   int W, H, tiles_x, tiles_y, rank, nranks, ntiles_local;
   int blocks_x, tb;       // tile blocks per block row, block side (csrc/rt_tiles.h: ranks own whole blocks)
   uint32_t* list;         // nprim: prims the float fast path cannot prove safe (pass 0)
-  rtc::Footprint* fp;     // nprim: footprint of list entry j (pass 1, read by passes 2 and big)
+  rtc::Footprint* fp;     // nprim: footprint of list entry j with a big footprint (pass 1, read by
+                          // the big passes); of every entry with tiles when store_fp (host check)
+  uint4* sfp;             // 2 nprim: a small footprint's rows as column intervals (pass 1 -> emit_kernel;
+                          // NULL: emit_kernel reads fp, which store_fp must then keep)
+  uint32_t store_fp;
   uint32_t* visits;       // nprim + 1: pass 0 flags, then tile entries of list entry j (pass 1)
   const uint32_t* off;    // nprim + 1: exclusive scan of visits
   uint32_t* keys;         // entries: local tile index (pass 2)

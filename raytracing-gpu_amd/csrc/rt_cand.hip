@@ -682,6 +682,8 @@ constexpr uint32_t kChunk = RT_CAND_CHUNK;
 // waves instead of on the scattered third of the lanes of every wave.
 __global__ __launch_bounds__(RT_LIST_BLOCK) void quick_kernel(CandParams p) {
   const uint32_t prim = blockIdx.x * blockDim.x + threadIdx.x;
+  if (prim < 8u) p.ctr[prim] = 0u;         // the frame's counters (count / big passes, later launches)
+  if (prim == 0u) p.visits[p.nprim] = 0u;  // the scan's last input
   if (prim >= p.nprim) return;
   p.visits[prim] = quick_class(p, (const float*)(p.tri + 3 * (size_t)prim)) == Q_LIST ? 1u : 0u;
 }
@@ -706,6 +708,29 @@ __host__ __device__ inline bool small_count(const CandParams& p, const Footprint
   return n <= kSmallEntries;
 }
 
+// A small footprint as emit_kernel needs it: its first tile row and row
+// count, and per row (at most kSmallRows) row_ivs's three column intervals as
+// 16-bit values -- 32 B instead of the 120 B footprint, and no f64 row
+// geometry in the emission.  (cand_prepare keeps the footprint path for
+// frames of 32,767 tile columns or more.)
+__device__ __forceinline__ void store_small(const CandParams& p, const Footprint& fp, uint32_t j) {
+  int r0, r1;
+  raster_rows(p, fp, r0, r1);  // true: the footprint has tiles
+  const int ty0 = r0 >> 3, nr = (r1 >> 3) - ty0 + 1;
+  uint32_t w[8] = {(uint32_t)ty0 | ((uint32_t)nr << 16), 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+  for (int r = 0; r < nr; r++) {
+    int x[6], f[3];
+    uint32_t c[3];
+    row_ivs(p, fp, ty0 + r, r0, r1, x, f, c);
+    for (int i = 0; i < 6; i++) {
+      const int h = 1 + r * 3 + i / 2;  // words 1..3 row 0, 4..6 row 1
+      w[h] |= ((uint32_t)x[i] & 0xffffu) << (16 * (i & 1));
+    }
+  }
+  p.sfp[2 * (size_t)j] = make_uint4(w[0], w[1], w[2], w[3]);
+  p.sfp[2 * (size_t)j + 1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+
 // Pass 1: classify the listed prims, keep each one's footprint and count the
 // tiles of the small ones (visits[j] for list entry j; visits is zero beyond
 // the list); big ones are queued for big_count_kernel.
@@ -722,9 +747,13 @@ __device__ __forceinline__ void count_one(const CandParams& p, uint32_t j) {
   } else if (c == FOOTPRINT) {
     p.skip[prim] = fp.skip;
     if (small_count(p, fp, visits)) {
-      if (visits) p.fp[j] = fp;
+      if (visits) {
+        if (p.store_fp) p.fp[j] = fp;
+        if (p.sfp) store_small(p, fp, j);
+      }
     } else {
       p.fp[j] = fp;
+      if (p.sfp) p.sfp[2 * (size_t)j] = make_uint4(0xffffffffu, 0u, 0u, 0u);  // big: not emit_kernel's
       p.big[atomicAdd(p.ctr + 2, 1u)] = j;
       visits = 0;  // big_count_kernel
     }
@@ -842,10 +871,24 @@ __global__ __launch_bounds__(RT_LIST_BLOCK) void emit_kernel(CandParams p) {
   uint32_t o = p.off[j];
   const uint32_t n = p.off[j + 1] - o;
   if (n == 0 || n > kSmallEntries) return;  // big footprints: big_kernel
+  const uint32_t prim = p.list[j];
+  if (p.sfp) {
+    const uint4 a = p.sfp[2 * (size_t)j];
+    if (a.x == 0xffffffffu) return;  // a big footprint of few entries
+    const uint4 b = p.sfp[2 * (size_t)j + 1];
+    const uint32_t w[7] = {a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    const int ty0 = (int)(a.x & 0xffffu), nr = (int)(a.x >> 16);
+    for (int r = 0; r < nr; r++)
+      for (int i = 0; i < 3; i++) {
+        const uint32_t v = w[r * 3 + i];
+        const int x0 = (int)(int16_t)(v & 0xffffu), x1 = (int)(int16_t)(v >> 16);
+        o += emit_interval(p, ty0 + r, x0, x1, o, prim);
+      }
+    return;
+  }
   const Footprint fp = p.fp[j];
   int r0, r1;
   if (!raster_rows(p, fp, r0, r1) || (r1 >> 3) - (r0 >> 3) + 1 > kSmallRows) return;
-  const uint32_t prim = p.list[j];
   for (int ty = r0 >> 3; ty <= (r1 >> 3); ty++) o += emit_row(p, fp, ty, r0, r1, o, prim);
 }
 
@@ -1293,7 +1336,10 @@ extern "C" int rt_cand_verify_host(const CandParams* p, const float* tri, const 
 extern "C" size_t rt_cand_footprint_bytes(void) { return sizeof(rtc::Footprint); }
 
 extern "C" hipError_t rt_cand_quick(const CandParams* p, hipStream_t s) {
-  if (p->nprim == 0) return hipSuccess;
+  if (p->nprim == 0) {  // no quick_kernel to zero the counters and the scan's last input
+    hipError_t e = hipMemsetAsync(p->ctr, 0, 8 * sizeof(uint32_t), s);
+    return e != hipSuccess ? e : hipMemsetAsync(p->visits, 0, sizeof(uint32_t), s);
+  }
   hipLaunchKernelGGL(rtc::quick_kernel, dim3((p->nprim + RT_LIST_BLOCK - 1) / RT_LIST_BLOCK), dim3(RT_LIST_BLOCK), 0, s, *p);
   return hipGetLastError();
 }

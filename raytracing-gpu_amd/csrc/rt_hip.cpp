@@ -49,6 +49,14 @@ extern "C" {
 
 #define RT_TIMED_FRAMES 1024
 
+// per-frame counters (one allocation, rt_hip_ctx::d_counter): 8 item-stream
+// counters 128 B apart, the stats, RT_HIT_REGIONS hit-record and as many
+// shade-chunk counters 32 words apart
+static constexpr size_t kItemCounterBytes = 8 * 128;
+static constexpr size_t kStatBytes = (RT_NSTATS * sizeof(unsigned long long) + 255) / 256 * 256;
+static constexpr size_t kHitCounterBytes = 2 * RT_HIT_REGIONS * 32 * sizeof(uint32_t);
+static constexpr size_t kFrameCounterBytes = kItemCounterBytes + kStatBytes + kHitCounterBytes;
+
 struct rt_hip_ctx {
   int device = 0;
   int accel = RT_ACCEL_FLAT;
@@ -111,6 +119,8 @@ struct rt_hip_ctx {
   uint32_t nprim = 0;
   uint32_t* d_cand_list = nullptr;    // nprim
   void* d_cand_fp = nullptr;          // nprim footprints (rt_cand_footprint_bytes each)
+  uint4* d_cand_sfp = nullptr;        // 2 nprim: compact small footprints (CandParams::sfp)
+  int cand_store_fp = 0;              // keep every footprint (rt_hip_cand_verify's re-derivation)
   uint32_t* d_cand_visits = nullptr;  // nprim + 1
   uint32_t* d_cand_off = nullptr;     // nprim + 1
   uint32_t* d_cand_start = nullptr;   // ntiles + 1
@@ -198,14 +208,12 @@ extern "C" void rt_hip_destroy(rt_hip_ctx* c) {
   (void)hipFree(c->d_mat);
   (void)hipFree(c->d_light);
   (void)hipFree(c->d_node);
-  (void)hipFree(c->d_counter);
-  (void)hipFree(c->d_stats);
+  (void)hipFree(c->d_counter);  // also holds d_stats and d_hit_count (kFrameCounterBytes)
   (void)hipFree(c->d_spill);
   (void)hipFree(c->d_tile_cycles);
   (void)hipFree(c->d_hit);
   (void)hipFree(c->d_hit_prev);
   (void)hipFree(c->d_hit_term);
-  (void)hipFree(c->d_hit_count);
   (void)hipFree(c->d_last);
   (void)hipFree(c->d_prim_mu);
   (void)hipFree(c->d_node_mu);
@@ -217,6 +225,7 @@ extern "C" void rt_hip_destroy(rt_hip_ctx* c) {
   if (c->d_tri_prim != c->d_tri) (void)hipFree(c->d_tri_prim);
   (void)hipFree(c->d_cand_list);
   (void)hipFree(c->d_cand_fp);
+  (void)hipFree(c->d_cand_sfp);
   (void)hipFree(c->d_cand_visits);
   (void)hipFree(c->d_cand_off);
   (void)hipFree(c->d_cand_start);
@@ -484,9 +493,14 @@ extern "C" int rt_hip_create(int device, const rt_scene* scene, int accel, rt_hi
   if (!rc) rc = upload(&c->d_mat, fs.mat, bytes_mat);
   if (!rc) rc = upload(&c->d_light, fs.light, bytes_light);
   if (!rc && fs.nnode) rc = upload(&c->d_node, fs.node, bytes_node);
-  if (!rc) rc = upload(&c->d_counter, nullptr, 8 * 128);  // 8 item-stream counters (rt_render.hip)
-  if (!rc) rc = upload(&c->d_stats, nullptr, RT_NSTATS * sizeof(unsigned long long));
-  if (!rc) rc = upload(&c->d_hit_count, nullptr, 2 * RT_HIT_REGIONS * 32 * sizeof(uint32_t));
+  // the per-frame counters in one allocation, zeroed by one memset per frame:
+  // 8 item-stream counters (rt_render.hip), the stats, the hit-record and
+  // shade-chunk counters
+  if (!rc) rc = upload(&c->d_counter, nullptr, kFrameCounterBytes);
+  if (!rc) {
+    c->d_stats = (unsigned long long*)((char*)c->d_counter + kItemCounterBytes);
+    c->d_hit_count = (uint32_t*)((char*)c->d_counter + kItemCounterBytes + kStatBytes);
+  }
   if (!rc && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
     rc = rt_set_error(RT_EHIP, "hipStreamCreate");
   rt_device_tree tree{};
@@ -717,14 +731,28 @@ extern "C" int rt_cand_survey(const rt_scene* scene, float eps_ulps, double boun
   return rc;
 }
 
+static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream_t s);
+
 extern "C" int rt_hip_cand_verify(rt_hip_ctx* c, const rt_frame* f, int rank, int nranks,
                                   unsigned long long out[7]) {
   if (!c || !f || !out) return rt_set_error(RT_EINVAL, "null argument");
   if (!c->d_cand_start || !c->d_cand || !c->d_cand_list)
     return rt_set_error(RT_EINVAL, "no candidate lists (render a frame with exact camera rays first)");
+  if (c->last_p.rank != rank || c->last_p.nranks != nranks)
+    return rt_set_error(RT_EINVAL, "the last render was rank %d of %d", c->last_p.rank, c->last_p.nranks);
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = c->last_stream ? c->last_stream : c->stream;
   HIP_TRY(hipStreamSynchronize(s));
+  // the render keeps only the big footprints: build the frame's lists again
+  // (deterministic: the same entries at the same places) keeping every one
+  {
+    KParams kp = c->last_p;
+    c->cand_store_fp = 1;
+    const int rp = cand_prepare(c, f, &kp, s);
+    c->cand_store_fp = 0;
+    if (rp) return rp;
+    HIP_TRY(hipStreamSynchronize(s));
+  }
   CandParams cp;
   int rc = cand_params(f, c->scene_c, c->scene_r, c->cam_eps_ulps, c->bound_scale, rank, nranks, &cp);
   if (rc) return rc;
@@ -1006,7 +1034,8 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
   if (!c->h_cand) {
     // h_cand is allocated last: a partial set left by an earlier failure is
     // freed here, never allocated over
-    for (void** b : {(void**)&c->d_cand_list, &c->d_cand_fp, (void**)&c->d_cand_visits, (void**)&c->d_cand_off,
+    for (void** b : {(void**)&c->d_cand_list, &c->d_cand_fp, (void**)&c->d_cand_sfp, (void**)&c->d_cand_visits,
+                     (void**)&c->d_cand_off,
                      (void**)&c->d_cand_global, (void**)&c->d_cand_big, (void**)&c->d_cand_ctr,
                      (void**)&c->d_cand_skip, (void**)&c->d_cand_big_lane, (void**)&c->d_cand_items,
                      (void**)&c->d_cand_wave_items, (void**)&c->d_cand_wave_base, (void**)&c->d_scan_bsum}) {
@@ -1015,6 +1044,7 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
     }
     HIP_TRY(hipMalloc((void**)&c->d_cand_list, (np + 1) * sizeof(uint32_t)));
     HIP_TRY(hipMalloc(&c->d_cand_fp, (np + 1) * rt_cand_footprint_bytes()));
+    HIP_TRY(hipMalloc((void**)&c->d_cand_sfp, 2 * (np + 1) * sizeof(uint4)));
     HIP_TRY(hipMalloc((void**)&c->d_cand_visits, (np + 1) * sizeof(uint32_t)));
     HIP_TRY(hipMalloc((void**)&c->d_cand_off, (np + 1) * sizeof(uint32_t)));
     HIP_TRY(hipMalloc((void**)&c->d_cand_global, (np + 1) * sizeof(uint32_t)));
@@ -1038,6 +1068,9 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
   }
   cp.list = c->d_cand_list;
   cp.fp = (rtc::Footprint*)c->d_cand_fp;
+  // compact small footprints while tile columns fit their 16-bit intervals
+  cp.sfp = cp.tiles_x < 32767 ? c->d_cand_sfp : nullptr;
+  cp.store_fp = (c->cand_store_fp || !cp.sfp) ? 1u : 0u;
   cp.visits = c->d_cand_visits;
   cp.off = c->d_cand_off;
   cp.global = c->d_cand_global;
@@ -1050,8 +1083,7 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
   cp.item_cap = c->cand_item_cap < kItemCap ? c->cand_item_cap : kItemCap;
   cp.wave_items = c->d_cand_wave_items;
   cp.wave_base = c->d_cand_wave_base;
-  HIP_TRY(hipMemsetAsync(c->d_cand_visits + np, 0, sizeof(uint32_t), s));
-  HIP_TRY(hipMemsetAsync(c->d_cand_ctr, 0, 8 * sizeof(uint32_t), s));
+  // (ctr[0 .. 7] and visits[np] are zeroed by quick_kernel)
   size_t tb = 0;
   HIP_TRY(rt_cand_scan(c->d_cand_visits, c->d_cand_off, (uint32_t)np, nullptr, &tb, s));
   rc = ensure_tmp(c, tb);
@@ -1303,9 +1335,7 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
     return rt_set_error(RT_EHIP, "render: prim-order records missing");
   if (!p.hit || !p.last || !p.out || (p.nrec && (!p.tri || !p.nrm)))
     return rt_set_error(RT_EHIP, "render: device buffers missing");
-  HIP_TRY(hipMemsetAsync(c->d_counter, 0, 8 * 128, s));  // 8 item streams, 128 B apart
-  HIP_TRY(hipMemsetAsync(c->d_stats, 0, RT_NSTATS * sizeof(unsigned long long), s));
-  HIP_TRY(hipMemsetAsync(c->d_hit_count, 0, 2 * RT_HIT_REGIONS * 32 * sizeof(uint32_t), s));
+  HIP_TRY(hipMemsetAsync(c->d_counter, 0, kFrameCounterBytes, s));  // item streams, stats, record counters
   if (c->timing) HIP_TRY(hipEventRecord(ev[1], s));
   HIP_TRY(rt_launch_trace(&p, dacc, c->count_work, pol, gt, s));
   if (c->timing) HIP_TRY(hipEventRecord(ev[2], s));
@@ -1664,9 +1694,7 @@ extern "C" int rt_hip_render_compat(rt_hip_ctx* c, const rt_camera* cam, unsigne
     p.sh_omax = c->sh_omax;
   }
   p.tri_prim = c->d_tri_prim;
-  if (hipMemsetAsync(c->d_counter, 0, 8 * 128, s) != hipSuccess ||
-      hipMemsetAsync(c->d_stats, 0, RT_NSTATS * sizeof(unsigned long long), s) != hipSuccess ||
-      hipMemsetAsync(c->d_hit_count, 0, 2 * RT_HIT_REGIONS * 32 * sizeof(uint32_t), s) != hipSuccess ||
+  if (hipMemsetAsync(c->d_counter, 0, kFrameCounterBytes, s) != hipSuccess ||
       rt_launch_compat(&p, accel, c->grid, s) != hipSuccess ||
       rt_launch_downscale(d_hi, d_lo, cam->width, cam->height, s) != hipSuccess ||
       hipMemcpyAsync(h_rgba, d_lo, nlo * sizeof(uint32_t), hipMemcpyDeviceToHost, s) != hipSuccess)
