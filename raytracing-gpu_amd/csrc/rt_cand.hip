@@ -711,24 +711,28 @@ __host__ __device__ inline bool small_count(const CandParams& p, const Footprint
 // A small footprint as emit_kernel needs it: its first tile row and row
 // count, and per row (at most kSmallRows) row_ivs's three column intervals as
 // 16-bit values -- 32 B instead of the 120 B footprint, and no f64 row
-// geometry in the emission.  (cand_prepare keeps the footprint path for
+// geometry in the emission.  small_count and this form in one pass (row_ivs's
+// counts add up to count_row's).  (cand_prepare keeps the footprint path for
 // frames of 32,767 tile columns or more.)
-__device__ __forceinline__ void store_small(const CandParams& p, const Footprint& fp, uint32_t j) {
+__device__ __forceinline__ bool small_pack(const CandParams& p, const Footprint& fp, uint32_t& n, uint32_t* w) {
   int r0, r1;
-  raster_rows(p, fp, r0, r1);  // true: the footprint has tiles
+  n = 0;
+  if (!raster_rows(p, fp, r0, r1)) return true;
   const int ty0 = r0 >> 3, nr = (r1 >> 3) - ty0 + 1;
-  uint32_t w[8] = {(uint32_t)ty0 | ((uint32_t)nr << 16), 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+  if (nr > kSmallRows) return false;
+  w[0] = (uint32_t)ty0 | ((uint32_t)nr << 16);
+  for (int h = 1; h < 8; h++) w[h] = 0u;
   for (int r = 0; r < nr; r++) {
     int x[6], f[3];
     uint32_t c[3];
     row_ivs(p, fp, ty0 + r, r0, r1, x, f, c);
+    n += c[0] + c[1] + c[2];
     for (int i = 0; i < 6; i++) {
       const int h = 1 + r * 3 + i / 2;  // words 1..3 row 0, 4..6 row 1
       w[h] |= ((uint32_t)x[i] & 0xffffu) << (16 * (i & 1));
     }
   }
-  p.sfp[2 * (size_t)j] = make_uint4(w[0], w[1], w[2], w[3]);
-  p.sfp[2 * (size_t)j + 1] = make_uint4(w[4], w[5], w[6], w[7]);
+  return n <= kSmallEntries;
 }
 
 // Pass 1: classify the listed prims, keep each one's footprint and count the
@@ -746,10 +750,14 @@ __device__ __forceinline__ void count_one(const CandParams& p, uint32_t j) {
     p.skip[prim] = -1e30f;
   } else if (c == FOOTPRINT) {
     p.skip[prim] = fp.skip;
-    if (small_count(p, fp, visits)) {
+    uint32_t w[8];
+    if (p.sfp ? small_pack(p, fp, visits, w) : small_count(p, fp, visits)) {
       if (visits) {
         if (p.store_fp) p.fp[j] = fp;
-        if (p.sfp) store_small(p, fp, j);
+        if (p.sfp) {
+          p.sfp[2 * (size_t)j] = make_uint4(w[0], w[1], w[2], w[3]);
+          p.sfp[2 * (size_t)j + 1] = make_uint4(w[4], w[5], w[6], w[7]);
+        }
       }
     } else {
       p.fp[j] = fp;
