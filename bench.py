@@ -268,11 +268,18 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    retry = 0
     try:
         st = ctx.stats()
     except rtgpu.RtError as e:  # the first frame sized the hit-record buffer: once more
         if e.code != -10:
             raise
+        retry = 1
+    # every rank steps again if any rank must (step() holds a collective)
+    flag = torch.tensor([retry], dtype=torch.int32, device=dev)
+    if world > 1:
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+    if int(flag.item()):
         step()
         torch.cuda.synchronize()
         st = ctx.stats()

@@ -120,6 +120,10 @@ typedef struct rt_accel_info {
    * triangles listed along a band of a point light's cube map */
   unsigned long long lightbuf_never;
   unsigned long long lightbuf_band;
+  /* lights whose buffer could not be built (too many entries, out of device
+   * memory): their shadow queries walk the octree instead (default mode; the
+   * exact-shadow mode fails rt_hip_set_exact_shadows / rt_hip_create instead) */
+  unsigned long long lightbuf_failed;
 } rt_accel_info;
 
 /* Host-only: build the acceleration structure rt_hip_create would build and
@@ -229,6 +233,10 @@ int rt_hip_set_exact_camera(rt_hip_ctx *ctx, int enable);
  * built once per scene and slack; 0: every shadow query walks the octree.
  * Both are exact in the same sense (DESIGN.md §2 "Shadow rays"). */
 int rt_hip_set_light_buffers(rt_hip_ctx *ctx, int enable);
+/* Test hook: a light buffer of more than cap entries fails its build (0 = no
+ * cap), exercising the fallback (that light's queries walk the octree,
+ * rt_accel_info.lightbuf_failed); rebuilds the buffers now. */
+int rt_hip_set_lightbuf_entry_cap(rt_hip_ctx *ctx, unsigned long long cap);
 int rt_hip_set_exact_shadows(rt_hip_ctx *ctx, int enable);
 /* Host-only survey (no device) of light `light`'s buffer as rt_hip_create
  * builds it for this scene (exact = proven footprints), every stride-th

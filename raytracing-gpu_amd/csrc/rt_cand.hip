@@ -1164,6 +1164,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_apply_kernel(const uint32_t
 }  // namespace rtc
 
 #include <algorithm>
+#include <cstdlib>
 #include <thread>
 #include <vector>
 
@@ -1275,68 +1276,94 @@ extern "C" int rt_cand_verify_host(const CandParams* p, const float* tri, const 
   out[0] = nlist;
   out[1] = start[ntiles];
   const rtc::Footprint* fpd = (const rtc::Footprint*)fp_dev;
-  std::vector<std::vector<uint32_t>> want(ntiles);
-  for (uint32_t j = 0; j < nlist; j++) {
-    const uint32_t prim = list[j];
-    rtc::Footprint fp;
-    std::memset(&fp, 0, sizeof fp);
-    const float* lb = prim_leaf ? node + 8 * (size_t)prim_leaf[prim] : nullptr;
-    const int c = rtc::classify(*p, tri + 12 * (size_t)prim, lb, fp);
-    if (c == rtc::GLOBAL) {
-      out[4]++;
-      continue;
-    }
-    if (c != rtc::FOOTPRINT) continue;  // safe after all (leaf box): no tiles
-    uint32_t n = 0;
-    rtc::raster(*p, fp, [&](uint32_t t) {
-      if (t < ntiles) want[t].push_back(prim);
-      n++;
-    });
-    if (n == 0) continue;  // the device keeps no footprint without tiles
-    const rtc::Footprint& d = fpd[j];
-    // (k, l, dimg are only set -- and only read -- with tri_ok)
-    bool same = d.tri_ok == fp.tri_ok && d.b0 == fp.b0 && d.b1 == fp.b1 && d.b2 == fp.b2 &&
-                d.hw == fp.hw && d.hw0 == fp.hw0 && d.skip == fp.skip;
-    if (same && fp.tri_ok) same = d.dimg == fp.dimg;
-    for (int k = 0; k < 3 && same && fp.tri_ok; k++) same = d.k[k] == fp.k[k] && d.l[k] == fp.l[k];
-    if (!same) out[2]++;
-  }
-  // prims the fast path did not list: proven safe, or their footprint has no
-  // tile of this rank (the rank/frame filter must never drop a needed one)
-  {
-    std::vector<unsigned char> listed(p->nprim + 1, 0);
-    for (uint32_t j = 0; j < nlist; j++) listed[list[j]] = 1;
-    for (uint32_t prim = 0; prim < p->nprim; prim++) {
-      const int qc = rtc::quick_class(*p, tri + 12 * (size_t)prim);
-      if (listed[prim]) {
-        if (qc != rtc::Q_LIST) out[5]++;
-        continue;
-      }
-      if (qc == rtc::Q_SAFE) {
-        // the float fast path's proof checked against the f64 one: a prim it
-        // calls safe must have no tile here by classify() either
+  // host threads: the process's share (OMP_NUM_THREADS on the GPU box), at
+  // most 64 -- C5 re-classifies ~10^7 prims in f64
+  int threads = (int)std::thread::hardware_concurrency();
+  if (const char* e = std::getenv("OMP_NUM_THREADS"))
+    if (std::atoi(e) > 0) threads = std::atoi(e);
+  threads = threads < 1 ? 1 : (threads > 64 ? 64 : threads);
+  std::vector<std::vector<uint64_t>> pairs(threads);  // (tile << 32 | prim) the host raster gives
+  std::vector<unsigned long long> cnt(7 * (size_t)threads, 0);
+  auto leafbox = [&](uint32_t prim) { return prim_leaf ? node + 8 * (size_t)prim_leaf[prim] : nullptr; };
+  std::vector<unsigned char> listed(p->nprim + 1, 0);
+  for (uint32_t j = 0; j < nlist; j++) listed[list[j]] = 1;
+  std::vector<std::thread> th;
+  for (int ti = 0; ti < threads; ti++)
+    th.emplace_back([&, ti]() {
+      unsigned long long* o = &cnt[7 * (size_t)ti];
+      // every prim the fast path listed: re-classified, its footprint
+      // compared with the device's bit for bit, its tiles collected
+      for (uint32_t j = (uint32_t)ti; j < nlist; j += (uint32_t)threads) {
+        const uint32_t prim = list[j];
         rtc::Footprint fp;
-        const float* lb = prim_leaf ? node + 8 * (size_t)prim_leaf[prim] : nullptr;
-        const int c = rtc::classify(*p, tri + 12 * (size_t)prim, lb, fp);
-        if (c == rtc::GLOBAL || (c == rtc::FOOTPRINT && rtc::raster_count(*p, fp) != 0)) out[5]++;
-        continue;
+        std::memset(&fp, 0, sizeof fp);
+        const int c = rtc::classify(*p, tri + 12 * (size_t)prim, leafbox(prim), fp);
+        if (c == rtc::GLOBAL) {
+          o[4]++;
+          continue;
+        }
+        if (c != rtc::FOOTPRINT) continue;  // safe after all (leaf box): no tiles
+        uint32_t n = 0;
+        rtc::raster(*p, fp, [&](uint32_t t) {
+          if (t < ntiles) pairs[ti].push_back((uint64_t)t << 32 | prim);
+          n++;
+        });
+        if (n == 0) continue;  // the device keeps no footprint without tiles
+        const rtc::Footprint& d = fpd[j];
+        // (k, l, dimg are only set -- and only read -- with tri_ok)
+        bool same = d.tri_ok == fp.tri_ok && d.b0 == fp.b0 && d.b1 == fp.b1 && d.b2 == fp.b2 &&
+                    d.hw == fp.hw && d.hw0 == fp.hw0 && d.skip == fp.skip;
+        if (same && fp.tri_ok) same = d.dimg == fp.dimg;
+        for (int k = 0; k < 3 && same && fp.tri_ok; k++) same = d.k[k] == fp.k[k] && d.l[k] == fp.l[k];
+        if (!same) o[2]++;
       }
-      if (qc == rtc::Q_LIST) {  // the device should have listed it
-        out[5]++;
-        continue;
+      // prims the fast path did not list: proven safe, or their footprint has
+      // no tile of this rank (the rank/frame filter must never drop a needed one)
+      const uint32_t chunk = (p->nprim + (uint32_t)threads - 1) / (uint32_t)threads;
+      const uint32_t b = (uint32_t)ti * chunk, e = b + chunk < p->nprim ? b + chunk : p->nprim;
+      for (uint32_t prim = b; prim < e; prim++) {
+        const int qc = rtc::quick_class(*p, tri + 12 * (size_t)prim);
+        if (listed[prim]) {
+          if (qc != rtc::Q_LIST) o[5]++;
+          continue;
+        }
+        if (qc == rtc::Q_LIST) {  // the device should have listed it
+          o[5]++;
+          continue;
+        }
+        // Q_SAFE: the float fast path's proof checked against the f64 one --
+        // a prim it calls safe must have no tile here by classify() either;
+        // Q_AWAY: the rank/frame filter's drop, likewise
+        rtc::Footprint fp;
+        const int c = rtc::classify(*p, tri + 12 * (size_t)prim, leafbox(prim), fp);
+        if (c == rtc::GLOBAL || (c == rtc::FOOTPRINT && rtc::raster_count(*p, fp) != 0)) o[5]++;
+        if (qc != rtc::Q_SAFE) o[6]++;
       }
-      rtc::Footprint fp;
-      const float* lb = prim_leaf ? node + 8 * (size_t)prim_leaf[prim] : nullptr;
-      const int c = rtc::classify(*p, tri + 12 * (size_t)prim, lb, fp);
-      if (c == rtc::GLOBAL || (c == rtc::FOOTPRINT && rtc::raster_count(*p, fp) != 0)) out[5]++;
-      out[6]++;
-    }
+    });
+  for (auto& x : th) x.join();
+  for (int ti = 0; ti < threads; ti++)
+    for (int k = 2; k < 7; k++) out[k] += cnt[7 * (size_t)ti + k];
+  // every tile's list as a multiset: the host pairs sorted (tile, prim)
+  // against each tile's sorted device entries
+  size_t np = 0;
+  for (auto& v : pairs) np += v.size();
+  std::vector<uint64_t> want;
+  want.reserve(np);
+  for (auto& v : pairs) {
+    want.insert(want.end(), v.begin(), v.end());
+    std::vector<uint64_t>().swap(v);
   }
+  std::sort(want.begin(), want.end());
+  size_t w = 0;
+  std::vector<uint32_t> got;
   for (uint32_t t = 0; t < ntiles; t++) {
-    std::vector<uint32_t> got(cand + start[t], cand + start[t + 1]);
+    got.assign(cand + start[t], cand + start[t + 1]);
     std::sort(got.begin(), got.end());
-    std::sort(want[t].begin(), want[t].end());
-    if (got != want[t]) out[3]++;
+    bool same = true;
+    size_t k = 0;
+    for (; w < want.size() && (uint32_t)(want[w] >> 32) == t; w++, k++)
+      same = same && k < got.size() && got[k] == (uint32_t)want[w];
+    if (!same || k != got.size()) out[3]++;
   }
   return 0;
 }

@@ -30,6 +30,8 @@ extern "C" {
 
 #ifndef RT_EPS_ULPS_DEFAULT
 #define RT_EPS_ULPS_DEFAULT 64
+#endif
+#ifndef RT_OOB_CAP
 #define RT_OOB_CAP (1u << 20)  // deferred shadow queries per render (exact-shadow mode)
 #endif
 // camera rays (bounce depth 0): a wider slack lets the walk itself find most
@@ -99,6 +101,7 @@ struct rt_hip_ctx {
   RtLightBuf* d_lbuf = nullptr;     // per light, device
   float lb_ulps = -1.0f;
   int lb_proven = -1;               // built proven (exact_shadows) or slack-grown
+  unsigned long long lb_entry_cap = 0;  // test hook: fail builds past this many entries (0: none)
   KParams last_p{};                 // the last render's parameters (rt_hip_verify_shadows)
   // exact shadow rays (csrc/rt_shadow.hip), built for the slack sh_ulps
   float2* d_prim_mu = nullptr;
@@ -385,6 +388,7 @@ static int lbuf_prepare(rt_hip_ctx* c, hipStream_t s) {
   std::vector<RtLightBuf> hb(c->nlight);
   std::memset(hb.data(), 0, hb.size() * sizeof(RtLightBuf));
   char err[256] = {0};
+  uint32_t failed = 0;
   for (uint32_t li = 0; li < c->nlight; li++) {
     const uint32_t t = c->light_type[li];
     if (t != 1 && t != 2) continue;
@@ -392,11 +396,23 @@ static int lbuf_prepare(rt_hip_ctx* c, hipStream_t s) {
     lb_fill(lp, c->scene_c, c->scene_r, c->scene_lo, c->scene_hi, c->eps_ulps, t, &c->light_v[3 * li], c->nprim,
             c->exact_shadows);
     lp.tri = c->d_tri_prim;
+    lp.max_entries = c->lb_entry_cap;
     if (rt_lightbuf_build(&lp, &hb[li], &c->lb_dev[li], s, err, sizeof err)) {
-      lbuf_release(c);
-      return rt_set_error(RT_EHIP, "light buffer of light %u: %s", li, err);
+      // the proven mode's exactness needs every buffer (its walk fallback is
+      // the per-node multiplier walk, not built alongside); otherwise the
+      // light's queries walk the octree (hb[li] is zeroed: RT_LB_NONE), as
+      // they did before light buffers -- a scene that fits the walk still loads
+      if (c->exact_shadows) {
+        lbuf_release(c);
+        return rt_set_error(RT_EHIP, "light buffer of light %u: %s", li, err);
+      }
+      std::memset(&hb[li], 0, sizeof hb[li]);
+      c->lb_dev[li] = nullptr;
+      (void)hipGetLastError();  // an out-of-memory hipMalloc is not sticky; clear it anyway
+      failed++;
     }
   }
+  c->info.lightbuf_failed = failed;
   HIP_TRY(hipMalloc((void**)&c->d_lbuf, hb.size() * sizeof(RtLightBuf)));
   HIP_TRY(hipMemcpy(c->d_lbuf, hb.data(), hb.size() * sizeof(RtLightBuf), hipMemcpyHostToDevice));
   c->lb_ulps = c->eps_ulps;
@@ -452,6 +468,14 @@ extern "C" int rt_hip_set_light_buffers(rt_hip_ctx* c, int enable) {
   c->light_buffers = enable ? 1 : 0;
   if (!c->light_buffers) lbuf_release(c);
   return RT_OK;
+}
+
+extern "C" int rt_hip_set_lightbuf_entry_cap(rt_hip_ctx* c, unsigned long long cap) {
+  if (!c) return rt_set_error(RT_EINVAL, "null context");
+  c->lb_entry_cap = cap;
+  lbuf_release(c);  // rebuilt (and the cap applied) by the next render
+  HIP_TRY(hipSetDevice(c->device));
+  return lbuf_prepare(c, c->stream);
 }
 
 extern "C" int rt_hip_create(int device, const rt_scene* scene, int accel, rt_hip_ctx** out) {
@@ -1266,6 +1290,22 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
   // (DESIGN.md "Conservative culling")
   p.eps_rel = c->eps_ulps * 5.9604645e-8f;
   p.eps_rel_cam = c->cam_eps_ulps * 5.9604645e-8f;
+  if (p.ntiles_local == 0) {
+    // a rank past the frame's last block (e.g. 96x54 over 8 ranks: 6 blocks)
+    // renders nothing; its tile buffer (sized by rank 0) stays as it is and
+    // gathers as padding.  Its stats read 0.
+    c->cand_prims = c->cand_entries = c->cand_global = 0;
+    hipEvent_t* ev = c->ev[c->frames % RT_TIMED_FRAMES];
+    if (c->timing) HIP_TRY(hipEventRecord(ev[0], s));
+    HIP_TRY(hipMemsetAsync(c->d_counter, 0, kFrameCounterBytes, s));
+    if (c->timing) {
+      for (int k = 1; k < 5; k++) HIP_TRY(hipEventRecord(ev[k], s));
+      c->frames++;
+    }
+    c->last_p = p;
+    c->last_stream = s;
+    return RT_OK;
+  }
   {
     int rc = hit_buffers(c, (size_t)p.ntiles_local);
     if (rc) return rc;
@@ -1300,7 +1340,11 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
     if (rc) return rc;
     if (c->policy == RT_POLICY_DEFAULT || c->policy == RT_POLICY_LANE) p.lbuf = c->d_lbuf;
   }
-  if (p.lbuf && c->exact_shadows) {  // proven buffers: the off-box queries' queue
+  // proven buffers: the off-box queries' queue.  An entry carries the
+  // decided bits of lights 0..31 only, so with more lights the off-box
+  // queries are counted instead (shadow_unproven -> RT_EINEXACT), never
+  // re-shaded without the lights past the 32nd
+  if (p.lbuf && c->exact_shadows && c->nlight <= 32) {
     if (!c->d_oob) {
       HIP_TRY(hipMalloc((void**)&c->d_oob_count, sizeof(uint32_t)));
       HIP_TRY(hipMalloc((void**)&c->d_oob, (size_t)RT_OOB_CAP * sizeof(uint4)));

@@ -57,6 +57,9 @@ struct LBParams {
   // walk); 1: grown by the reference float test's proven error region for the
   // light's ray family (exact by construction, DESIGN.md §2 "Shadow rays")
   uint32_t proven;
+  // test hook (rt_hip_set_lightbuf_entry_cap): fail a build of more entries
+  // than this (0: only the 2^31 format limit)
+  uint64_t max_entries;
 };
 
 struct LBDevice;  // device allocations of one light's buffer (rt_lightbuf.hip)

@@ -1158,7 +1158,7 @@ extern "C" int rt_lightbuf_build(const LBParams* in, RtLightBuf* out, LBDevice**
       total = sum;
     }
   }
-  if (total >= (1ull << 31)) {
+  if (total >= (1ull << 31) || (in->max_entries && total > in->max_entries)) {
     snprintf(err, errlen, "light buffer of %llu entries", (unsigned long long)total);
     rc = -1;
     goto done;

@@ -109,7 +109,8 @@ class AccelInfo(C.Structure):
                 ("max_leaf", C.c_ulonglong), ("shadow_global", C.c_ulonglong),
                 ("shadow_mu_max", C.c_double), ("lightbuf_entries", C.c_ulonglong),
                 ("lightbuf_global", C.c_ulonglong), ("lightbuf_seconds", C.c_double),
-                ("lightbuf_never", C.c_ulonglong), ("lightbuf_band", C.c_ulonglong)]
+                ("lightbuf_never", C.c_ulonglong), ("lightbuf_band", C.c_ulonglong),
+                ("lightbuf_failed", C.c_ulonglong)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -159,6 +160,7 @@ _PROTOS = [
     ("rt_hip_set_policy", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_set_exact_shadows", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_set_light_buffers", C.c_int, [C.c_void_p, C.c_int]),
+    ("rt_hip_set_lightbuf_entry_cap", C.c_int, [C.c_void_p, C.c_ulonglong]),
     ("rt_lightbuf_survey", C.c_int, [C.c_void_p, C.c_uint, C.c_int, C.c_uint, C.c_void_p]),
     ("rt_hip_probe_shadows", C.c_int, [C.c_void_p, C.c_uint, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]),
     ("rt_hip_tile_cycles", C.c_int, [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_size_t]),
@@ -459,6 +461,11 @@ class Context:
     def set_light_buffers(self, on=True):
         """Light buffers for the default shadow queries (rt_hip_set_light_buffers)."""
         _check(lib().rt_hip_set_light_buffers(self.h, 1 if on else 0), "light_buffers")
+
+    def set_lightbuf_entry_cap(self, cap):
+        """Test hook: light-buffer builds of more than `cap` entries fail (0: no cap);
+        the buffers are rebuilt now (rt_hip_set_lightbuf_entry_cap)."""
+        _check(lib().rt_hip_set_lightbuf_entry_cap(self.h, int(cap)), "lightbuf_entry_cap")
 
     def probe_shadows(self, light, origins, brute=False):
         """Shadow rays of light `light` from (n, 3) origins: shadowed flags

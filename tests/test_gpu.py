@@ -472,6 +472,26 @@ def test_candidate_lists_match_host(gpu, accel, nranks, ranks, item_cap):
         assert v["filter_violation"] == 0 and v["filtered"] > 0, str(v)
 
 
+def test_candidate_lists_match_host_c5(gpu):
+    """The headline scene itself (C5: 10,010,626 triangles at 3840x2160):
+    every float fast-path verdict (Q_SAFE / Q_LIST / rank-filtered) checked
+    against the f64 classify() over all 10M triangles, every listed
+    footprint bit for bit and every tile's list as a multiset -- for the
+    whole frame (N = 1) and for ranks 0 and 3 of an 8-way split.  This pins
+    the exactness of the shipped camera-ray lists on the shipped tree
+    (/root/reference/cpu/hit.c:4-44,72-91)."""
+    s = gpu.Scene.synthetic(32, 32, 9776, seed=0x5EED, width=3840, height=2160)
+    assert s.triangle_count == 10010626
+    f = s.frame()
+    ctx = gpu.Context(s, "octree_gpu")
+    for nranks, rank in ((1, 0), (8, 0), (8, 3)):
+        _tiles_of_rank(ctx, f, rank, nranks)
+        v = ctx.cand_verify(f, rank, nranks)
+        assert v["listed"] > 0 and v["entries"] > 0, v
+        assert v["fp_mismatch"] == 0 and v["tile_mismatch"] == 0, (nranks, rank, v)
+        assert v["filter_violation"] == 0, (nranks, rank, v)
+
+
 def test_zero_normal_is_an_error(gpu, tmp_path):
     """cpu/hit.c:79 skips an object whose closest hit has an exactly zero
     interpolated normal; that rule is not reproduced, so a render that meets
@@ -571,6 +591,89 @@ def test_light_buffer_probe_grazing(gpu, li, exact):
     assert 0.01 < ref.mean() < 0.99, ref.mean()
     assert len(bad) == 0, (f"{len(bad)} of {len(o)} grazing shadow rays differ from brute force "
                            f"(buffer lit, brute shadowed: {int((~got & ref).sum())}); first {bad[:5].tolist()}")
+
+
+def test_empty_rank_on_fresh_context(gpu, scene_dir, manifest):
+    """A rank past the frame's last tile block renders nothing: 96x54 over 8
+    ranks has 6 blocks of 4x4 tiles, so ranks 6 and 7 own none.  On a fresh
+    context the render succeeds with zero counts, and the 8-rank assemble of
+    all ranks (the empty ones' buffers as padding) is the golden image."""
+    import ctypes as C
+    case = next(c for c in manifest if c["scene"] == "cube" and c["width"] == 96)
+    s = gpu.Scene.load_svati(os.path.join(scene_dir, "cube.svati"))
+    s.set_size(case["width"], case["height"])
+    f = s.frame()
+    assert gpu.rank_tile_count(f.width, f.height, 7, 8) == 0
+    fresh = gpu.Context(s, "octree")
+    t, st = _tiles_of_rank(fresh, f, 7, 8)
+    assert len(t) == 0 and st["closest"] == 0 and st["shadow"] == 0 and st["pixels"] == 0
+    ctx = gpu.Context(s, "octree")
+    n = 8
+    per = gpu.tile_buffer_floats(f.width, f.height, n)
+    L = gpu.lib()
+    dg, drgb = C.c_void_p(), C.c_void_p()
+    assert L.rt_hip_malloc(0, per * n * 4, C.byref(dg)) == 0
+    assert L.rt_hip_malloc(0, f.width * f.height * 12, C.byref(drgb)) == 0
+    tot = 0
+    for r in (7, 6, 0, 1, 2, 3, 4, 5):  # the empty ranks first, on this context too
+        ctx.render(f, r, n, dg.value + r * per * 4)
+        tot += ctx.stats()["closest"]
+    ctx.assemble(f, dg.value, n, drgb.value)
+    img = np.empty((f.height, f.width, 3), np.float32)
+    ctx.stats()
+    assert L.rt_hip_memcpy_d2h(img.ctypes.data_as(C.c_void_p), drgb, img.nbytes) == 0
+    L.rt_hip_free(dg)
+    L.rt_hip_free(drgb)
+    assert_bitexact(img, golden_image(case), "8 ranks, two of them empty")
+    assert tot == case["closest"]
+
+
+def test_light_buffer_build_failure_falls_back_to_walk(gpu):
+    """A light buffer that cannot be built (here: capped at one entry by the
+    test hook) leaves that light's shadow queries on the octree walk instead
+    of failing the context; the image is unchanged.  The exact-shadow mode,
+    whose proof needs the buffers, fails loudly instead."""
+    s = gpu.Scene.synthetic(3, 3, 9776, seed=0x5EED, width=320, height=180)
+    f = s.frame()
+    ctx = gpu.Context(s, "octree_gpu")
+    img, st = ctx.render_image(f)
+    assert ctx.info()["lightbuf_failed"] == 0 and ctx.info()["lightbuf_entries"] > 0
+    ctx.set_lightbuf_entry_cap(1)
+    assert ctx.info()["lightbuf_failed"] == 2 and ctx.info()["lightbuf_entries"] == 0
+    img2, st2 = ctx.render_image(f)
+    assert_bitexact(img2, img, "shadow queries on the walk after a failed light-buffer build")
+    assert (st2["closest"], st2["shadow"]) == (st["closest"], st["shadow"])
+    with pytest.raises(gpu.RtError):
+        ctx.set_exact_shadows(True)
+
+
+def test_exact_shadows_more_than_32_lights(gpu, tmp_path):
+    """Exact-shadow mode with 35 lights: the off-box queue carries the bits
+    of lights 0..31 only, so it is off and every off-box query is counted
+    (RT_EINEXACT) -- the render equals brute force or fails loudly, never
+    silently drops lights 32 and up."""
+    base = gpu.Scene.synthetic(3, 3, 9776, seed=0x5EED, width=160, height=90)
+    src = tmp_path / "base.svati"
+    base.write_svati(str(src))
+    lines = open(src).read().split("\n")
+    extra = [f"p_light 0.02 0.03 0.04 {-6 + 0.4 * k:.2f} {3 + 0.1 * k:.2f} -4" if k % 2 else
+             f"d_light 0.03 0.02 0.01 {0.1 * (k - 16):.2f} -1 0.5" for k in range(32)]
+    cam = next(i for i, ln in enumerate(lines) if ln.startswith("camera"))
+    sv = tmp_path / "lights35.svati"
+    sv.write_text("\n".join(lines[:cam + 1] + extra + lines[cam + 1:]))
+    s = gpu.Scene.load_svati(str(sv))
+    assert s.s.light_count == 35
+    f = s.frame()
+    img_f, st_f = gpu.Context(s, "flat").render_image(f)
+    ctx = gpu.Context(s, "octree_gpu")
+    ctx.set_exact_shadows(True)
+    try:
+        img, st = ctx.render_image(f)
+    except gpu.RtError as e:
+        assert e.code == gpu.Context.RT_EINEXACT, e
+        return
+    assert_bitexact(img, img_f, "35 lights, exact shadows vs brute force")
+    assert (st["closest"], st["shadow"]) == (st_f["closest"], st_f["shadow"])
 
 
 @pytest.mark.parametrize("exact", [False, True])
