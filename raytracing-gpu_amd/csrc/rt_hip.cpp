@@ -91,7 +91,7 @@ struct rt_hip_ctx {
   size_t hit_need = 0;              // per region: what the last overflowing frame needed
   uint32_t* d_last = nullptr;       // per (item, lane): a path's deepest record
   size_t last_cap = 0;              // items
-  int grid_of[2][4][2] = {};        // persistent grids [trace][policy][count_work]
+  int grid_of[2][5][2] = {};        // persistent grids [trace][policy][count_work] (policy 4: shade only)
   int cus = 0;                      // compute units of the device
   std::vector<uint32_t> light_type; // per light (rt_hip_verify_shadows)
   std::vector<float> light_v;       // per light: l.v (3 floats)
@@ -602,7 +602,7 @@ extern "C" int rt_hip_create(int device, const rt_scene* scene, int accel, rt_hi
   int gmax = c->grid;
   const int dacc = c->accel == RT_ACCEL_FLAT ? RT_ACCEL_FLAT_D : RT_ACCEL_OCTREE_D;
   for (int tr = 0; tr < 2; tr++)
-    for (int pol = 0; pol < 4; pol++)
+    for (int pol = 0; pol < (tr ? 4 : 5); pol++)
       for (int cw = 0; cw < 2; cw++) {
         int g = 0;
         hipError_t he = rt_render_grid(tr, dacc, cw, pol, prop.multiProcessorCount, &g);
@@ -1372,7 +1372,17 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
   const bool empty = c->accel == RT_ACCEL_OCTREE && !c->d_node;
   const int dacc = (c->accel == RT_ACCEL_FLAT || empty) ? RT_ACCEL_FLAT_D : RT_ACCEL_OCTREE_D;
   const int pol = dacc == RT_ACCEL_FLAT_D ? 0 : c->policy, cw = c->count_work ? 1 : 0;
-  const int gt = empty ? c->grid : c->grid_of[1][pol][cw], gs = empty ? c->grid : c->grid_of[0][pol][cw];
+  // the shade kernel without the walk when every directional / point light
+  // queries its buffer (the default and per-lane policies use buffers)
+  int spol = pol;
+  if (dacc == RT_ACCEL_OCTREE_D && p.lbuf && !p.node_mu && !p.n_sh_global &&
+      (pol == RT_POLICY_DEFAULT || pol == RT_POLICY_LANE)) {
+    bool all = true;
+    for (uint32_t li = 0; li < c->nlight && all; li++)
+      if (c->light_type[li] == 1 || c->light_type[li] == 2) all = c->lb_dev[li] != nullptr;
+    if (all) spol = RT_POLICY_LBUF;
+  }
+  const int gt = empty ? c->grid : c->grid_of[1][pol][cw], gs = empty ? c->grid : c->grid_of[0][spol][cw];
   // every device pointer the kernels will follow must exist (a null one
   // would fault the card, not fail the call)
   if (!p.tri_prim && (p.lbuf || p.n_sh_global || p.cand_start))
@@ -1383,7 +1393,7 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
   if (c->timing) HIP_TRY(hipEventRecord(ev[1], s));
   HIP_TRY(rt_launch_trace(&p, dacc, c->count_work, pol, gt, s));
   if (c->timing) HIP_TRY(hipEventRecord(ev[2], s));
-  HIP_TRY(rt_launch_shade(&p, dacc, c->count_work, pol, gs, s));
+  HIP_TRY(rt_launch_shade(&p, dacc, c->count_work, spol, gs, s));
   HIP_TRY(rt_launch_shade_fixup(&p, c->nprim, s));
   if (c->timing) HIP_TRY(hipEventRecord(ev[3], s));
   HIP_TRY(rt_launch_fold(&p, s));

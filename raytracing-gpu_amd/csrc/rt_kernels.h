@@ -43,6 +43,11 @@
 #ifndef RT_SHADE_MIN_WAVES
 #define RT_SHADE_MIN_WAVES 8
 #endif
+// the staged test policies' shade kernels (packet any-hit walks, test / A/B
+// only) need more registers than 8 waves allow: their own, reachable, target
+#ifndef RT_STAGED_SHADE_MIN_WAVES
+#define RT_STAGED_SHADE_MIN_WAVES 4
+#endif
 // camera candidate tests two records per packed-float instruction
 // (rt_render.hip mt_candidate_pk); 0: one record per scalar test.  Measured
 // slower (C5 trace 6.27 -> 6.51 ms, profiles/r04e_pk/ab.log): the phase is
@@ -66,6 +71,11 @@
 #define RT_POLICY_LANE 1        // every octree query per lane
 #define RT_POLICY_STAGED 2      // every octree query as a staged packet
 #define RT_POLICY_DIR_STAGED 3  // default + staged packet directional-light shadows
+// shade kernel only, chosen by the host (never by rt_hip_set_policy): the
+// default policy when every directional / point light has a light buffer --
+// the shadow queries compile to the buffer scan alone, without the octree
+// walk's registers and code (the default's fallback for lights without one)
+#define RT_POLICY_LBUF 4
 
 // wave-total counters (wave-uniform, so they live in SGPRs; 32-bit per wave,
 // widened to 64-bit by the final atomics)

@@ -1146,12 +1146,29 @@ __device__ bool lbuf_any(const KParams& p, const RtLightBuf& L, const Ray& r, La
 template <int ACCEL, bool COUNT, int POL>
 __device__ __forceinline__ bool shadow_q(const KParams& p, f3 o, f3 d, uint32_t type, uint32_t li,
                                          bool act, Stack& s, WaveCtx& w, WorkCount& wc, bool* defer = nullptr,
-                                         const LbRange* pre = nullptr) {
+                                         const LbRange* pre = nullptr, bool can_defer = true) {
   uint64_t am = __ballot(act);
   wc.shadow += (uint32_t)__popcll(am);
   Ray r = make_ray(p, o, d, p.eps_rel);
   if (ACCEL == RT_ACCEL_FLAT_D)
     return use_tp(p, act) ? flat_any_tp<COUNT>(p, r, act, wc) : flat_any_w<COUNT>(p, r, act, w, wc);
+  if (POL == RT_POLICY_LBUF) {  // every such light has a buffer (rt_hip.cpp): no walk, no global prims
+    const RtLightBuf& L = p.lbuf[li];
+    LaneCount lc = {0, 0, 0, 0, 0, 0, 0};
+    bool hit = act && (pre ? lbuf_scan<COUNT>(p, L, r, *pre, lc) : lbuf_any<COUNT>(p, L, r, lc));
+    absorb<COUNT>(wc, lc, true);
+    if (L.proven) {  // as below
+      const bool out = act && !(o.x >= L.olo[0] && o.x <= L.ohi[0] && o.y >= L.olo[1] && o.y <= L.ohi[1] &&
+                                o.z >= L.olo[2] && o.z <= L.ohi[2]);
+      if (defer && can_defer && p.oob) {
+        *defer = out;
+        if (out) hit = false;
+      } else {
+        wc.sh_unproven += (uint32_t)__popcll(__ballot(out));
+      }
+    }
+    return hit;
+  }
   bool staged = POL == RT_POLICY_STAGED ||
                 (POL == RT_POLICY_DIR_STAGED && type == 1 && __popcll(am) >= kPacketMin);
   bool hit;
@@ -1169,7 +1186,7 @@ __device__ __forceinline__ bool shadow_q(const KParams& p, f3 o, f3 d, uint32_t 
       // record after the pass (cpu/hit.c:93-109)
       const bool out = act && !(o.x >= L.olo[0] && o.x <= L.ohi[0] && o.y >= L.olo[1] && o.y <= L.ohi[1] &&
                                 o.z >= L.olo[2] && o.z <= L.ohi[2]);
-      if (defer && p.oob) {  // decided GPU-wide after the pass (rt_launch_shade_fixup)
+      if (defer && can_defer && p.oob) {  // decided GPU-wide after the pass (rt_launch_shade_fixup)
         *defer = out;
         if (out) hit = false;
       } else {  // (lights past the 32nd) counted, never assumed: RT_EINEXACT
@@ -1618,8 +1635,10 @@ __device__ __forceinline__ col shade_record(const KParams& p, bool valid, size_t
         // (issuing the first two lights' cell-range loads before either
         // query, through shadow_q's `pre`, measured slower: shade 1.92 ->
         // 2.16 ms on C5, profiles/r04b_shade_pre/)
+        // (df by address, the block-0 condition a flag: a pointer chosen per
+        // block kept df on the stack, a scratch store per query)
         const bool sh = shadow_q<ACCEL, COUNT, POL>(p, P, shadow_dir(type, lv, P), type, li, valid, s, w, wc,
-                                                    l0 == 0 ? &df : nullptr);
+                                                    &df, nullptr, l0 == 0);
         if (COUNT) {
           const uint32_t dc = (uint32_t)(__builtin_readcyclecounter() - c0);
           wc.cy_shadow += dc;
@@ -1656,7 +1675,9 @@ __device__ __forceinline__ col shade_record(const KParams& p, bool valid, size_t
 // cpu/light.c:33-100 with the shadow queries of cpu/light.c:24-31, then the
 // term color_mul(local, coef) of cpu/raytracer.c:30.
 template <int ACCEL, bool COUNT, int POL>
-__global__ __launch_bounds__(64, ACCEL == RT_ACCEL_FLAT_D ? RT_FLAT_SHADE_MIN_WAVES : RT_SHADE_MIN_WAVES) void shade_kernel(KParams p) {
+__global__ __launch_bounds__(64, ACCEL == RT_ACCEL_FLAT_D ? RT_FLAT_SHADE_MIN_WAVES
+                                : ((POL == RT_POLICY_STAGED || POL == RT_POLICY_DIR_STAGED) ? RT_STAGED_SHADE_MIN_WAVES
+                                                                                              : RT_SHADE_MIN_WAVES)) void shade_kernel(KParams p) {
   const int lane = threadIdx.x & 63;
   WorkCount wc = {};
   constexpr bool kStaged = POL == RT_POLICY_STAGED || POL == RT_POLICY_DIR_STAGED;
@@ -2081,6 +2102,9 @@ static const void* kernel_of(int accel, int count_work, int policy) {
                       : (const void*)trace_kernel<RT_ACCEL_OCTREE_D, false, RT_POLICY_DEFAULT>;
   }
   if (policy == RT_POLICY_STAGED) return (const void*)shade_kernel<RT_ACCEL_OCTREE_D, false, RT_POLICY_STAGED>;
+  if (policy == RT_POLICY_LBUF)
+    return count_work ? (const void*)shade_kernel<RT_ACCEL_OCTREE_D, true, RT_POLICY_LBUF>
+                      : (const void*)shade_kernel<RT_ACCEL_OCTREE_D, false, RT_POLICY_LBUF>;
   if (policy == RT_POLICY_DIR_STAGED)
     return (const void*)shade_kernel<RT_ACCEL_OCTREE_D, false, RT_POLICY_DIR_STAGED>;
   return count_work ? (const void*)shade_kernel<RT_ACCEL_OCTREE_D, true, RT_POLICY_DEFAULT>
