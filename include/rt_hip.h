@@ -212,7 +212,9 @@ int rt_hip_tile_cycles(rt_hip_ctx *ctx, unsigned long long *out, size_t n);
 int rt_hip_set_count_work(rt_hip_ctx *ctx, int enable);
 /* The same items' phase clocks (trace kernel): phase 0 = the item's total
  * (= rt_hip_tile_cycles), 1 camera walk, 2 camera candidate tests, 3
- * secondary walks.  Shadow queries run in the shade kernel, per hit record. */
+ * secondary walks; 4 and 5 are counts, not clocks: the most node visits and
+ * triangle tests one lane of the item made in per-lane secondary walks.
+ * Shadow queries run in the shade kernel, per hit record. */
 int rt_hip_tile_phase_cycles(rt_hip_ctx *ctx, int phase, unsigned long long *out, size_t n);
 /* Exact camera rays (default 1): per-frame candidate lists of the triangles
  * whose float Moller-Trumbore error region the octree slack does not cover

@@ -880,7 +880,7 @@ extern "C" int rt_hip_tile_cycles(rt_hip_ctx* c, unsigned long long* out, size_t
 }
 
 extern "C" int rt_hip_tile_phase_cycles(rt_hip_ctx* c, int phase, unsigned long long* out, size_t n) {
-  if (!c || !out || phase < 0 || phase > 3) return rt_set_error(RT_EINVAL, "bad argument");
+  if (!c || !out || phase < 0 || phase > 5) return rt_set_error(RT_EINVAL, "bad argument");
   if (!c->d_tile_cycles || n > c->tile_cycles_n)
     return rt_set_error(RT_EINVAL, "%zu item clocks asked, %zu recorded (rt_hip_set_count_work)", n,
                         c->tile_cycles_n);

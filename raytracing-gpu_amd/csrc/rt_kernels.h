@@ -48,13 +48,6 @@
 #ifndef RT_STAGED_SHADE_MIN_WAVES
 #define RT_STAGED_SHADE_MIN_WAVES 4
 #endif
-// camera candidate tests two records per packed-float instruction
-// (rt_render.hip mt_candidate_pk); 0: one record per scalar test.  Measured
-// slower (C5 trace 6.27 -> 6.51 ms, profiles/r04e_pk/ab.log): the phase is
-// not VALU-issue bound, and the pairs cost registers (7 -> 17 spills)
-#ifndef RT_CAND_PK
-#define RT_CAND_PK 0
-#endif
 // the brute-force (FLAT) shade kernel streams records through LDS, two at a
 // time (mt_candidate2): at 8 waves it spilled 96 B per lane
 #ifndef RT_FLAT_SHADE_MIN_WAVES
@@ -92,6 +85,9 @@ struct WorkCount {
   uint32_t stack_spills;   // per-lane stack pushes past the LDS entries (COUNT pass)
   uint32_t zero_risk;      // shadow hits on objects whose interpolated normal can vanish
   uint32_t sh_unproven;    // point-light shadow rays from beyond the proof's assumed extent
+  // COUNT pass, per work item (rt_hip_tile_phase_cycles phases 4, 5): the
+  // most node visits / triangle tests one lane made in per-lane secondary walks
+  uint32_t sec_lane_nodes, sec_lane_tris;
 };
 
 struct KParams {

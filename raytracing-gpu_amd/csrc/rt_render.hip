@@ -139,39 +139,6 @@ __device__ __forceinline__ void mt_candidate2(f3 o, f3 d, const float4* qa, cons
   cb = cb && !(tb < kEps * (1.0f - m) || tb > t_cut);
 }
 
-// Two records per instruction: a pair of staged records held component-wise,
-// P[c] = (record A's c-th float, record B's), c = 0 .. 11 in the record's own
-// order (v0, e1, e2, then q2.yzw).  float2 arithmetic lowers to v_pk_mul_f32 /
-// v_pk_add_f32 -- per half the same IEEE operation as the scalar
-// instruction, so every value below has the bits mt_candidate computes.
-typedef float pf2 __attribute__((ext_vector_type(2)));
-
-// mt_candidate of both records of a staged pair (hasb false: A only).  Same
-// operations in the same order (cross, dot as rt_device.h), same decisions,
-// about half the VALU instructions of two scalar calls.
-__device__ __forceinline__ void mt_candidate_pk(f3 o, f3 d, const pf2* P, bool hasb, float t_cut,
-                                                bool& ca, bool& cb) {
-  const float m = 1e-5f;
-  const pf2 v0x = P[0], v0y = P[1], v0z = P[2], e1x = P[3], e1y = P[4], e1z = P[5];
-  const pf2 e2x = P[6], e2y = P[7], e2z = P[8];
-  const pf2 hx = d.y * e2z - d.z * e2y, hy = d.z * e2x - d.x * e2z, hz = d.x * e2y - d.y * e2x;
-  const pf2 a = e1x * hx + e1y * hy + e1z * hz;
-  const pf2 r = {__builtin_amdgcn_rcpf(a.x), __builtin_amdgcn_rcpf(a.y)};
-  const pf2 sx = o.x - v0x, sy = o.y - v0y, sz = o.z - v0z;
-  const pf2 u = (sx * hx + sy * hy + sz * hz) * r;
-  ca = !(a.x > -kEps && a.x < kEps) && !(u.x < -1e-30f || u.x > 1.0f + m);
-  cb = hasb && !(a.y > -kEps && a.y < kEps) && !(u.y < -1e-30f || u.y > 1.0f + m);
-  if (__ballot(ca || cb) == 0) return;
-  const pf2 qx = sy * e1z - sz * e1y, qy = sz * e1x - sx * e1z, qz = sx * e1y - sy * e1x;
-  const pf2 v = (d.x * qx + d.y * qy + d.z * qz) * r;
-  ca = ca && !(v.x < -1e-30f || u.x + v.x > 1.0f + m);
-  cb = cb && !(v.y < -1e-30f || u.y + v.y > 1.0f + m);
-  if (__ballot(ca || cb) == 0) return;
-  const pf2 t = (e2x * qx + e2y * qy + e2z * qz) * r;
-  ca = ca && !(t.x < kEps * (1.0f - m) || t.x > t_cut);
-  cb = cb && !(t.y < kEps * (1.0f - m) || t.y > t_cut);
-}
-
 struct Best {
   float dist;  // +inf = none
   float t_cut; // parametric bound beyond which no triangle can win (+inf = none)
@@ -1031,6 +998,16 @@ __device__ __forceinline__ void closest_q(const KParams& p, const Ray& r, bool a
     LaneCount lc = {0, 0, 0, 0, 0, 0, 0};
     if (act) oct_closest<COUNT>(p, r, b, s, lc);
     absorb<COUNT>(wc, lc, false);
+    if (COUNT && depth > 0) {
+      uint32_t mn = lc.lnodes, mt = lc.ltris;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        mn = max(mn, (uint32_t)__shfl_xor((int)mn, off));
+        mt = max(mt, (uint32_t)__shfl_xor((int)mt, off));
+      }
+      wc.sec_lane_nodes = max(wc.sec_lane_nodes, uni(mn));
+      wc.sec_lane_tris = max(wc.sec_lane_tris, uni(mt));
+    }
   }
 }
 
@@ -1299,31 +1276,16 @@ __device__ col apply_light(const KParams& p, bool hit, const float* m, f3 P, f3 
 // and of the global list, tested with the reference's exact arithmetic after
 // the walk -- the ones whose float Moller-Trumbore error region reaches
 // beyond the walk's culling slack.
+// Entries [s, e) of the candidate list (kOctRecs per round: each lane loads
+// one entry and its skip bound, the survivors' records are gathered in
+// parallel -- one memory round trip -- into the LDS stage, compacted, then
+// tested one after another as LDS broadcasts).  bmax: entries whose depth
+// skip bound exceeds it cannot win any lane.  Returns the entries tested.
 template <bool COUNT>
-__device__ __forceinline__ void cand_closest(const KParams& p, const Ray& r, bool act, uint32_t tile,
-                                             Best& b, WaveCtx& w, WorkCount& wc) {
-  if (!p.cand_start || __ballot(act) == 0) return;
-  // Depth skip: a candidate's float new_dist is at least |pos - o| + its
-  // entry's cand_skip (csrc/rt_cand.hip), so one whose bound exceeds every
-  // lane's best - |pos - o| (plus the float error of that difference)
-  // cannot win here -- one compare instead of a test.  (A per-lane test of
-  // the footprint's image-space band, measured: the bands of the long
-  // footprints are 6-34 pixels wide, so nearly every listed tile has lanes
-  // inside; it removed 1 % of the tests and cost 2.7 ms on C5.)
-  float bl = -__builtin_inff();
-  if (act)
-    bl = b.dist == __builtin_inff() ? __builtin_inff()
-                                    : (b.dist - length(sub(p.pos, r.o))) + (2e-3f + 4e-7f * b.dist);
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) bl = fmaxf(bl, __shfl_xor(bl, off));
-  const float bmax = __uint_as_float(uni(__float_as_uint(bl)));
-  const uint32_t s = uni(p.cand_start[tile]), e = uni(p.cand_start[tile + 1]);
+__device__ __forceinline__ uint32_t cand_range(const KParams& p, const Ray& r, bool act, uint32_t s, uint32_t e,
+                                               float bmax, Best& b, WaveCtx& w) {
   const int lane = w.lane;
   uint32_t tested = 0;
-  // kOctRecs entries per round: each lane loads one entry and its skip
-  // bound, the survivors' records are gathered in parallel (one memory round
-  // trip) into the LDS stage, compacted, then tested one after another as
-  // LDS broadcasts
   for (uint32_t base = s; base < e; base += kOctRecs) {
     uint32_t prim = 0;
     bool keep = false;
@@ -1343,28 +1305,6 @@ __device__ __forceinline__ void cand_closest(const KParams& p, const Ray& r, boo
       g2 = q[2];
     }
     wave_sync();  // after the previous readers of stage
-#if RT_CAND_PK
-    // pairs of survivors, component-wise (mt_candidate_pk): slot s is half
-    // s & 1 of pair s >> 1, whose 12 float2 take 6 ds_read_b128
-    if (keep) {
-      float* sf = (float*)w.stage + (slot >> 1) * 24 + (slot & 1);
-      const float c[12] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w, g2.x, g2.y, g2.z, g2.w};
-#pragma unroll
-      for (int i = 0; i < 12; i++) sf[2 * i] = c[i];
-    }
-    wave_sync();
-    for (uint32_t k = 0; k < n; k += 2) {
-      const pf2* P = (const pf2*)w.stage + (k >> 1) * 12;
-      bool ca = false, cb = false;
-      if (act) mt_candidate_pk(r.o, r.d, P, k + 1 < n, b.t_cut, ca, cb);
-      if (ca)
-        consider_exact(r, float4{P[0].x, P[1].x, P[2].x, P[3].x}, float4{P[4].x, P[5].x, P[6].x, P[7].x},
-                       float4{P[8].x, P[9].x, P[10].x, P[11].x}, b);
-      if (cb)
-        consider_exact(r, float4{P[0].y, P[1].y, P[2].y, P[3].y}, float4{P[4].y, P[5].y, P[6].y, P[7].y},
-                       float4{P[8].y, P[9].y, P[10].y, P[11].y}, b);
-    }
-#else
     if (keep) {
       w.stage[3 * slot] = g0;
       w.stage[3 * slot + 1] = g1;
@@ -1373,14 +1313,37 @@ __device__ __forceinline__ void cand_closest(const KParams& p, const Ray& r, boo
     wave_sync();
     // (two candidates per step as two scalar chains, as the brute-force loops
     // do, measured slower here: C5 frame 15.96 -> 16.10 ms,
-    // profiles/r03f_bench/ab.log)
+    // profiles/r03f_bench/ab.log; two per packed-float instruction, RT_CAND_PK
+    // of round 3, slower too: profiles/r04e_pk/ab.log)
     for (uint32_t k = 0; k < n; k++) {
       float4 q0 = w.stage[3 * k], q1 = w.stage[3 * k + 1], q2 = w.stage[3 * k + 2];
       if (act) consider(r, q0, q1, q2, b);
     }
-#endif
     tested += n;
   }
+  return tested;
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void cand_closest(const KParams& p, const Ray& r, bool act, uint32_t tile,
+                                             Best& b, WaveCtx& w, WorkCount& wc) {
+  if (!p.cand_start || __ballot(act) == 0) return;
+    // Depth skip: a candidate's float new_dist is at least |pos - o| + its
+    // entry's cand_skip (csrc/rt_cand.hip), so one whose bound exceeds every
+    // lane's best - |pos - o| (plus the float error of that difference)
+    // cannot win here -- one compare instead of a test.  (A per-lane test of
+    // the footprint's image-space band, measured: the bands of the long
+    // footprints are 6-34 pixels wide, so nearly every listed tile has lanes
+    // inside; it removed 1 % of the tests and cost 2.7 ms on C5.)
+    float bl = -__builtin_inff();
+    if (act)
+      bl = b.dist == __builtin_inff() ? __builtin_inff()
+                                      : (b.dist - length(sub(p.pos, r.o))) + (2e-3f + 4e-7f * b.dist);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) bl = fmaxf(bl, __shfl_xor(bl, off));
+    const float bmax = __uint_as_float(uni(__float_as_uint(bl)));
+  const uint32_t tested =
+      cand_range<COUNT>(p, r, act, uni(p.cand_start[tile]), uni(p.cand_start[tile + 1]), bmax, b, w);
   for (uint32_t k = 0; k < p.n_cand_global; k++) {
     const float4* q = p.tri_prim + 3 * (size_t)uni(p.cand_global[k]);
     float4 q0 = ldu(q, 0), q1 = ldu(q, 1), q2 = ldu(q, 2);
@@ -1441,6 +1404,25 @@ __device__ __forceinline__ void flush_counts(const KParams& p, const WorkCount& 
 // previous record in hit_prev.  Record index = region | (slot << 3).
 __device__ __forceinline__ size_t rec_addr(const KParams& p, uint32_t idx) {
   return (size_t)(idx & 7u) * p.hit_cap + (idx >> 3);
+}
+
+// Camera sample smp of lane `lane` of rank-local tile t: its ray (origin on
+// the film, direction towards the eye) exactly as cpu/raytracer.c:55-60
+// computes it; false when the lane's pixel lies outside the framebuffer's
+// even-sized area (its ray is still defined).
+__device__ __forceinline__ bool camera_sample(const KParams& p, uint32_t t, int smp, int lane, f3& point, f3& dir) {
+  int pr, pc;
+  tile_pixel(p, t, lane, pr, pc);
+  // PPM (row, col) -> framebuffer slot (j, i) of cpu/raytracer.c:71,128-134
+  const int ii = p.W - pc, jj = p.H - pr;
+  const bool valid = pr < p.H && pc < p.W && ii >= 1 && ii <= 2 * (p.W / 2) && jj >= 1 && jj <= 2 * (p.H / 2);
+  const int i = ii - p.W / 2, j = jj - p.H / 2;
+  // for (float k = i; k < i + 1; k += 0.5) for (float l = j; ...)  (cpu/raytracer.c:55-58)
+  const float k = (float)i + 0.5f * (float)(smp >> 1);
+  const float l = (float)j + 0.5f * (float)(smp & 1);
+  point = add(add(p.C, scale(p.u, k)), scale(p.v, l));
+  dir = normalize(sub(p.pos, point));
+  return valid;
 }
 
 // One camera sample for every lane of the wave (trace_kernel): the
@@ -1573,21 +1555,12 @@ __global__ __launch_bounds__(64, RT_TRACE_MIN_WAVES) void trace_kernel(KParams p
     const uint32_t u = 4u * (p.tile_order ? p.tile_order[pos] : pos) + (q & 3u);  // item 4t + s
     const unsigned long long c0 = COUNT ? __builtin_readcyclecounter() : 0ull;
     const uint32_t ph0[3] = {wc.cy_cam, wc.cy_cand, wc.cy_sec};
+    wc.sec_lane_nodes = wc.sec_lane_tris = 0;
     const uint32_t t = u >> 2;
     const int smp = (int)(u & 3u);
-    int pr, pc;
-    tile_pixel(p, t, lane, pr, pc);
-    // PPM (row, col) -> framebuffer slot (j, i) of cpu/raytracer.c:71,128-134
-    const int ii = p.W - pc, jj = p.H - pr;
-    const bool valid = pr < p.H && pc < p.W && ii >= 1 && ii <= 2 * (p.W / 2) && jj >= 1 &&
-                       jj <= 2 * (p.H / 2);
-    const int i = ii - p.W / 2, j = jj - p.H / 2;
+    f3 point, dir;
+    const bool valid = camera_sample(p, t, smp, lane, point, dir);
     if (smp == 0) wc.pixels += (uint32_t)__popcll(__ballot(valid));
-    // for (float k = i; k < i + 1; k += 0.5) for (float l = j; ...)  (cpu/raytracer.c:55-58)
-    const float k = (float)i + 0.5f * (float)(smp >> 1);
-    const float l = (float)j + 0.5f * (float)(smp & 1);
-    f3 point = add(add(p.C, scale(p.u, k)), scale(p.v, l));
-    f3 dir = normalize(sub(p.pos, point));
     p.last[(size_t)u * 64 + lane] =
         trace_path<ACCEL, COUNT, POL>(p, valid, point, dir, x, stk, w, wc, t);
     if (COUNT && p.tile_cycles && lane == 0) {
@@ -1598,6 +1571,8 @@ __global__ __launch_bounds__(64, RT_TRACE_MIN_WAVES) void trace_kernel(KParams p
       p.tile_cycles[u] = __builtin_readcyclecounter() - c0;
 #pragma unroll
       for (int k2 = 0; k2 < 3; k2++) p.tile_cycles[u + (size_t)(k2 + 1) * items] = ph1[k2] - ph0[k2];
+      p.tile_cycles[u + 4 * items] = wc.sec_lane_nodes;
+      p.tile_cycles[u + 5 * items] = wc.sec_lane_tris;
     }
   }
   flush_counts(p, wc, lane);
