@@ -283,6 +283,10 @@ int rt_cand_survey(const rt_scene *scene, float eps_ulps, double bound_scale, in
 int rt_hip_cand_verify(rt_hip_ctx *ctx, const rt_frame *frame, int rank, int nranks,
                        unsigned long long out[7]);
 
+/* The same after an rt_hip_render_compat of `camera` (its 3x frame's lists,
+ * one sample per high-resolution pixel). */
+int rt_hip_cand_verify_compat(rt_hip_ctx *ctx, const rt_camera *camera, unsigned long long out[7]);
+
 /* Test hook: after an rt_hip_render, shade every stride-th hit record of
  * each region again through the context's walk and by brute force over every
  * triangle (cpu/hit.c:93-109), and compare each record's shadow outcome per
@@ -319,7 +323,9 @@ int rt_hip_render_image(rt_hip_ctx *ctx, const rt_frame *frame, float *h_rgb, rt
  * reflections summed front to back over at most 11 closest-hit queries, then
  * a 3x3 box downscale.  h_rgba receives width x height RGBA8 pixels (alpha
  * 255) in gpu/rt's PNG row order.  stats as rt_hip_stats (camera = pixels =
- * high-resolution rays).  No camera candidate lists in this mode. */
+ * high-resolution rays).  Camera rays keep the exactness of cpu mode: the
+ * per-frame candidate lists of the 3x frame's one-ray-per-pixel camera
+ * (csrc/rt_cand.hip, CandParams::compat). */
 int rt_hip_render_compat(rt_hip_ctx *ctx, const rt_camera *cam, unsigned char *h_rgba,
                          rt_stats *stats);
 /* Drop-in for gpu/rt's main (gpu/rt.cpp:56-97): load, render in

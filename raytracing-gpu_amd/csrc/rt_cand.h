@@ -35,6 +35,11 @@ struct CandParams {
   double eps_avail;       // culling slack every camera ray gets, minus the slab test's rounding
   double c_dot, c_a;      // error-bound constants (tools/mt_bound.py C_DOT, C_A)
   double kmin, kmax, lmin, lmax_;  // sample coordinates of the frame
+  // sample model: 0 = cpu/rt's (pixel (r, c) samples k in [W/2 - c, W/2 - c
+  // + 1/2], l likewise, cpu/raytracer.c:55-58); 1 = gpu/rt's compatibility
+  // mode (one ray per pixel of the 3x frame at k = c - W/2, l = r - H/2,
+  // gpu/raytracer.cu:97-103; one rank)
+  int compat;
   int W, H, tiles_x, tiles_y, rank, nranks, ntiles_local;
   int blocks_x, tb;       // tile blocks per block row, block side (csrc/rt_tiles.h: ranks own whole blocks)
   uint32_t* list;         // nprim: prims the float fast path cannot prove safe (pass 0)

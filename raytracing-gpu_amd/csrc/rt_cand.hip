@@ -288,6 +288,24 @@ __host__ __device__ inline uint32_t rank_tiles(const CandParams& p, int ty, int 
                            (uint32_t)p.tb, nullptr);
 }
 
+// The pixel columns (rows: row = true) whose samples' k (l) can lie in
+// [a, b], clamped to the frame (empty: c0 > c1).  cpu/rt: pixel c samples
+// k in [W/2 - c, W/2 - c + 1/2] (cpu/raytracer.c:55-58);
+// compatibility mode: pixel c is the one sample k = c - W/2.  Clamped in
+// double before the conversion (a far-off footprint gives values beyond
+// int range, whose conversion the host does not saturate).
+__host__ __device__ inline void pixel_range(const CandParams& p, double a, double b, int& c0, int& c1, bool row) {
+  const int n = row ? p.H : p.W;
+  const double h = (double)(n / 2);
+  if (p.compat) {
+    c0 = (int)fmin(fmax(0.0, ceil(a + h)), (double)n);
+    c1 = (int)fmax(fmin((double)(n - 1), floor(b + h)), -1.0);
+  } else {
+    c0 = (int)fmin(fmax(0.0, ceil(h - b)), (double)n);
+    c1 = (int)fmax(fmin((double)(n - 1), floor(h - a + 0.5)), -1.0);
+  }
+}
+
 // Can a footprint inside the ball (q, rb) -- every candidate crossing point
 // of the triangle lies in it -- reach a tile of this rank?  The ball's
 // bounding box projects (through the eye, on one side of the eye plane) into
@@ -340,11 +358,9 @@ RTC_FN bool rank_may_touch(const CandParams& p, const double q[3], double rb) {
   lmn -= m;
   lmx += m;
   // samples of pixel (r, c): k in [W/2 - c, W/2 - c + 1/2], l likewise (raster_rows)
-  const double hw_ = (double)(p.W / 2), hh = (double)(p.H / 2);
-  const int r0 = (int)fmin(fmax(0.0, ceil(hh - lmx)), (double)p.H);
-  const int r1 = (int)fmax(fmin((double)(p.H - 1), floor(hh - lmn + 0.5)), -1.0);
-  const int c0 = (int)fmin(fmax(0.0, ceil(hw_ - kmx)), (double)p.W);
-  const int c1 = (int)fmax(fmin((double)(p.W - 1), floor(hw_ - kmn + 0.5)), -1.0);
+  int r0, r1, c0, c1;
+  pixel_range(p, (double)kmn, (double)kmx, c0, c1, false);
+  pixel_range(p, (double)lmn, (double)lmx, r0, r1, true);
   if (r0 > r1 || c0 > c1) return false;  // off the frame
   const uint32_t n = (uint32_t)p.nranks, rk = (uint32_t)p.rank;
   if (n == 1) return true;
@@ -480,17 +496,13 @@ RTC_FN int quick_class(const CandParams& p, const float* r) {
 // r).
 // Pixel rows [r0, r1] the footprint can reach; false: none.
 __host__ __device__ inline bool raster_rows(const CandParams& p, const Footprint& fp, int& r0, int& r1) {
-  const double hh = (double)(p.H / 2);
   r0 = 0;
   r1 = p.H - 1;
   if (fp.tri_ok && fp.hw0 < 0.0) {
     const double lmn = fmin(fp.l[0], fmin(fp.l[1], fp.l[2])) - fp.dimg;
     const double lmx = fmax(fp.l[0], fmax(fp.l[1], fp.l[2])) + fp.dimg;
     if (!(lmx >= p.lmin && lmn <= p.lmax_)) return false;
-    // clamped in double before the conversion (a far-off footprint gives
-    // values beyond int range, whose conversion the host does not saturate)
-    r0 = (int)fmin(fmax(0.0, ceil(hh - lmx)), (double)p.H);
-    r1 = (int)fmax(fmin((double)(p.H - 1), floor(hh - lmn + 0.5)), -1.0);
+    pixel_range(p, lmn, lmx, r0, r1, true);
   }
   return r0 <= r1;
 }
@@ -500,10 +512,9 @@ __host__ __device__ inline bool raster_rows(const CandParams& p, const Footprint
 // counts where it leaves the first).
 __host__ __device__ inline void row_tiles(const CandParams& p, const Footprint& fp, int ty, int r0,
                                           int r1, int& a0, int& a1, int& b0, int& b1) {
-  const double hw_ = (double)(p.W / 2), hh = (double)(p.H / 2);
+  const double hh = (double)(p.H / 2);
   auto cols = [&](double a, double b, int& c0, int& c1) {  // k in [a, b] -> columns
-    c0 = (int)fmin(fmax(0.0, ceil(hw_ - b)), (double)p.W);  // clamped before the conversion
-    c1 = (int)fmax(fmin((double)(p.W - 1), floor(hw_ - a + 0.5)), -1.0);
+    pixel_range(p, a, b, c0, c1, false);
   };
   // k-range of a band |b0 + b1 k + b2 l| <= hw for some l in [la, lb]
   auto band = [&](double hw, double la, double lb, double& a, double& b) {
@@ -526,7 +537,8 @@ __host__ __device__ inline void row_tiles(const CandParams& p, const Footprint& 
     }
   };
   const int ra = ty * 8 > r0 ? ty * 8 : r0, rb = ty * 8 + 7 < r1 ? ty * 8 + 7 : r1;
-  const double la = hh - rb, lb = hh - ra + 0.5;  // l-range of the strip's samples
+  // l-range of the strip's samples
+  const double la = p.compat ? ra - hh : hh - rb, lb = p.compat ? rb - hh : hh - ra + 0.5;
   double a = -1e300, b = 1e300;
   if (fp.tri_ok) {  // the projected T_D cut to the (widened) strip
     const double la2 = la - fp.dimg, lb2 = lb + fp.dimg;

@@ -55,7 +55,8 @@ extern "C" {
 // counters 128 B apart, the stats, RT_HIT_REGIONS hit-record and as many
 // shade-chunk counters 32 words apart
 static constexpr size_t kItemCounterBytes = 8 * 128;
-static constexpr size_t kStatBytes = (RT_NSTATS * sizeof(unsigned long long) + 255) / 256 * 256;
+static_assert(RT_NSTATS <= RT_STAT_STRIDE, "stat copies overlap");
+static constexpr size_t kStatBytes = RT_STAT_SETS * RT_STAT_STRIDE * sizeof(unsigned long long);
 static constexpr size_t kHitCounterBytes = 2 * RT_HIT_REGIONS * 32 * sizeof(uint32_t);
 static constexpr size_t kFrameCounterBytes = kItemCounterBytes + kStatBytes + kHitCounterBytes;
 
@@ -157,7 +158,7 @@ struct rt_hip_ctx {
 };
 
 static int cand_params(const rt_frame* f, const float scene_c[3], float scene_r, float eps_ulps,
-                       double bound_scale, int rank, int nranks, CandParams* out);
+                       double bound_scale, int rank, int nranks, CandParams* out, int compat = 0);
 
 static int tiles_x_of(int W) { return (W + 7) / 8; }
 static int tiles_y_of(int H) { return (H + 7) / 8; }
@@ -755,7 +756,9 @@ extern "C" int rt_cand_survey(const rt_scene* scene, float eps_ulps, double boun
   return rc;
 }
 
-static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream_t s);
+static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream_t s, int compat = 0);
+
+static int cand_verify(rt_hip_ctx* c, const rt_frame* f, KParams kp, int compat, unsigned long long out[7]);
 
 extern "C" int rt_hip_cand_verify(rt_hip_ctx* c, const rt_frame* f, int rank, int nranks,
                                   unsigned long long out[7]) {
@@ -764,21 +767,45 @@ extern "C" int rt_hip_cand_verify(rt_hip_ctx* c, const rt_frame* f, int rank, in
     return rt_set_error(RT_EINVAL, "no candidate lists (render a frame with exact camera rays first)");
   if (c->last_p.rank != rank || c->last_p.nranks != nranks)
     return rt_set_error(RT_EINVAL, "the last render was rank %d of %d", c->last_p.rank, c->last_p.nranks);
+  return cand_verify(c, f, c->last_p, 0, out);
+}
+
+// The same for the compatibility mode's lists (rt_hip_render_compat): the
+// camera's 3x frame, one sample per pixel (CandParams::compat), one rank.
+extern "C" int rt_hip_cand_verify_compat(rt_hip_ctx* c, const rt_camera* cam, unsigned long long out[7]) {
+  if (!c || !cam || !out) return rt_set_error(RT_EINVAL, "null argument");
+  if (!c->d_cand_start || !c->d_cand || !c->d_cand_list)
+    return rt_set_error(RT_EINVAL, "no candidate lists (render a frame with exact camera rays first)");
+  rt_camera big = *cam;
+  big.width = 3 * cam->width;
+  big.height = 3 * cam->height;
+  rt_frame f;
+  int rc = rt_frame_from_camera(&big, &f);
+  if (rc) return rc;
+  KParams kp;
+  std::memset(&kp, 0, sizeof kp);
+  kp.rank = 0;
+  kp.nranks = 1;
+  kp.ntiles_local = tiles_x_of(big.width) * tiles_y_of(big.height);
+  return cand_verify(c, &f, kp, 1, out);
+}
+
+static int cand_verify(rt_hip_ctx* c, const rt_frame* f, KParams kp, int compat, unsigned long long out[7]) {
+  const int rank = kp.rank, nranks = kp.nranks;
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = c->last_stream ? c->last_stream : c->stream;
   HIP_TRY(hipStreamSynchronize(s));
   // the render keeps only the big footprints: build the frame's lists again
   // (deterministic: the same entries at the same places) keeping every one
   {
-    KParams kp = c->last_p;
     c->cand_store_fp = 1;
-    const int rp = cand_prepare(c, f, &kp, s);
+    const int rp = cand_prepare(c, f, &kp, s, compat);
     c->cand_store_fp = 0;
     if (rp) return rp;
     HIP_TRY(hipStreamSynchronize(s));
   }
   CandParams cp;
-  int rc = cand_params(f, c->scene_c, c->scene_r, c->cam_eps_ulps, c->bound_scale, rank, nranks, &cp);
+  int rc = cand_params(f, c->scene_c, c->scene_r, c->cam_eps_ulps, c->bound_scale, rank, nranks, &cp, compat);
   if (rc) return rc;
   cp.nprim = c->nprim;
   const uint32_t nt = (uint32_t)cp.ntiles_local;
@@ -940,7 +967,7 @@ extern "C" int rt_hip_set_cand_item_cap(rt_hip_ctx* c, unsigned cap) {
 
 // Frame constants of the candidate lists for rank/nranks (no device work).
 static int cand_params(const rt_frame* f, const float scene_c[3], float scene_r, float eps_ulps,
-                       double bound_scale, int rank, int nranks, CandParams* out) {
+                       double bound_scale, int rank, int nranks, CandParams* out, int compat) {
   const double eps = 0x1p-24;
   CandParams& cp = *out;
   std::memset(&cp, 0, sizeof cp);
@@ -967,11 +994,21 @@ static int cand_params(const rt_frame* f, const float scene_c[3], float scene_r,
   cp.ginv[2] = g00 / det;
   cp.gscale = std::sqrt(cp.ginv[0] * cp.ginv[0] + 2 * cp.ginv[1] * cp.ginv[1] + cp.ginv[2] * cp.ginv[2]);
   const int W = f->width, H = f->height;
-  // samples: k = i + {0, 1/2}, i in [1 - W/2, W/2] (cpu/raytracer.c:50-58)
-  cp.kmin = 1.0 - W / 2;
-  cp.kmax = W / 2 + 0.5;
-  cp.lmin = 1.0 - H / 2;
-  cp.lmax_ = H / 2 + 0.5;
+  cp.compat = compat;
+  if (compat) {
+    // gpu/rt: one sample per pixel of the 3x frame, k = px - W/2, px in
+    // [0, W - 1] (gpu/raytracer.cu:97-103), likewise l
+    cp.kmin = -(double)(W / 2);
+    cp.kmax = (double)(W - 1 - W / 2);
+    cp.lmin = -(double)(H / 2);
+    cp.lmax_ = (double)(H - 1 - H / 2);
+  } else {
+    // samples: k = i + {0, 1/2}, i in [1 - W/2, W/2] (cpu/raytracer.c:50-58)
+    cp.kmin = 1.0 - W / 2;
+    cp.kmax = W / 2 + 0.5;
+    cp.lmin = 1.0 - H / 2;
+    cp.lmax_ = H / 2 + 0.5;
+  }
   double lmax = 0, omax = 0;
   for (int ci = 0; ci < 4; ci++) {  // |o - pos| and |o| are convex: corners bound them
     const double k = (ci & 1) ? cp.kmax : cp.kmin, l = (ci & 2) ? cp.lmax_ : cp.lmin;
@@ -1040,10 +1077,10 @@ static int ensure_tmp(rt_hip_ctx* c, size_t bytes) {
 // count -> scan -> (read back the entry total: the only host sync) -> emit
 // -> radix sort by tile -> per-tile offsets.  No contended atomics; the list
 // order is deterministic.
-static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream_t s) {
+static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream_t s, int compat) {
   CandParams cp;
   int rc = cand_params(f, c->scene_c, c->scene_r, c->cam_eps_ulps, c->bound_scale, kp->rank, kp->nranks,
-                       &cp);
+                       &cp, compat);
   if (rc) return rc;
   cp.tri = c->d_tri_prim;
   cp.nprim = c->nprim;
@@ -1382,7 +1419,17 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
       if (c->light_type[li] == 1 || c->light_type[li] == 2) all = c->lb_dev[li] != nullptr;
     if (all) spol = RT_POLICY_LBUF;
   }
-  const int gt = empty ? c->grid : c->grid_of[1][pol][cw], gs = empty ? c->grid : c->grid_of[0][spol][cw];
+  int gt = empty ? c->grid : c->grid_of[1][pol][cw], gs = empty ? c->grid : c->grid_of[0][spol][cw];
+  // small frames: no more persistent waves than work items (every wave pulls
+  // items until all 8 streams drain, so any grid covers the frame; the
+  // surplus waves of a full grid only cost dispatch on a frame of a few
+  // thousand items -- C1 has 4,096).  The shade kernel's records are not
+  // known before the trace, at least one 64-record chunk per item is assumed
+  {
+    const long long items = 4ll * p.ntiles_local;
+    if (items < gt) gt = (int)items;
+    if (items < gs) gs = (int)items;
+  }
   // every device pointer the kernels will follow must exist (a null one
   // would fault the card, not fail the call)
   if (!p.tri_prim && (p.lbuf || p.n_sh_global || p.cand_start))
@@ -1441,7 +1488,7 @@ extern "C" int rt_hip_verify_shadows_from(rt_hip_ctx* c, unsigned stride, unsign
       hipMalloc((void**)&lit[1], n * sizeof(uint32_t)) != hipSuccess ||
       hipMalloc((void**)&term, n * sizeof(float4)) != hipSuccess ||
       hipMalloc((void**)&ctr, RT_HIT_REGIONS * 32 * sizeof(uint32_t)) != hipSuccess ||
-      hipMalloc((void**)&st, RT_NSTATS * sizeof(unsigned long long)) != hipSuccess) {
+      hipMalloc((void**)&st, kStatBytes) != hipSuccess) {
     rc = rt_set_error(RT_EHIP, "hipMalloc shadow verification buffers");
     goto done;
   }
@@ -1555,12 +1602,16 @@ extern "C" int rt_hip_probe_shadows(rt_hip_ctx* c, unsigned light, const float* 
 extern "C" int rt_hip_stats(rt_hip_ctx* c, rt_stats* out) {
   if (!c || !out) return rt_set_error(RT_EINVAL, "null argument");
   HIP_TRY(hipSetDevice(c->device));
-  unsigned long long h[RT_NSTATS];
+  unsigned long long hs[RT_STAT_SETS * RT_STAT_STRIDE], h[RT_NSTATS];
   uint32_t hc[RT_HIT_REGIONS * 32];
   hipStream_t s = c->last_stream ? c->last_stream : c->stream;
-  HIP_TRY(hipMemcpyAsync(h, c->d_stats, sizeof h, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(hs, c->d_stats, sizeof hs, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(hc, c->d_hit_count, sizeof hc, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  for (int k = 0; k < RT_NSTATS; k++) {  // the copies of each counter (RT_STAT_SETS)
+    h[k] = 0;
+    for (int set = 0; set < RT_STAT_SETS; set++) h[k] += hs[set * RT_STAT_STRIDE + k];
+  }
   size_t need = 0;
   unsigned long long records = 0;
   for (int x = 0; x < RT_HIT_REGIONS; x++) {
@@ -1748,6 +1799,17 @@ extern "C" int rt_hip_render_compat(rt_hip_ctx* c, const rt_camera* cam, unsigne
     p.sh_omax = c->sh_omax;
   }
   p.tri_prim = c->d_tri_prim;
+  // exact camera rays in this mode too: the candidate lists of the 3x frame's
+  // one-sample-per-pixel camera (csrc/rt_cand.hip CandParams::compat)
+  c->cand_prims = c->cand_entries = c->cand_global = 0;
+  if (c->accel == RT_ACCEL_OCTREE && c->d_node && c->exact_camera) {
+    rc = cand_prepare(c, &f, &p, s, 1);
+    if (rc) {
+      (void)hipFree(d_hi);
+      (void)hipFree(d_lo);
+      return rc;
+    }
+  }
   if (hipMemsetAsync(c->d_counter, 0, kFrameCounterBytes, s) != hipSuccess ||
       rt_launch_compat(&p, accel, c->grid, s) != hipSuccess ||
       rt_launch_downscale(d_hi, d_lo, cam->width, cam->height, s) != hipSuccess ||

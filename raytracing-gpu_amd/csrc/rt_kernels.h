@@ -17,6 +17,13 @@
 // unbounded for mirrors of Nr >= 1; paths of Nr < 1 end long before this
 #define RT_MAX_BOUNCES 16384
 #define RT_NSTATS 22
+// the counters are kept in RT_STAT_SETS copies RT_STAT_STRIDE words apart,
+// wave b adding to copy b % 8 (its XCD's): every wave of a launch flushes
+// its counters with a few 64-bit atomics, and on a small frame (C1: 4,096
+// waves of one work item each) one copy queued them for most of the kernel;
+// rt_hip_stats sums the copies
+#define RT_STAT_SETS 8
+#define RT_STAT_STRIDE 32
 // per-lane global overflow area of the traversal stack (entries beyond LDS)
 #define RT_SPILL_STACK 112
 // hit records (the wavefront split, rt_render.hip): 8 regions, one per

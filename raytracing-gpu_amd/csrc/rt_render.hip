@@ -1381,7 +1381,8 @@ __device__ __forceinline__ void flush_counts(const KParams& p, const WorkCount& 
                            shade ? wc.nodes : 0u, shade ? wc.tris : 0u, wc.sh_unproven};
 #pragma unroll
   for (int k = 0; k < RT_NSTATS; k++)
-    if (lane == 0 && v[k]) atomicAdd(p.stats + k, (unsigned long long)v[k]);
+    if (lane == 0 && v[k])
+      atomicAdd(p.stats + (size_t)(blockIdx.x % RT_STAT_SETS) * RT_STAT_STRIDE + k, (unsigned long long)v[k]);
 }
 
 // ---------------------------------------------------------- wavefront split
@@ -1541,12 +1542,21 @@ __global__ __launch_bounds__(64, RT_TRACE_MIN_WAVES) void trace_kernel(KParams p
   const uint32_t nt = (uint32_t)p.ntiles_local;
   const uint32_t home = (uint32_t)blockIdx.x & 7u;
   uint32_t probe = 0;
+  bool first = true;
   for (;;) {
     const uint32_t x = (home + probe) & 7u;
     const uint32_t nx = nt > x ? (nt - x + 7u) / 8u : 0u;  // tiles of stream x
+    // the first (gridDim.x - x + 7) / 8 items of stream x go one to each of
+    // its home waves without an atomic (a small frame's few thousand waves
+    // would otherwise queue on 8 counters), the rest through its counter
     uint32_t q = 0;
-    if (lane == 0) q = atomicAdd(p.tile_counter + 32u * x, 1u);
-    q = uni(q);
+    if (first) {
+      q = (uint32_t)blockIdx.x >> 3;
+      first = false;
+    } else {
+      if (lane == 0) q = atomicAdd(p.tile_counter + 32u * x, 1u);
+      q = uni(q) + (gridDim.x - x + 7u) / 8u;
+    }
     if (q >= 4u * nx) {
       if (++probe == 8u) break;  // every stream drained: the wave exits
       continue;
@@ -1673,6 +1683,7 @@ __global__ __launch_bounds__(64, ACCEL == RT_ACCEL_FLAT_D ? RT_FLAT_SHADE_MIN_WA
   w.lane = lane;
   const uint32_t home = (uint32_t)blockIdx.x & 7u;
   uint32_t probe = 0;
+  bool first_chunk = true;
   for (;;) {
     const uint32_t x = (home + probe) & 7u;
     const uint32_t hc = p.hit_count[32u * x];
@@ -1680,9 +1691,15 @@ __global__ __launch_bounds__(64, ACCEL == RT_ACCEL_FLAT_D ? RT_FLAT_SHADE_MIN_WA
     const uint32_t stride = p.shade_stride > 1u ? p.shade_stride : 1u;  // verification only
     const uint32_t first = p.shade_first;
     const uint32_t ns = n > first ? (n - first + stride - 1u) / stride : 0u;  // records shaded
+    // first chunk of each home wave without an atomic (as trace_kernel)
     uint32_t q = 0;
-    if (lane == 0) q = atomicAdd(p.shade_counter + 32u * x, 1u);
-    q = uni(q);
+    if (first_chunk) {
+      q = (uint32_t)blockIdx.x >> 3;
+      first_chunk = false;
+    } else {
+      if (lane == 0) q = atomicAdd(p.shade_counter + 32u * x, 1u);
+      q = uni(q) + (gridDim.x - x + 7u) / 8u;
+    }
     if (q >= (ns + 63u) / 64u) {
       if (++probe == 8u) break;
       continue;
@@ -1971,6 +1988,9 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES) void compat_kernel(KParams p) {
       b.u = b.v = 0.0f;
       b.t = 0.0f;
       closest_q<ACCEL, false, POL>(p, r, alive, depth, b, stk, w, wc);
+      // the camera rays' candidate lists (rt_hip_render_compat builds them for
+      // this frame's sample model): the same exactness as cpu mode
+      if (ACCEL != RT_ACCEL_FLAT_D && depth == 0) cand_closest<false>(p, r, alive, t, b, w, wc);
       bool hit = alive && b.dist != __builtin_inff();
       f3 N = f3{0.0f, 0.0f, 0.0f};
       wc.hits += (uint32_t)__popcll(__ballot(hit));

@@ -152,6 +152,7 @@ _PROTOS = [
     ("rt_hip_set_cull_slack", C.c_int, [C.c_void_p, C.c_float]),
     ("rt_hip_set_camera_slack", C.c_int, [C.c_void_p, C.c_float]),
     ("rt_hip_cand_verify", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
+    ("rt_hip_cand_verify_compat", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     ("rt_hip_cand_tile_entries", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
     ("rt_hip_set_cand_item_cap", C.c_int, [C.c_void_p, C.c_uint]),
     ("rt_hip_verify_shadows", C.c_int, [C.c_void_p, C.c_uint, C.POINTER(C.c_ulonglong)]),
@@ -504,6 +505,13 @@ class Context:
         return dict(zip(("listed", "entries", "fp_mismatch", "tile_mismatch", "global",
                          "filter_violation", "filtered"), (int(x) for x in out)))
 
+    def cand_verify_compat(self, camera):
+        """cand_verify for the last rt_hip_render_compat of `camera`."""
+        out = (C.c_ulonglong * 7)()
+        _check(lib().rt_hip_cand_verify_compat(self.h, C.byref(camera), out), "cand_verify_compat")
+        return dict(zip(("listed", "entries", "fp_mismatch", "tile_mismatch", "global",
+                         "filter_violation", "filtered"), (int(x) for x in out)))
+
     def verify_shadows(self, stride=1, first=0):
         """Shadow outcomes of the last render's hit records (every stride-th
         per region, from the first-th): the walk vs brute force
@@ -558,8 +566,8 @@ class Context:
         st = Stats()
         cam = Camera()
         C.pointer(cam)[0] = camera
-        _check(lib().rt_hip_render_compat(self.h, C.byref(cam), img.ctypes.data_as(C.c_void_p),
-                                          C.byref(st)), "rt_hip_render_compat")
+        self._check_render(lib().rt_hip_render_compat(self.h, C.byref(cam), img.ctypes.data_as(C.c_void_p),
+                                                      C.byref(st)), "rt_hip_render_compat")
         return img, st.as_dict()
 
     def close(self):
