@@ -196,7 +196,7 @@ def main():
                          "default 0)")
     ap.add_argument("--exact-shadows", type=int, default=None, choices=[0, 1],
                     help="shadow queries through proven (1) or slack-grown (0) light buffers "
-                         "(rt_hip_set_exact_shadows; default = library default)")
+                         "(rt_hip_set_exact_shadows; default = library default, proven)")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary (tools/pmc_traffic.py) to report as roofline.traffic")
     ap.add_argument("--valu-json", default=None,
@@ -450,6 +450,12 @@ def main():
                                 "light_buffer_seconds": round(info["lightbuf_seconds"], 3)},
                 "parallelism": f"image tiles over {world} GPU(s) + RCCL gather" if world > 1
                                else "1 GPU",
+                # camera rays: candidate lists; shadow rays: proven light buffers
+                # (the library default) or slack-grown ones (--exact-shadows 0)
+                "exactness": {"camera_rays": "proven (candidate lists)",
+                              "shadow_rays": ("measured (slack-grown light buffers)"
+                                              if args.exact_shadows == 0 else
+                                              "proven (light buffers + off-box brute force)")},
                 "queries_per_frame": {"closest": int(closest), "shadow": int(shadow),
                                       "closest_hits": int(hits), "pixels": int(pixels)},
             },

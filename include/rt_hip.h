@@ -121,8 +121,8 @@ typedef struct rt_accel_info {
   unsigned long long lightbuf_never;
   unsigned long long lightbuf_band;
   /* lights whose buffer could not be built (too many entries, out of device
-   * memory): their shadow queries walk the octree instead (default mode; the
-   * exact-shadow mode fails rt_hip_set_exact_shadows / rt_hip_create instead) */
+   * memory): their shadow queries walk the octree instead (the proven walk in
+   * the exact-shadow mode) */
   unsigned long long lightbuf_failed;
 } rt_accel_info;
 
@@ -221,14 +221,19 @@ int rt_hip_tile_phase_cycles(rt_hip_ctx *ctx, int phase, unsigned long long *out
  * (csrc/rt_cand.hip).  0 = octree walk only (A/B timing; rt_hip_stats then
  * returns RT_EINEXACT: cpu/rt parity is not guaranteed for grazing camera rays). */
 int rt_hip_set_exact_camera(rt_hip_ctx *ctx, int enable);
-/* Proven shadow rays (default 0): the shadow walk grows each node's box by
- * a per-node multiple of the culling slack that covers the float
- * Moller-Trumbore error region of every triangle below it for every shadow
- * ray of the scene's lights, plus a global list (csrc/rt_shadow.hip,
- * DESIGN.md §2).  Exact by construction but, near the terminators where
- * shadow rays graze the surfaces, the bound grows like 1/cos: on C5 it
- * costs ~160x the shade time.  Default: the plain slack, whose shadow
- * decisions are verified against brute force (rt_hip_verify_shadows). */
+/* Shadow rays exact by proof (default 1; rt_hip_set_exact_shadows rebuilds
+ * the buffers now).  Each light buffer lists a triangle in every cell from
+ * which some shadow ray can make the float Moller-Trumbore test accept it
+ * (proven footprints, csrc/rt_lightbuf.hip); a query whose origin lies off the
+ * proof's box (a float garbage hit far past a triangle) is deferred and
+ * decided by brute force over every record after the shade pass (lights
+ * 0..31; with more lights it is counted -> RT_EINEXACT).  Queries that walk
+ * the octree (staged policies, light buffers off, a failed buffer, the
+ * compatibility mode) use the proven walk: each node's box grown by a
+ * per-node multiple of the culling slack covering every triangle below it,
+ * plus a global list (csrc/rt_shadow.hip).  0: slack-grown
+ * buffers and the plain-slack walk, whose decisions are measured against
+ * brute force (rt_hip_verify_shadows), not proven; ~0.26 ms faster on C5. */
 /* Light buffers for the shadow queries of the default walk (1, the default):
  * per directional / point light a grid over the light's view whose cells list
  * the triangles a shadow ray starting there can meet (csrc/rt_lightbuf.hip),

@@ -114,7 +114,9 @@ struct rt_hip_ctx {
   float sh_ulps = -1.0f;
   float sh_omax = 0.0f;
   float sh_mu_max = 1.0f;
-  int exact_shadows = 0;  // opt-in: the proven shadow walk (rt_hip_set_exact_shadows)
+  // shadow rays exact by proof (rt_hip_set_exact_shadows, default on): proven
+  // light buffers, the per-node multiplier walk where a light has none
+  int exact_shadows = 1;
   size_t tile_cycles_cap = 0, tile_cycles_n = 0;
   // exact camera rays (csrc/rt_cand.hip)
   int exact_camera = 1;
@@ -399,14 +401,10 @@ static int lbuf_prepare(rt_hip_ctx* c, hipStream_t s) {
     lp.tri = c->d_tri_prim;
     lp.max_entries = c->lb_entry_cap;
     if (rt_lightbuf_build(&lp, &hb[li], &c->lb_dev[li], s, err, sizeof err)) {
-      // the proven mode's exactness needs every buffer (its walk fallback is
-      // the per-node multiplier walk, not built alongside); otherwise the
-      // light's queries walk the octree (hb[li] is zeroed: RT_LB_NONE), as
-      // they did before light buffers -- a scene that fits the walk still loads
-      if (c->exact_shadows) {
-        lbuf_release(c);
-        return rt_set_error(RT_EHIP, "light buffer of light %u: %s", li, err);
-      }
+      // the light's queries walk the octree instead (hb[li] is zeroed:
+      // RT_LB_NONE), as they did before light buffers -- a scene that fits the
+      // walk still loads; in the exact-shadow mode that walk is the proven
+      // per-node multiplier walk (shadow_prepare, built by the render)
       std::memset(&hb[li], 0, sizeof hb[li]);
       c->lb_dev[li] = nullptr;
       (void)hipGetLastError();  // an out-of-memory hipMalloc is not sticky; clear it anyway
@@ -1367,15 +1365,17 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
     p.tile_cycles = c->d_tile_cycles;
   }
   {
-    int rc = shadow_prepare(c, s);  // no-op unless the culling slack changed
-    if (rc) return rc;
-  }
-  {
     // light buffers, proven in exact-shadow mode (no-op unless the slack or
     // the mode changed); the staged policies walk
     int rc = lbuf_prepare(c, s);
     if (rc) return rc;
     if (c->policy == RT_POLICY_DEFAULT || c->policy == RT_POLICY_LANE) p.lbuf = c->d_lbuf;
+  }
+  // the proven walk's multipliers: only where some light's queries walk
+  const bool walks = !p.lbuf || c->info.lightbuf_failed;
+  if (walks) {
+    int rc = shadow_prepare(c, s);  // no-op unless the culling slack changed
+    if (rc) return rc;
   }
   // proven buffers: the off-box queries' queue.  An entry carries the
   // decided bits of lights 0..31 only, so with more lights the off-box
@@ -1391,7 +1391,7 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
     p.oob_cap = RT_OOB_CAP;
     HIP_TRY(hipMemsetAsync(c->d_oob_count, 0, sizeof(uint32_t), s));
   }
-  if (c->exact_shadows && !p.lbuf) {  // the proven walk
+  if (c->exact_shadows && walks) {  // the proven walk
     p.node_mu = c->d_node_mu;
     p.sh_global = c->d_sh_global;
     p.n_sh_global = c->n_sh_global;

@@ -1148,10 +1148,11 @@ __device__ __forceinline__ bool shadow_q(const KParams& p, f3 o, f3 d, uint32_t 
   }
   bool staged = POL == RT_POLICY_STAGED ||
                 (POL == RT_POLICY_DIR_STAGED && type == 1 && __popcll(am) >= kPacketMin);
-  bool hit;
+  bool hit, walked = true;
   if (staged) {
     hit = staged_any<COUNT>(p, r, act, w, wc);
   } else if (p.lbuf && p.lbuf[li].kind != RT_LB_NONE) {
+    walked = false;
     const RtLightBuf& L = p.lbuf[li];
     LaneCount lc = {0, 0, 0, 0, 0, 0, 0};
     hit = act && (pre ? lbuf_scan<COUNT>(p, L, r, *pre, lc) : lbuf_any<COUNT>(p, L, r, lc));
@@ -1176,8 +1177,9 @@ __device__ __forceinline__ bool shadow_q(const KParams& p, f3 o, f3 d, uint32_t 
     absorb<COUNT>(wc, lc, true);
   }
   // the prims whose float error region no slack multiplier bounds
-  // (csrc/rt_shadow.hip): tested by every ray the walk found unshadowed
-  if (p.n_sh_global && __ballot(act && !hit)) {
+  // (csrc/rt_shadow.hip): tested by every ray the walk found unshadowed (a
+  // light buffer's proof covers its light's queries without them)
+  if (walked && p.n_sh_global && __ballot(act && !hit)) {
     uint32_t risk = 0;
     for (uint32_t k = 0; k < p.n_sh_global; k++) {
       const float4* q = p.tri_prim + 3 * (size_t)uni(p.sh_global[k]);
@@ -1189,7 +1191,7 @@ __device__ __forceinline__ bool shadow_q(const KParams& p, f3 o, f3 d, uint32_t 
   }
   // point lights (exact-shadow mode): the cosine bound assumed origins within
   // sh_omax of the scene centre
-  if (type == 2 && p.node_mu) {
+  if (walked && type == 2 && p.node_mu) {
     const float m = fmaxf(fabsf(o.x - p.scene_c.x), fmaxf(fabsf(o.y - p.scene_c.y), fabsf(o.z - p.scene_c.z)));
     wc.sh_unproven += (uint32_t)__popcll(__ballot(act && !(m <= p.sh_omax)));
   }

@@ -479,7 +479,9 @@ class Context:
         return out.astype(bool)
 
     def set_exact_shadows(self, on=True):
-        """Proven shadow walk (rt_hip_set_exact_shadows; slow near terminators)."""
+        """Shadow rays exact by proof (rt_hip_set_exact_shadows; default on):
+        proven light buffers, the proven walk where a light's queries walk.
+        Off: slack-grown buffers, measured against brute force, not proven."""
         _check(lib().rt_hip_set_exact_shadows(self.h, 1 if on else 0), "exact_shadows")
 
     def set_policy(self, policy):

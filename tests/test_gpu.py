@@ -373,8 +373,8 @@ def test_shadow_queries_match_brute_force(gpu, accel, policy, exact, lbuf):
         assert ctx.info()["lightbuf_entries"] > 0
     ctx.set_light_buffers(lbuf)
     ctx.set_policy(policy)
+    ctx.set_exact_shadows(exact)  # the default is on
     if exact:  # proven light buffers, or (staged policies) the proven walk
-        ctx.set_exact_shadows(True)
         assert ctx.info()["shadow_mu_max"] >= 1.0
         if lbuf:
             assert ctx.info()["lightbuf_entries"] > 0
@@ -394,8 +394,7 @@ def test_no_camera_lists_with_light_buffers(gpu, exact_shadows):
     s = gpu.Scene.synthetic(3, 3, 9776, seed=0x5EED, width=320, height=180)
     f = s.frame()
     ctx = gpu.Context(s, "octree_gpu")
-    if exact_shadows:
-        ctx.set_exact_shadows(True)
+    ctx.set_exact_shadows(exact_shadows)
     img, _ = ctx.render_image(f)
     ctx.set_exact_camera(False)
     img_nc, _ = ctx.render_image(f)
@@ -417,8 +416,7 @@ def test_light_buffer_point_light_near_surface(gpu, height, exact):
     L.v.x, L.v.y, L.v.z = float(top[k, 0]), float(top[k, 1]) + height, float(top[k, 2])
     f = s.frame()
     ctx = gpu.Context(s, "octree_gpu")
-    if exact:  # proven footprints (a light on the sphere: its tangent plane)
-        ctx.set_exact_shadows(True)
+    ctx.set_exact_shadows(exact)  # proven footprints (a light on the sphere: its tangent plane)
     img, _ = ctx.render_image(f)
     v = ctx.verify_shadows(1)
     assert v["records"] > 10000 and v["records_differ"] == 0 and v["walk_lit_brute_shadowed"] == 0, v
@@ -663,14 +661,17 @@ def test_empty_rank_on_fresh_context(gpu, scene_dir, manifest):
     assert tot == case["closest"]
 
 
-def test_light_buffer_build_failure_falls_back_to_walk(gpu):
+@pytest.mark.parametrize("exact", [False, True])
+def test_light_buffer_build_failure_falls_back_to_walk(gpu, exact):
     """A light buffer that cannot be built (here: capped at one entry by the
     test hook) leaves that light's shadow queries on the octree walk instead
-    of failing the context; the image is unchanged.  The exact-shadow mode,
-    whose proof needs the buffers, fails loudly instead."""
+    of failing the context -- the proven walk in the exact-shadow mode (the
+    default); the image is unchanged and equals brute force."""
     s = gpu.Scene.synthetic(3, 3, 9776, seed=0x5EED, width=320, height=180)
     f = s.frame()
+    img_f, st_f = gpu.Context(s, "flat").render_image(f)
     ctx = gpu.Context(s, "octree_gpu")
+    ctx.set_exact_shadows(exact)
     img, st = ctx.render_image(f)
     assert ctx.info()["lightbuf_failed"] == 0 and ctx.info()["lightbuf_entries"] > 0
     ctx.set_lightbuf_entry_cap(1)
@@ -678,8 +679,9 @@ def test_light_buffer_build_failure_falls_back_to_walk(gpu):
     img2, st2 = ctx.render_image(f)
     assert_bitexact(img2, img, "shadow queries on the walk after a failed light-buffer build")
     assert (st2["closest"], st2["shadow"]) == (st["closest"], st["shadow"])
-    with pytest.raises(gpu.RtError):
-        ctx.set_exact_shadows(True)
+    assert_bitexact(img2, img_f, "walk fallback vs brute force")
+    if exact:
+        assert ctx.info()["shadow_mu_max"] >= 1.0  # the proven walk's multipliers were built
 
 
 def test_exact_shadows_more_than_32_lights(gpu, tmp_path):
