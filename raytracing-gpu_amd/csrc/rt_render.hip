@@ -181,6 +181,48 @@ __device__ __forceinline__ void consider_exact(const Ray& r, const float4& q0, c
   }
 }
 
+// consider() for wave-converged loops over LDS-broadcast records (the packet
+// walk's leaves, the candidate lists): the same prefilter decisions, but one
+// wave-uniform exit after the u stage instead of a divergent branch per
+// stage.  Each divergent stage cost an exec save / branch / restore of scalar
+// instructions per record -- as many SALU as VALU in those loops
+// (profiles/r04t_c5/pmc_sq.json: 2.13 G SALU to 3.89 G VALU per trace launch);
+// the v and t stages run for the whole wave once any lane passes u (a
+// divergent stage costs the wave the same VALU cycles anyway).  act: the
+// lane's query; the call itself must be wave-uniform.
+#ifndef RT_CONSIDER_W
+#define RT_CONSIDER_W 1
+#endif
+__device__ __forceinline__ void consider_w(const Ray& r, bool act, const float4& q0, const float4& q1,
+                                           const float4& q2, Best& b) {
+#if RT_CONSIDER_W
+  const float m = 1e-5f;  // as mt_candidate
+  const f3 v0{q0.x, q0.y, q0.z}, e1{q0.w, q1.x, q1.y}, e2{q1.z, q1.w, q2.x};
+  const f3 h = cross(r.d, e2);
+  const float a = dot(e1, h);
+  const float rc = __builtin_amdgcn_rcpf(a);
+  const f3 s = sub(r.o, v0);
+  const float u = dot(s, h) * rc;
+  bool c = act && !(a > -kEps && a < kEps) && !(u < -1e-30f || u > 1.0f + m);
+  if (__ballot(c) == 0) return;
+  const f3 q = cross(s, e1);
+  const float v = dot(r.d, q) * rc;
+  const float t = dot(e2, q) * rc;
+  c = c && !(v < -1e-30f || u + v > 1.0f + m) && !(t < kEps * (1.0f - m) || t > b.t_cut);
+  if (c) consider_exact(r, q0, q1, q2, b);
+#else
+  if (act) consider(r, q0, q1, q2, b);
+#endif
+}
+
+// Records [0, n) of the LDS stage tested as broadcasts (consider_w).
+// Converged call.  (The next record's reads issued during a test -- the
+// index clamped, no branch -- measured slower: trace 6.05 -> 6.51 ms on C5,
+// profiles/r05q_consider_w/ab_lds_pipe.log; round 1 found the same.)
+__device__ __forceinline__ void stage_test(const Ray& r, bool act, uint32_t n, Best& b, const float4* stage) {
+  for (uint32_t k = 0; k < n; k++) consider_w(r, act, stage[3 * k], stage[3 * k + 1], stage[3 * k + 2], b);
+}
+
 // Any hit with new_dist > 0.01 (cpu/hit.c:93-109: collide_dist > 0 <=>
 // shadowed, cpu/light.c:24-31).  Early exit is exact for an object none of
 // whose triangles can interpolate an exactly zero normal (record flag bit 0,
@@ -884,10 +926,7 @@ __device__ void staged_closest(const KParams& p, const Ray& r, bool act, Best& b
       for (uint32_t base = 0; base < cnt; base += kOctRecs) {
         uint32_t m = chunk<kOctRecs>(cnt, base);
         if (base) stage_load(tri + 3 * (size_t)(first + base), 3 * (int)m, w);
-        for (uint32_t k = 0; k < m; k++) {
-          float4 q0 = w.stage[3 * k], q1 = w.stage[3 * k + 1], q2 = w.stage[3 * k + 2];
-          if (want) consider(r, q0, q1, q2, b);
-        }
+        stage_test(r, want, m, b, w.stage);
       }
       limit = rt_prune_limit(b.dist, r.eps);
       if (COUNT) {
@@ -1317,10 +1356,7 @@ __device__ __forceinline__ uint32_t cand_range(const KParams& p, const Ray& r, b
     // do, measured slower here: C5 frame 15.96 -> 16.10 ms,
     // profiles/r03f_bench/ab.log; two per packed-float instruction, RT_CAND_PK
     // of round 3, slower too: profiles/r04e_pk/ab.log)
-    for (uint32_t k = 0; k < n; k++) {
-      float4 q0 = w.stage[3 * k], q1 = w.stage[3 * k + 1], q2 = w.stage[3 * k + 2];
-      if (act) consider(r, q0, q1, q2, b);
-    }
+    stage_test(r, act, n, b, w.stage);
     tested += n;
   }
   return tested;
