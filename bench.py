@@ -19,6 +19,7 @@ Default workload = config C5 (BASELINE.json): the deterministic synthetic
 Prints ONE JSON line on rank 0 (plus progress on stderr).
 """
 import argparse
+import ctypes
 import gzip
 import json
 import os
@@ -197,6 +198,12 @@ def main():
     ap.add_argument("--exact-shadows", type=int, default=None, choices=[0, 1],
                     help="shadow queries through proven (1) or slack-grown (0) light buffers "
                          "(rt_hip_set_exact_shadows; default = library default, proven)")
+    ap.add_argument("--lists", default=None, choices=["rank", "partition"],
+                    help="camera candidate lists of an N-GPU frame: built by every rank for its "
+                         "tiles over all triangles ('rank'), or triangle-parallel -- each rank "
+                         "1/N of the triangles for every rank's tiles, one all-to-all "
+                         "('partition', rt_hip_cand_produce / consume); default: partition "
+                         "when N > 1")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary (tools/pmc_traffic.py) to report as roofline.traffic")
     ap.add_argument("--valu-json", default=None,
@@ -256,7 +263,28 @@ def main():
                 raise
     ctx.set_count_work(False)
 
+    partition = (args.lists or ("partition" if world > 1 else "rank")) == "partition" and \
+        wl["accel"] != "flat"
+    send = [None]
+
+    def exchange_lists():
+        # triangle-parallel lists: this rank's slice of the triangles for
+        # every rank's tiles -> all-to-all over RCCL -> this rank's lists
+        counts, ng = ctx.cand_produce(frame, rank, world, sh)
+        ptr, n = ctx.cand_send_buffer()
+        if send[0] is None or send[0].shape[0] < n:
+            send[0] = torch.empty((n + n // 4 + 1024, 3), dtype=torch.int32, device=dev)
+        rtgpu.lib().rt_hip_memcpy_d2d(ctypes.c_void_p(send[0].data_ptr()), ctypes.c_void_p(ptr), n * 12,
+                                      ctypes.c_void_p(sh))
+        if world > 1:
+            recv, g = rtgpu.exchange_cand_entries(dist, send[0], counts, ng)
+        else:
+            recv, g = send[0][:n], ng
+        ctx.cand_consume(frame, rank, world, recv.data_ptr(), int(recv.shape[0]), g, sh)
+
     def step():
+        if partition:
+            exchange_lists()
         ctx.render(frame, rank, world, tiles.data_ptr(), sh)
         if world > 1:
             dist.gather(tiles, list(gathered.view(world, per)) if rank == 0 else None, dst=0)
@@ -452,6 +480,9 @@ def main():
                                else "1 GPU",
                 # camera rays: candidate lists; shadow rays: proven light buffers
                 # (the library default) or slack-grown ones (--exact-shadows 0)
+                "candidate_lists": ("triangle-parallel: rt_hip_cand_produce over 1/N of the "
+                                    "triangles, RCCL all-to-all, rt_hip_cand_consume" if partition
+                                    else "per rank: every triangle, this rank's tiles"),
                 "exactness": {"camera_rays": "proven (candidate lists)",
                               "shadow_rays": ("measured (slack-grown light buffers)"
                                               if args.exact_shadows == 0 else

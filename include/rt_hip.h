@@ -312,6 +312,33 @@ int rt_hip_cand_tile_entries(rt_hip_ctx *ctx, unsigned int *out, size_t n);
  * one wave per footprint instead (the same lists). */
 int rt_hip_set_cand_item_cap(rt_hip_ctx *ctx, unsigned cap);
 
+/* Triangle-parallel camera candidate lists of an nranks-way frame (new; the
+ * per-rank build of rt_hip_render runs the float fast path, classification
+ * and emission over every triangle on every rank).  Each rank:
+ *   1. rt_hip_cand_produce: the whole frame's list entries of triangles
+ *      [rank P / nranks, (rank + 1) P / nranks), routed to the ranks that own
+ *      their tiles; counts[d] = entries for rank d (global triangles included,
+ *      one entry per rank each), *nglobal = this slice's global triangles.
+ *      Synchronises its stream (the entry total).
+ *   2. rt_hip_cand_send_buffer: the routed entries (device memory of the
+ *      context, 3 x 32-bit words each, destination-rank order: counts[0]
+ *      entries for rank 0, then rank 1's, ...), valid until the next produce.
+ *   3. an all-to-all of those blocks (e.g. RCCL / torch.distributed
+ *      all_to_all_single), every rank receiving its blocks from every rank,
+ *      and the sum of the producers' *nglobal;
+ *   4. rt_hip_cand_consume: this rank's lists from the n received entries
+ *      (any source order); the next rt_hip_render of the same frame, rank and
+ *      nranks uses them instead of building its own (once).
+ * The lists equal the per-rank build's, tile by tile, as multisets (the
+ * render is order-independent: the lexicographic (new_dist, prim) key).
+ * Octree contexts with exact camera rays only (else RT_EINVAL).  stream:
+ * as rt_hip_render. */
+int rt_hip_cand_produce(rt_hip_ctx *ctx, const rt_frame *frame, int rank, int nranks, unsigned *counts,
+                        unsigned *nglobal, void *stream);
+int rt_hip_cand_send_buffer(const rt_hip_ctx *ctx, const void **d_entries, size_t *n);
+int rt_hip_cand_consume(rt_hip_ctx *ctx, const rt_frame *frame, int rank, int nranks, const void *d_entries,
+                        size_t n, unsigned nglobal, void *stream);
+
 /* d_gathered = nranks consecutive tile buffers (rank-major, as an RCCL gather
  * delivers them); writes the PPM-order image (W*H*3 floats) to d_rgb. */
 int rt_hip_assemble(rt_hip_ctx *ctx, const rt_frame *frame, const float *d_gathered, int nranks,
@@ -341,6 +368,8 @@ int rt_hip_malloc(int device, size_t bytes, void **d_ptr);
 int rt_hip_free(void *d_ptr);
 int rt_hip_memcpy_d2h(void *h_dst, const void *d_src, size_t bytes);
 int rt_hip_memcpy_h2d(void *d_dst, const void *h_src, size_t bytes);
+/* device -> device, asynchronous on stream (NULL: the null stream) */
+int rt_hip_memcpy_d2d(void *d_dst, const void *d_src, size_t bytes, void *stream);
 
 /* Drop-in for raytrace() (cpu/raytracer.c:79-136): parse, render on GPU 0,
  * write the P3 PPM.  Returns an RT_E* code instead of exiting. */

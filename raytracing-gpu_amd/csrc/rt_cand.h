@@ -21,6 +21,8 @@ struct CandParams {
   const float4* node;     // octree nodes (2 float4 each: box + words), may be NULL
   const uint32_t* prim_leaf;  // nprim: a leaf holding a record of the prim (NULL: none)
   uint32_t nprim;
+  uint32_t prim0, prim1;  // the prims this build lists: [prim0, prim1) (a slice of a
+                          // triangle-parallel multi-GPU build; else [0, nprim))
   double pos[3];          // eye (camera position)
   double u[3], v[3];      // image-plane axes (normalised camera u, v)
   double C[3];            // image-plane origin
@@ -115,6 +117,27 @@ extern "C" hipError_t rt_cand_entry_skip(const uint32_t* cand, const float* skip
                                          uint32_t n, hipStream_t s);
 extern "C" hipError_t rt_cand_bounds(const uint32_t* keys, uint32_t n, uint32_t* start,
                                      uint32_t ntiles, hipStream_t s);
+// Triangle-parallel multi-GPU lists (rt_hip_cand_produce / rt_hip_cand_consume):
+// a whole-frame build (one rank, scanline tiles) of a slice of the prims, its
+// entries routed to the N-rank tile map.  route: key = scanline tile ->
+// dest_rank * (tpr + 1) + rank-local tile (tpr = tiles per rank); globals:
+// one entry per rank with the local slot tpr.  rank_bounds: start[d] = first
+// entry of rank d in the routed, sorted keys (start[n] = total).  pack: 3
+// words per entry (local tile or tpr, prim, skip bits).  unpack (consumer):
+// keys = local tile (tpr -> ntiles: the globals sort last), idx = i.
+// gather: the sorted entries' prims and skip bounds.
+extern "C" hipError_t rt_cand_route(uint32_t* keys, uint32_t n, int tiles_x, int nranks, int blocks_x, int tb,
+                                    uint32_t tpr, hipStream_t s);
+extern "C" hipError_t rt_cand_route_globals(const uint32_t* global, uint32_t nglobal, int nranks, uint32_t tpr,
+                                            uint32_t* keys, uint32_t* vals, hipStream_t s);
+extern "C" hipError_t rt_cand_rank_bounds(const uint32_t* keys, uint32_t n, uint32_t tpr, int nranks,
+                                          uint32_t* start, hipStream_t s);
+extern "C" hipError_t rt_cand_pack(const uint32_t* keys, const uint32_t* prims, const float* skip, uint32_t n,
+                                   uint32_t tpr, uint32_t* out, hipStream_t s);
+extern "C" hipError_t rt_cand_unpack(const uint32_t* in, uint32_t n, uint32_t ntiles, uint32_t tpr, uint32_t* keys,
+                                     uint32_t* idx, hipStream_t s);
+extern "C" hipError_t rt_cand_gather(const uint32_t* in, const uint32_t* idx, uint32_t n, uint32_t* cand,
+                                     float* skip, hipStream_t s);
 // longest-first work order of the tiles (heavy candidate lists first):
 // perm[position] = tile.  tmp == NULL: *tmp_bytes = the scan's need.
 extern "C" hipError_t rt_cand_order(const uint32_t* start, uint32_t ntiles, uint32_t total,

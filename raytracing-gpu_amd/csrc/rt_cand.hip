@@ -697,7 +697,10 @@ __global__ __launch_bounds__(RT_LIST_BLOCK) void quick_kernel(CandParams p) {
   if (prim < 8u) p.ctr[prim] = 0u;         // the frame's counters (count / big passes, later launches)
   if (prim == 0u) p.visits[p.nprim] = 0u;  // the scan's last input
   if (prim >= p.nprim) return;
-  p.visits[prim] = quick_class(p, (const float*)(p.tri + 3 * (size_t)prim)) == Q_LIST ? 1u : 0u;
+  p.visits[prim] = prim >= p.prim0 && prim < p.prim1 &&
+                           quick_class(p, (const float*)(p.tri + 3 * (size_t)prim)) == Q_LIST
+                       ? 1u
+                       : 0u;
 }
 
 __global__ __launch_bounds__(256) void scatter_kernel(CandParams p) {
@@ -1026,7 +1029,10 @@ __global__ __launch_bounds__(256) void prim_leaf_kernel(const float4* node, uint
   const uint32_t first = __float_as_uint(node[2 * ni].w), info = __float_as_uint(node[2 * ni + 1].w);
   if (!(info & 0x80000000u)) return;  // RT_NODE_LEAF
   const uint32_t cnt = info & 0x7fffffffu;
-  for (uint32_t k = 0; k < cnt; k++) prim_leaf[__float_as_uint(tri[3 * (size_t)(first + k) + 2].y)] = ni;
+  // the smallest leaf index holding the prim (a prim referenced by several
+  // leaves -- the host SAH tree duplicates -- gets the same leaf on every
+  // build, so the lists do not depend on the order of these writes)
+  for (uint32_t k = 0; k < cnt; k++) atomicMin(prim_leaf + __float_as_uint(tri[3 * (size_t)(first + k) + 2].y), ni);
 }
 
 // start[t] = first entry of tile t in the tile-sorted keys; start[n] = total
@@ -1051,6 +1057,75 @@ __global__ __launch_bounds__(256) void entry_skip_kernel(const uint32_t* cand, c
                                                          float* out, uint32_t n) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = skip[cand[i]];
+}
+
+// --- triangle-parallel multi-GPU lists (rt_cand.h "route") ---------------
+// A whole-frame entry (scanline tile of the one-rank map) -> its rank d and
+// rank-local tile l under the N-rank block map: key d (tpr + 1) + l.
+__global__ __launch_bounds__(256) void route_kernel(uint32_t* keys, uint32_t n, int tiles_x, int nranks,
+                                                    int blocks_x, int tb, uint32_t tpr) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t t = keys[i];
+  uint32_t d;
+  const uint32_t l = rt_tile_local((int)(t % (uint32_t)tiles_x), (int)(t / (uint32_t)tiles_x), (uint32_t)nranks,
+                                   (uint32_t)blocks_x, (uint32_t)tb, &d);
+  keys[i] = d * (tpr + 1u) + l;
+}
+
+// the slice's globals: one entry per rank, local slot tpr
+__global__ __launch_bounds__(256) void route_globals_kernel(const uint32_t* global, uint32_t nglobal, int nranks,
+                                                            uint32_t tpr, uint32_t* keys, uint32_t* vals) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nglobal * (uint32_t)nranks) return;
+  const uint32_t d = i / nglobal, g = i % nglobal;
+  keys[i] = d * (tpr + 1u) + tpr;
+  vals[i] = global[g];
+}
+
+// start[d] = first entry of rank d (keys sorted), start[nranks] = n
+__global__ __launch_bounds__(64) void rank_bounds_kernel(const uint32_t* keys, uint32_t n, uint32_t tpr,
+                                                         int nranks, uint32_t* start) {
+  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d > (uint32_t)nranks) return;
+  const uint32_t key = d * (tpr + 1u);
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = lo + (hi - lo) / 2;
+    if (keys[mid] < key)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  start[d] = d == (uint32_t)nranks ? n : lo;
+}
+
+__global__ __launch_bounds__(256) void pack_kernel(const uint32_t* keys, const uint32_t* prims, const float* skip,
+                                                   uint32_t n, uint32_t tpr, uint32_t* out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t prim = prims[i];
+  out[3 * (size_t)i] = keys[i] % (tpr + 1u);
+  out[3 * (size_t)i + 1] = prim;
+  out[3 * (size_t)i + 2] = __float_as_uint(skip[prim]);
+}
+
+__global__ __launch_bounds__(256) void unpack_kernel(const uint32_t* in, uint32_t n, uint32_t ntiles, uint32_t tpr,
+                                                     uint32_t* keys, uint32_t* idx) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t l = in[3 * (size_t)i];
+  keys[i] = l >= tpr ? ntiles : l;  // the globals after every tile
+  idx[i] = i;
+}
+
+__global__ __launch_bounds__(256) void gather_kernel(const uint32_t* in, const uint32_t* idx, uint32_t n,
+                                                     uint32_t* cand, float* skip) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const size_t k = 3 * (size_t)idx[j];
+  cand[j] = in[k + 1];
+  skip[j] = __uint_as_float(in[k + 2]);
 }
 
 // Work order of the trace kernel's tiles (longest processing time first): a
@@ -1488,6 +1563,51 @@ extern "C" hipError_t rt_cand_bounds(const uint32_t* keys, uint32_t n, uint32_t*
   return hipGetLastError();
 }
 
+
+extern "C" hipError_t rt_cand_route(uint32_t* keys, uint32_t n, int tiles_x, int nranks, int blocks_x, int tb,
+                                    uint32_t tpr, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(rtc::route_kernel, dim3((n + 255) / 256), dim3(256), 0, s, keys, n, tiles_x, nranks, blocks_x,
+                     tb, tpr);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t rt_cand_route_globals(const uint32_t* global, uint32_t nglobal, int nranks, uint32_t tpr,
+                                            uint32_t* keys, uint32_t* vals, hipStream_t s) {
+  const uint32_t n = nglobal * (uint32_t)nranks;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(rtc::route_globals_kernel, dim3((n + 255) / 256), dim3(256), 0, s, global, nglobal, nranks,
+                     tpr, keys, vals);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t rt_cand_rank_bounds(const uint32_t* keys, uint32_t n, uint32_t tpr, int nranks,
+                                          uint32_t* start, hipStream_t s) {
+  hipLaunchKernelGGL(rtc::rank_bounds_kernel, dim3((nranks + 1 + 63) / 64), dim3(64), 0, s, keys, n, tpr, nranks,
+                     start);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t rt_cand_pack(const uint32_t* keys, const uint32_t* prims, const float* skip, uint32_t n,
+                                   uint32_t tpr, uint32_t* out, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(rtc::pack_kernel, dim3((n + 255) / 256), dim3(256), 0, s, keys, prims, skip, n, tpr, out);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t rt_cand_unpack(const uint32_t* in, uint32_t n, uint32_t ntiles, uint32_t tpr, uint32_t* keys,
+                                     uint32_t* idx, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(rtc::unpack_kernel, dim3((n + 255) / 256), dim3(256), 0, s, in, n, ntiles, tpr, keys, idx);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t rt_cand_gather(const uint32_t* in, const uint32_t* idx, uint32_t n, uint32_t* cand,
+                                     float* skip, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(rtc::gather_kernel, dim3((n + 255) / 256), dim3(256), 0, s, in, idx, n, cand, skip);
+  return hipGetLastError();
+}
 
 extern "C" hipError_t rt_cand_order(const uint32_t* start, uint32_t ntiles, uint32_t total,
                                     uint32_t* flags, uint32_t* pos, uint32_t* perm, void* tmp,

@@ -151,6 +151,17 @@ struct rt_hip_ctx {
   size_t scan_tmp_bytes = 0;
   uint32_t* h_cand = nullptr;  // pinned: total entries, risky, global, visits
   unsigned long long cand_prims = 0, cand_entries = 0, cand_global = 0;
+  // triangle-parallel lists (rt_hip_cand_produce / rt_hip_cand_consume)
+  uint32_t* d_send = nullptr;   // 3 words per routed entry, destination-rank order
+  size_t send_cap = 0;          // words
+  uint32_t send_n = 0;          // entries of the last produce
+  uint32_t* d_rstart = nullptr;  // nranks + 1 first entries per destination
+  uint32_t* h_rstart = nullptr;  // pinned copy
+  size_t rstart_cap = 0;
+  KParams ext{};                // the consumed lists' kernel parameters
+  int ext_ready = 0, ext_rank = -1, ext_nranks = 0;
+  rt_frame ext_frame{};         // the frame they were built for (compared bytewise)
+  uint32_t ext_total = 0;
   // phase timing (rt_hip_set_timing): per frame, events before the
   // candidate lists, before the render kernel and after it, on the render's
   // stream; a ring of the last RT_TIMED_FRAMES frames
@@ -252,6 +263,9 @@ extern "C" void rt_hip_destroy(rt_hip_ctx* c) {
   (void)hipFree(c->d_order);
   (void)hipFree(c->d_scan_tmp);
   if (c->h_cand) (void)hipHostFree(c->h_cand);
+  (void)hipFree(c->d_send);
+  (void)hipFree(c->d_rstart);
+  if (c->h_rstart) (void)hipHostFree(c->h_rstart);
   for (auto& f : c->ev)
     for (hipEvent_t e : f)
       if (e) (void)hipEventDestroy(e);
@@ -1072,20 +1086,81 @@ static int ensure_tmp(rt_hip_ctx* c, size_t bytes) {
   return RT_OK;
 }
 
-// count -> scan -> (read back the entry total: the only host sync) -> emit
-// -> radix sort by tile -> per-tile offsets.  No contended atomics; the list
-// order is deterministic.
-static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream_t s, int compat) {
-  CandParams cp;
-  int rc = cand_params(f, c->scene_c, c->scene_r, c->cam_eps_ulps, c->bound_scale, kp->rank, kp->nranks,
-                       &cp, compat);
+// The entry buffers (keys, vals, keys2, cand) for n entries.
+static int cand_entry_buffers(rt_hip_ctx* c, size_t n) {
+  if (n + 1 <= c->cand_cap) return RT_OK;
+  for (uint32_t** b : {&c->d_cand_keys, &c->d_cand_vals, &c->d_cand_keys2, &c->d_cand}) {
+    (void)hipFree(*b);
+    *b = nullptr;
+  }
+  c->cand_cap = 0;  // set only once all four entry buffers exist
+  size_t cap = 0;
+  int rc = grow_dev(&c->d_cand_keys, &cap, n + 1);
   if (rc) return rc;
+  for (uint32_t** b : {&c->d_cand_vals, &c->d_cand_keys2, &c->d_cand})
+    HIP_TRY(hipMalloc((void**)b, cap * sizeof(uint32_t)));
+  c->cand_cap = cap;
+  return RT_OK;
+}
+
+// The per-tile offsets and work-order buffers for nt tiles.
+static int cand_tile_buffers(rt_hip_ctx* c, size_t nt) {
+  if (nt + 1 > c->cand_tiles_cap) {
+    size_t cap = c->cand_tiles_cap;
+    int rc = grow_dev(&c->d_cand_start, &cap, nt + 1);
+    if (rc) return rc;
+    c->cand_tiles_cap = cap;
+  }
+  if (nt + 1 > c->order_cap) {
+    (void)hipFree(c->d_order);
+    c->d_order = nullptr;
+    c->order_cap = 0;
+    HIP_TRY(hipMalloc((void**)&c->d_order, 3 * (nt + 1) * sizeof(uint32_t)));
+    c->order_cap = nt + 1;
+  }
+  return RT_OK;
+}
+
+// The longest-first work order of the nt tiles from their offsets, and the
+// lists' kernel parameters common to both builds.
+static int cand_order(rt_hip_ctx* c, KParams* kp, size_t nt, uint32_t total, hipStream_t s) {
+  size_t tb = 0;
+  HIP_TRY(rt_cand_order(c->d_cand_start, (uint32_t)nt, total, c->d_order, c->d_order + nt + 1,
+                        c->d_order + 2 * (nt + 1), nullptr, &tb, s));
+  int rc = ensure_tmp(c, tb);
+  if (rc) return rc;
+  tb = c->scan_tmp_bytes;
+  HIP_TRY(rt_cand_order(c->d_cand_start, (uint32_t)nt, total, c->d_order, c->d_order + nt + 1,
+                        c->d_order + 2 * (nt + 1), c->d_scan_tmp, &tb, s));
+  kp->tile_order = c->d_order + 2 * (nt + 1);
+  kp->cand_start = c->d_cand_start;
+  kp->tri_prim = c->d_tri_prim;
+  return RT_OK;
+}
+
+// Radix sort bits of keys below n_keys.
+static int key_bits(size_t n_keys) {
+  int bits = 1;
+  while ((1ull << bits) < n_keys) bits++;
+  return bits;
+}
+
+// Passes 0-2 of the lists of cp (the prims [cp.prim0, cp.prim1)): the
+// unsorted (tile, prim) entries in d_cand_keys / d_cand_vals, each listed
+// prim's depth-skip bound in d_cand_skip and the global prims in
+// d_cand_global; count -> scan -> (read back the entry total: the build's
+// only host sync) -> emit.  The entry buffers are sized for total +
+// glob_copies x globals (the triangle-parallel build routes each global to
+// every rank).  No contended atomics; deterministic.
+static int cand_build(rt_hip_ctx* c, CandParams& cp, hipStream_t s, uint32_t glob_copies, uint32_t* total_out,
+                      uint32_t* nglobal_out) {
+  int rc = RT_OK;
   cp.tri = c->d_tri_prim;
   cp.nprim = c->nprim;
-  const size_t nt = (size_t)kp->ntiles_local;
   const size_t np = c->nprim;
   if (!c->d_prim_leaf && c->d_node) {  // once per scene: which leaf holds each prim
     HIP_TRY(hipMalloc((void**)&c->d_prim_leaf, (np + 1) * sizeof(uint32_t)));
+    HIP_TRY(hipMemsetAsync(c->d_prim_leaf, 0xff, (np + 1) * sizeof(uint32_t), s));  // atomicMin's start
     HIP_TRY(rt_cand_prim_leaf(c->d_node, (uint32_t)c->info.nodes, c->d_tri, c->d_prim_leaf, s));
   }
   cp.node = c->d_node;
@@ -1118,12 +1193,6 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
     HIP_TRY(hipMalloc((void**)&c->d_cand_wave_base, nw * sizeof(uint32_t)));
     HIP_TRY(hipMalloc((void**)&c->d_scan_bsum, (size_t)rt_cand_scan_dev_tiles((uint32_t)np) * sizeof(uint32_t)));
     HIP_TRY(hipHostMalloc((void**)&c->h_cand, 8 * sizeof(uint32_t), hipHostMallocDefault));
-  }
-  if (nt + 1 > c->cand_tiles_cap) {
-    size_t cap = c->cand_tiles_cap;
-    rc = grow_dev(&c->d_cand_start, &cap, nt + 1);
-    if (rc) return rc;
-    c->cand_tiles_cap = cap;
   }
   cp.list = c->d_cand_list;
   cp.fp = (rtc::Footprint*)c->d_cand_fp;
@@ -1185,20 +1254,8 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
   HIP_TRY(hipStreamSynchronize(s));
   const uint32_t total = c->h_cand[0], nglobal = c->h_cand[1], nbig = c->h_cand[2];
   const uint32_t nitems = c->h_cand[4], items_over = c->h_cand[5];
-  if (total + 1 > c->cand_cap) {
-    for (uint32_t** b : {&c->d_cand_keys, &c->d_cand_vals, &c->d_cand_keys2, &c->d_cand}) {
-      (void)hipFree(*b);
-      *b = nullptr;
-    }
-
-    c->cand_cap = 0;  // set only once all four entry buffers exist
-    size_t cap = 0;
-    rc = grow_dev(&c->d_cand_keys, &cap, total + 1);
-    if (rc) return rc;
-    for (uint32_t** b : {&c->d_cand_vals, &c->d_cand_keys2, &c->d_cand})
-      HIP_TRY(hipMalloc((void**)b, cap * sizeof(uint32_t)));
-    c->cand_cap = cap;
-  }
+  rc = cand_entry_buffers(c, (size_t)total + (size_t)glob_copies * nglobal);
+  if (rc) return rc;
   cp.keys = c->d_cand_keys;
   cp.vals = c->d_cand_vals;
   HIP_TRY(rt_cand_emit(&cp, s));
@@ -1206,47 +1263,169 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
     HIP_TRY(rt_cand_big(&cp, nbig, s));
   else
     HIP_TRY(rt_cand_big_items(&cp, nitems, s));
-  int bits = 1;
-  while ((1ull << bits) <= nt) bits++;
-  tb = 0;
-  HIP_TRY(rt_cand_sort(c->d_cand_keys, c->d_cand_keys2, c->d_cand_vals, c->d_cand, total, bits,
-                       nullptr, &tb, s));
-  rc = ensure_tmp(c, tb);
+  *total_out = total;
+  *nglobal_out = nglobal;
+  return RT_OK;
+}
+
+// Sorts n (key < n_keys, value) pairs keys/vals -> keys2/vals2 (rocPRIM radix
+// sort, temporary storage in d_scan_tmp).
+static int cand_sort(rt_hip_ctx* c, uint32_t* keys, uint32_t* keys2, uint32_t* vals, uint32_t* vals2, uint32_t n,
+                     size_t n_keys, hipStream_t s) {
+  const int bits = key_bits(n_keys);
+  size_t tb = 0;
+  HIP_TRY(rt_cand_sort(keys, keys2, vals, vals2, n, bits, nullptr, &tb, s));
+  int rc = ensure_tmp(c, tb);
   if (rc) return rc;
   tb = c->scan_tmp_bytes;
-  if (total)
-    HIP_TRY(rt_cand_sort(c->d_cand_keys, c->d_cand_keys2, c->d_cand_vals, c->d_cand, total, bits,
-                         c->d_scan_tmp, &tb, s));
+  if (n) HIP_TRY(rt_cand_sort(keys, keys2, vals, vals2, n, bits, c->d_scan_tmp, &tb, s));
+  return RT_OK;
+}
+
+// This rank's lists, built on this rank: cand_build for the rank's tiles
+// (every prim) -> radix sort by tile -> per-tile offsets -> per-entry skip
+// bounds -> work order.
+static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream_t s, int compat) {
+  CandParams cp;
+  int rc = cand_params(f, c->scene_c, c->scene_r, c->cam_eps_ulps, c->bound_scale, kp->rank, kp->nranks,
+                       &cp, compat);
+  if (rc) return rc;
+  cp.prim0 = 0;
+  cp.prim1 = c->nprim;
+  const size_t nt = (size_t)kp->ntiles_local;
+  uint32_t total = 0, nglobal = 0;
+  rc = cand_build(c, cp, s, 0, &total, &nglobal);
+  if (rc) return rc;
+  rc = cand_tile_buffers(c, nt);
+  if (rc) return rc;
+  // keys are tiles < nt (a key of nt would need one more bit: nt + 1 keys)
+  rc = cand_sort(c, c->d_cand_keys, c->d_cand_keys2, c->d_cand_vals, c->d_cand, total, nt + 1, s);
+  if (rc) return rc;
   HIP_TRY(rt_cand_bounds(c->d_cand_keys2, total, c->d_cand_start, (uint32_t)nt, s));
   // the sorted keys are spent: their buffer takes the per-entry skip bounds
   float* entry_skip = (float*)c->d_cand_keys2;
   HIP_TRY(rt_cand_entry_skip(c->d_cand, c->d_cand_skip, entry_skip, total, s));
   // longest-first work order of the rank's tiles (heavy lists first)
-  if (nt + 1 > c->order_cap) {
-    (void)hipFree(c->d_order);
-    c->d_order = nullptr;
-    c->order_cap = 0;
-    HIP_TRY(hipMalloc((void**)&c->d_order, 3 * (nt + 1) * sizeof(uint32_t)));
-    c->order_cap = nt + 1;
-  }
-  tb = 0;
-  HIP_TRY(rt_cand_order(c->d_cand_start, (uint32_t)nt, total, c->d_order, c->d_order + nt + 1,
-                        c->d_order + 2 * (nt + 1), nullptr, &tb, s));
-  rc = ensure_tmp(c, tb);
+  rc = cand_order(c, kp, nt, total, s);
   if (rc) return rc;
-  tb = c->scan_tmp_bytes;
-  HIP_TRY(rt_cand_order(c->d_cand_start, (uint32_t)nt, total, c->d_order, c->d_order + nt + 1,
-                        c->d_order + 2 * (nt + 1), c->d_scan_tmp, &tb, s));
-  kp->tile_order = c->d_order + 2 * (nt + 1);
-  kp->cand_start = c->d_cand_start;
   kp->cand = c->d_cand;
   kp->cand_global = c->d_cand_global;
   kp->n_cand_global = nglobal;
-  kp->tri_prim = c->d_tri_prim;
   kp->cand_skip = entry_skip;
   c->cand_entries = total;
   c->cand_global = nglobal;
   c->cand_prims = 0;  // not counted separately (entries and globals are)
+  return RT_OK;
+}
+
+// Triangle-parallel lists of an N-rank frame:
+// rank r builds the whole frame's entries of prims [r P / N, (r + 1) P / N)
+// -- the float fast path, classification and emission each run once per
+// prim over the N GPUs instead of once per prim on every GPU -- and routes
+// them to the ranks owning their tiles; one all-to-all exchange gives each
+// rank its own lists (rt_hip_cand_consume).
+extern "C" int rt_hip_cand_produce(rt_hip_ctx* c, const rt_frame* f, int rank, int nranks, unsigned* counts,
+                                   unsigned* nglobal_out, void* stream) {
+  if (!c || !f || !counts || !nglobal_out) return rt_set_error(RT_EINVAL, "null argument");
+  if (nranks <= 0 || rank < 0 || rank >= nranks) return rt_set_error(RT_EINVAL, "rank %d of %d", rank, nranks);
+  if (c->accel != RT_ACCEL_OCTREE || !c->d_node || !c->exact_camera)
+    return rt_set_error(RT_EINVAL, "no camera candidate lists in this configuration (octree, exact camera rays)");
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  CandParams cp;
+  int rc = cand_params(f, c->scene_c, c->scene_r, c->cam_eps_ulps, c->bound_scale, 0, 1, &cp, 0);
+  if (rc) return rc;
+  const uint64_t np = c->nprim;
+  cp.prim0 = (uint32_t)(np * (uint64_t)rank / (uint64_t)nranks);
+  cp.prim1 = (uint32_t)(np * (uint64_t)(rank + 1) / (uint64_t)nranks);
+  uint32_t total = 0, nglobal = 0;
+  rc = cand_build(c, cp, s, (uint32_t)nranks, &total, &nglobal);
+  if (rc) return rc;
+  const uint32_t tpr = (uint32_t)rt_hip_tiles_per_rank(f->width, f->height, nranks);
+  const int tb = rt_block_side(nranks);
+  HIP_TRY(rt_cand_route(c->d_cand_keys, total, cp.tiles_x, nranks, rt_blocks_x(cp.tiles_x, tb), tb, tpr, s));
+  HIP_TRY(rt_cand_route_globals(c->d_cand_global, nglobal, nranks, tpr, c->d_cand_keys + total,
+                                c->d_cand_vals + total, s));
+  const uint32_t n = total + nglobal * (uint32_t)nranks;
+  rc = cand_sort(c, c->d_cand_keys, c->d_cand_keys2, c->d_cand_vals, c->d_cand, n,
+                 (size_t)nranks * (tpr + 1), s);
+  if (rc) return rc;
+  if ((size_t)nranks + 1 > c->rstart_cap) {
+    (void)hipFree(c->d_rstart);
+    (void)hipHostFree(c->h_rstart);
+    c->d_rstart = nullptr;
+    c->h_rstart = nullptr;
+    c->rstart_cap = 0;
+    HIP_TRY(hipMalloc((void**)&c->d_rstart, ((size_t)nranks + 1) * sizeof(uint32_t)));
+    HIP_TRY(hipHostMalloc((void**)&c->h_rstart, ((size_t)nranks + 1) * sizeof(uint32_t), hipHostMallocDefault));
+    c->rstart_cap = (size_t)nranks + 1;
+  }
+  if (3 * (size_t)n + 1 > c->send_cap) {
+    (void)hipFree(c->d_send);
+    c->d_send = nullptr;
+    c->send_cap = 0;
+    const size_t cap = 3 * ((size_t)n + n / 4 + 1024);
+    HIP_TRY(hipMalloc((void**)&c->d_send, cap * sizeof(uint32_t)));
+    c->send_cap = cap;
+  }
+  HIP_TRY(rt_cand_rank_bounds(c->d_cand_keys2, n, tpr, nranks, c->d_rstart, s));
+  HIP_TRY(rt_cand_pack(c->d_cand_keys2, c->d_cand, c->d_cand_skip, n, tpr, c->d_send, s));
+  HIP_TRY(hipMemcpyAsync(c->h_rstart, c->d_rstart, ((size_t)nranks + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                         s));
+  HIP_TRY(hipStreamSynchronize(s));
+  for (int d = 0; d < nranks; d++) counts[d] = c->h_rstart[d + 1] - c->h_rstart[d];
+  *nglobal_out = nglobal;
+  c->send_n = n;
+  return RT_OK;
+}
+
+extern "C" int rt_hip_cand_send_buffer(const rt_hip_ctx* c, const void** d_entries, size_t* n) {
+  if (!c || !d_entries || !n) return rt_set_error(RT_EINVAL, "null argument");
+  *d_entries = c->d_send;
+  *n = c->send_n;
+  return RT_OK;
+}
+
+// This rank's lists from the entries the producers routed to it (any order
+// of sources; 3 words each: rank-local tile or tpr for a global, prim, skip
+// bits): sort by tile -> gather prims and skip bounds -> offsets -> work
+// order.  The next rt_hip_render of (frame, rank, nranks) uses them.
+extern "C" int rt_hip_cand_consume(rt_hip_ctx* c, const rt_frame* f, int rank, int nranks, const void* d_entries,
+                                   size_t n, unsigned nglobal, void* stream) {
+  if (!c || !f || (!d_entries && n)) return rt_set_error(RT_EINVAL, "null argument");
+  if (nranks <= 0 || rank < 0 || rank >= nranks) return rt_set_error(RT_EINVAL, "rank %d of %d", rank, nranks);
+  if (n >= (1ull << 31) || nglobal > n) return rt_set_error(RT_EINVAL, "%zu entries, %u globals", n, nglobal);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  const size_t nt = (size_t)rank_tile_count(f->width, f->height, rank, nranks);
+  const uint32_t tpr = (uint32_t)rt_hip_tiles_per_rank(f->width, f->height, nranks);
+  int rc = cand_entry_buffers(c, n);
+  if (rc) return rc;
+  rc = cand_tile_buffers(c, nt);
+  if (rc) return rc;
+  const uint32_t* in = (const uint32_t*)d_entries;
+  HIP_TRY(rt_cand_unpack(in, (uint32_t)n, (uint32_t)nt, tpr, c->d_cand_keys, c->d_cand_vals, s));
+  // keys are tiles < nt, or nt for the globals: nt + 1 keys
+  rc = cand_sort(c, c->d_cand_keys, c->d_cand_keys2, c->d_cand_vals, c->d_cand, (uint32_t)n, nt + 1, s);
+  if (rc) return rc;
+  const uint32_t total = (uint32_t)(n - nglobal);
+  HIP_TRY(rt_cand_bounds(c->d_cand_keys2, total, c->d_cand_start, (uint32_t)nt, s));
+  // the spent unsorted keys take the skip bounds, the spent indices the prims
+  HIP_TRY(rt_cand_gather(in, c->d_cand, (uint32_t)n, c->d_cand_vals, (float*)c->d_cand_keys, s));
+  KParams kp;
+  std::memset(&kp, 0, sizeof kp);
+  rc = cand_order(c, &kp, nt, total, s);
+  if (rc) return rc;
+  c->ext = kp;
+  c->ext.cand = c->d_cand_vals;
+  c->ext.cand_skip = (const float*)c->d_cand_keys;
+  c->ext.cand_global = c->d_cand_vals + total;
+  c->ext.n_cand_global = nglobal;
+  c->ext_ready = 1;
+  c->ext_rank = rank;
+  c->ext_nranks = nranks;
+  std::memcpy(&c->ext_frame, f, sizeof *f);
+  c->ext_total = total;
   return RT_OK;
 }
 
@@ -1290,6 +1469,10 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
   if (f->width <= 0 || f->height <= 0) return rt_set_error(RT_EINVAL, "empty frame");
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  // lists rt_hip_cand_consume built for exactly this frame and rank: used once
+  const bool use_ext = c->ext_ready && c->ext_rank == rank && c->ext_nranks == nranks &&
+                       std::memcmp(&c->ext_frame, f, sizeof *f) == 0;
+  c->ext_ready = 0;
   KParams p;
   std::memset(&p, 0, sizeof p);
   p.tri = c->d_tri;
@@ -1401,8 +1584,21 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
   hipEvent_t* ev = c->ev[c->frames % RT_TIMED_FRAMES];
   if (c->timing) HIP_TRY(hipEventRecord(ev[0], s));
   if (c->accel == RT_ACCEL_OCTREE && c->d_node && c->exact_camera) {
-    int rc = cand_prepare(c, f, &p, s);
-    if (rc) return rc;
+    if (use_ext) {  // the lists rt_hip_cand_consume built from the producers' entries
+      p.cand_start = c->ext.cand_start;
+      p.cand = c->ext.cand;
+      p.cand_global = c->ext.cand_global;
+      p.n_cand_global = c->ext.n_cand_global;
+      p.cand_skip = c->ext.cand_skip;
+      p.tile_order = c->ext.tile_order;
+      p.tri_prim = c->ext.tri_prim;
+      c->cand_entries = c->ext_total;
+      c->cand_global = c->ext.n_cand_global;
+      c->cand_prims = 0;
+    } else {
+      int rc = cand_prepare(c, f, &p, s);
+      if (rc) return rc;
+    }
   }
   // an empty octree scene has nothing to traverse: the FLAT kernels with 0
   // records are exact (their grids are the FLAT instantiation's own)
@@ -1857,6 +2053,12 @@ extern "C" int rt_hip_memcpy_d2h(void* dst, const void* src, size_t bytes) {
 }
 extern "C" int rt_hip_memcpy_h2d(void* dst, const void* src, size_t bytes) {
   HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+  return RT_OK;
+}
+
+extern "C" int rt_hip_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream) {
+  if (!bytes) return RT_OK;
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
   return RT_OK;
 }
 

@@ -1003,7 +1003,10 @@ __device__ bool staged_any(const KParams& p, const Ray& r, bool act, WaveCtx& w,
 // shadow queries walk per lane, except directional-light shadows (parallel
 // rays, cpu/light.c:53) under RT_POLICY_DIR_STAGED.
 static constexpr int kPacketMin = 8;
-static constexpr int kPacketMaxDepth = 1;  // 0 measured: the same (C5 13.73 vs 13.73 ms, r02n)
+#ifndef RT_PACKET_MAX_DEPTH
+#define RT_PACKET_MAX_DEPTH 1
+#endif
+static constexpr int kPacketMaxDepth = RT_PACKET_MAX_DEPTH;  // 0 measured: the same (C5 13.73 vs 13.73 ms, r02n)
 
 // Brute force: triangle-parallel when the list is long enough to fill the
 // lanes and at most kTpMaxLanes lanes query (ray-parallel streaming costs the

@@ -177,12 +177,18 @@ _PROTOS = [
                                  C.POINTER(C.c_ulonglong)]),
     ("rt_hip_assemble", C.c_int, [C.c_void_p, C.POINTER(Frame), C.c_void_p, C.c_int, C.c_void_p,
                                   C.c_void_p]),
+    ("rt_hip_cand_produce", C.c_int, [C.c_void_p, C.POINTER(Frame), C.c_int, C.c_int, C.POINTER(C.c_uint),
+                                      C.POINTER(C.c_uint), C.c_void_p]),
+    ("rt_hip_cand_send_buffer", C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
+    ("rt_hip_cand_consume", C.c_int, [C.c_void_p, C.POINTER(Frame), C.c_int, C.c_int, C.c_void_p, C.c_size_t,
+                                      C.c_uint, C.c_void_p]),
     ("rt_hip_render_image", C.c_int, [C.c_void_p, C.POINTER(Frame), C.c_void_p,
                                       C.POINTER(Stats)]),
     ("rt_hip_malloc", C.c_int, [C.c_int, C.c_size_t, C.POINTER(C.c_void_p)]),
     ("rt_hip_free", C.c_int, [C.c_void_p]),
     ("rt_hip_memcpy_d2h", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
     ("rt_hip_memcpy_h2d", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
+    ("rt_hip_memcpy_d2d", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
     ("rt_raytrace", C.c_int, [C.c_char_p, C.c_char_p]),
     ("rt_hip_render_compat", C.c_int, [C.c_void_p, C.POINTER(Camera), C.c_void_p,
                                        C.POINTER(Stats)]),
@@ -547,6 +553,29 @@ class Context:
         self._check_render(lib().rt_hip_stats(self.h, C.byref(st)), "rt_hip_stats")
         return st.as_dict()
 
+    def cand_produce(self, frame, rank, nranks, stream=None):
+        """Triangle-parallel lists, step 1 (rt_hip_cand_produce): this rank's
+        slice of the prims over the whole frame, routed by destination rank.
+        Returns (counts per destination rank, this slice's global prims)."""
+        counts = (C.c_uint * nranks)()
+        ng = C.c_uint()
+        _check(lib().rt_hip_cand_produce(self.h, C.byref(frame), rank, nranks, counts, C.byref(ng),
+                                         C.c_void_p(stream) if stream else None), "rt_hip_cand_produce")
+        return [int(x) for x in counts], int(ng.value)
+
+    def cand_send_buffer(self):
+        """(device pointer, entries) of the last produce's routed entries
+        (3 x uint32 each, destination-rank order)."""
+        ptr, n = C.c_void_p(), C.c_size_t()
+        _check(lib().rt_hip_cand_send_buffer(self.h, C.byref(ptr), C.byref(n)), "rt_hip_cand_send_buffer")
+        return ptr.value or 0, int(n.value)
+
+    def cand_consume(self, frame, rank, nranks, d_entries, n, nglobal, stream=None):
+        """Step 4: this rank's lists from the n received entries; the next
+        render of (frame, rank, nranks) uses them (rt_hip_cand_consume)."""
+        _check(lib().rt_hip_cand_consume(self.h, C.byref(frame), rank, nranks, C.c_void_p(d_entries), n, nglobal,
+                                         C.c_void_p(stream) if stream else None), "rt_hip_cand_consume")
+
     def assemble(self, frame, d_gathered, nranks, d_rgb, stream=None):
         _check(lib().rt_hip_assemble(self.h, C.byref(frame), C.c_void_p(d_gathered), nranks,
                                      C.c_void_p(d_rgb), C.c_void_p(stream) if stream else None),
@@ -582,6 +611,29 @@ class Context:
             self.close()
         except Exception:
             pass
+
+
+def exchange_cand_entries(dist, send, counts, nglobal):
+    """Step 3 of the triangle-parallel lists (include/rt_hip.h
+    rt_hip_cand_produce): the all-to-all of the routed entries over
+    torch.distributed (RCCL for device tensors, gloo for host tensors).
+    send: (sum(counts), 3) int32 tensor in destination-rank order; counts:
+    entries for each rank; nglobal: this rank's global prims.  Returns (the
+    (n, 3) int32 entries this rank receives, in source-rank order, and the
+    producers' global prims summed).  Two collectives: the (count, globals)
+    pairs, then the entries."""
+    import torch
+    w = len(counts)
+    meta = torch.tensor([[int(c), int(nglobal)] for c in counts], dtype=torch.int64,
+                        device=send.device).reshape(-1)
+    rmeta = torch.empty_like(meta)
+    dist.all_to_all_single(rmeta, meta)
+    rm = rmeta.view(w, 2).tolist()
+    rc = [int(a) for a, _ in rm]
+    recv = torch.empty((sum(rc), 3), dtype=torch.int32, device=send.device)
+    dist.all_to_all_single(recv, send[: sum(counts)], output_split_sizes=rc,
+                           input_split_sizes=[int(c) for c in counts])
+    return recv, sum(int(b) for _, b in rm)
 
 
 def write_ppm(path, rgb):

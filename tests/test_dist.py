@@ -92,3 +92,43 @@ def test_tile_map_partitions_the_frame(built, W, H, n):
     img = np.random.default_rng(1).random((H, W, 3), dtype=np.float32)
     g = np.stack([rtgpu.tiles_from_image_numpy(img, r, n) for r in range(n)])
     assert np.array_equal(rtgpu.assemble_tiles_numpy(g, W, H, n), img)
+
+
+def _a2a_worker(rank, world, store, q):
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.join(REPO, "raytracing-gpu_amd"))
+    import rtgpu
+    dist.init_process_group("gloo", init_method="file://" + store, rank=rank, world_size=world)
+    # what every producer r routes to every rank d (csrc/rt_cand.hip pack
+    # format: local tile or tpr, prim, skip bits), deterministic per (r, d)
+    def block(r, d):
+        rng = np.random.default_rng(1000 * r + d)
+        n = int(rng.integers(0, 50)) if (r + d) % 3 else 0  # some empty blocks
+        return rng.integers(0, 2**31, (n, 3), dtype=np.int64).astype(np.int32)
+    blocks = [block(rank, d) for d in range(world)]
+    counts = [len(b) for b in blocks]
+    send = torch.from_numpy(np.concatenate(blocks + [np.zeros((7, 3), np.int32)]))  # slack rows past the counts
+    recv, g = rtgpu.exchange_cand_entries(dist, send, counts, nglobal=rank + 1)
+    want = np.concatenate([block(r, rank) for r in range(world)])
+    q.put((rank, bool(np.array_equal(recv.numpy(), want)), g == sum(r + 1 for r in range(world))))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_triangle_parallel_list_exchange_gloo(world, tmp_path):
+    """rtgpu.exchange_cand_entries (bench.py's all-to-all of the routed list
+    entries, rt_hip_cand_produce -> rt_hip_cand_consume) on gloo: every rank
+    receives exactly the blocks every producer routed to it, in source-rank
+    order (empty blocks included), and the producers' global counts summed."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    store = str(tmp_path / "rendezvous")
+    procs = [ctx.Process(target=_a2a_worker, args=(r, world, store, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    res = sorted(q.get(timeout=10) for _ in range(world))
+    assert all(ok and gok for _, ok, gok in res), res

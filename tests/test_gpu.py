@@ -490,6 +490,116 @@ def test_candidate_lists_match_host_c5(gpu):
         assert v["filter_violation"] == 0, (nranks, rank, v)
 
 
+def _produce_all(ctx, f, nranks):
+    """Every rank's triangle-parallel produce, on one context in turn: per
+    producer (host copy of its routed entries (n, 3) uint32, counts, globals)."""
+    import ctypes as C
+    L = gpu_lib()
+    parts = []
+    for r in range(nranks):
+        counts, ng = ctx.cand_produce(f, r, nranks)
+        ptr, n = ctx.cand_send_buffer()
+        assert n == sum(counts)
+        host = np.empty((max(n, 1), 3), np.uint32)
+        if n:
+            assert L.rt_hip_memcpy_d2h(host.ctypes.data_as(C.c_void_p), C.c_void_p(ptr), n * 12) == 0
+        parts.append((host[:n], counts, ng))
+    return parts
+
+
+def _consume_rank(ctx, f, d, nranks, parts):
+    """What rank d receives in the all-to-all (its block from every producer,
+    in source order), uploaded and consumed."""
+    import ctypes as C
+    L = gpu_lib()
+    blocks = []
+    for host, counts, _ in parts:
+        o = sum(counts[:d])
+        blocks.append(host[o:o + counts[d]])
+    recv = np.ascontiguousarray(np.concatenate(blocks) if blocks else np.empty((0, 3), np.uint32))
+    g = sum(p[2] for p in parts)
+    dptr = C.c_void_p()
+    assert L.rt_hip_malloc(0, max(recv.nbytes, 16), C.byref(dptr)) == 0
+    if recv.size:
+        assert L.rt_hip_memcpy_h2d(dptr, recv.ctypes.data_as(C.c_void_p), recv.nbytes) == 0
+    ctx.cand_consume(f, d, nranks, dptr.value, len(recv), g)
+    return dptr, len(recv), g
+
+
+@pytest.mark.parametrize("nranks,accel", [(3, "octree_gpu"), (8, "octree_gpu"), (2, "octree")])
+def test_triangle_parallel_lists_match_per_rank(gpu, nranks, accel):
+    """Triangle-parallel candidate lists (rt_hip_cand_produce -> all-to-all ->
+    rt_hip_cand_consume; the exchange emulated on the host): every producer
+    builds the whole frame's entries of its slice of the triangles, routed to
+    the tiles' ranks; each rank's consumed lists give the same per-tile entry
+    counts as its own per-rank build, and its render the same tile bits and
+    query counts (the winner's key is order-independent)."""
+    s = gpu.Scene.synthetic(6, 6, 9776, seed=0x5EED, width=960, height=540)
+    f = s.frame()
+    ctx = gpu.Context(s, accel)
+    ref = gpu.Context(s, accel)  # (prim -> leaf is the smallest leaf index: the same lists)
+    parts = _produce_all(ctx, f, nranks)
+    assert sum(sum(c) for _, c, _ in parts) > 0
+    L = gpu_lib()
+    for d in range(nranks):
+        dptr, n, g = _consume_rank(ctx, f, d, nranks, parts)
+        t_ext, st_ext = _tiles_of_rank(ctx, f, d, nranks)  # uses the consumed lists
+        nt = gpu.rank_tile_count(f.width, f.height, d, nranks)
+        e_ext = ctx.cand_tile_entries(nt)
+        L.rt_hip_free(dptr)
+        t_ref, st_ref = _tiles_of_rank(ref, f, d, nranks)
+        e_ref = ref.cand_tile_entries(nt)
+        assert np.array_equal(e_ext, e_ref), (d, int(e_ext.sum()), int(e_ref.sum()))
+        assert st_ext["cand_entries"] == st_ref["cand_entries"] == n - g
+        assert_bitexact(t_ext, t_ref, f"rank {d}/{nranks}: consumed vs per-rank lists")
+        assert (st_ext["closest"], st_ext["shadow"]) == (st_ref["closest"], st_ref["shadow"])
+    # the consumed lists are used once: the next render builds its own again
+    t2, st2 = _tiles_of_rank(ctx, f, 0, nranks)
+    t_ref, st_ref = _tiles_of_rank(ref, f, 0, nranks)
+    assert_bitexact(t2, t_ref, "per-rank build after a consumed frame")
+
+
+def test_triangle_parallel_lists_two_processes(gpu):
+    """Two processes (ranks of torch.distributed.run, both on GPU 0, gloo
+    for the exchange since RCCL needs a device per rank): each produces its
+    half of the triangles, the entries go through rtgpu.exchange_cand_entries
+    (bench.py's all-to-all), and each rank's render from the consumed lists
+    equals its render from its own per-rank lists (tests/gpu_dist_worker.py)."""
+    import json
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port),
+                        os.path.join(REPO, "tests", "gpu_dist_worker.py")],
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert line, r.stdout[-2000:]
+    res = json.loads(line[-1])
+    assert res["ok"], res
+
+
+def test_triangle_parallel_lists_c5_rank3(gpu):
+    """The same on C5 itself for rank 3 of 8: the consumed lists' per-tile
+    counts equal the per-rank build's and the rank's tiles are bit-identical."""
+    s = gpu.Scene.synthetic(32, 32, 9776, seed=0x5EED, width=3840, height=2160)
+    f = s.frame()
+    ctx = gpu.Context(s, "octree_gpu")
+    parts = _produce_all(ctx, f, 8)
+    dptr, n, g = _consume_rank(ctx, f, 3, 8, parts)
+    t_ext, st_ext = _tiles_of_rank(ctx, f, 3, 8)
+    nt = gpu.rank_tile_count(f.width, f.height, 3, 8)
+    e_ext = ctx.cand_tile_entries(nt)
+    gpu_lib().rt_hip_free(dptr)
+    t_ref, st_ref = _tiles_of_rank(ctx, f, 3, 8)
+    e_ref = ctx.cand_tile_entries(nt)
+    assert np.array_equal(e_ext, e_ref) and e_ref.sum() > 0
+    assert_bitexact(t_ext, t_ref, "C5 rank 3/8: consumed vs per-rank lists")
+    assert (st_ext["closest"], st_ext["shadow"]) == (st_ref["closest"], st_ref["shadow"])
+
+
 def test_zero_normal_is_an_error(gpu, tmp_path):
     """cpu/hit.c:79 skips an object whose closest hit has an exactly zero
     interpolated normal; that rule is not reproduced, so a render that meets
