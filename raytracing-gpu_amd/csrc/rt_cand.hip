@@ -693,24 +693,23 @@ constexpr uint32_t kChunk = RT_CAND_CHUNK;
 // turn into a compact list, so the f64 classification of pass 1 runs on full
 // waves instead of on the scattered third of the lanes of every wave.
 __global__ __launch_bounds__(RT_LIST_BLOCK) void quick_kernel(CandParams p) {
-  const uint32_t prim = blockIdx.x * blockDim.x + threadIdx.x;
-  if (prim < 8u) p.ctr[prim] = 0u;         // the frame's counters (count / big passes, later launches)
-  if (prim == 0u) p.visits[p.nprim] = 0u;  // the scan's last input
-  if (prim >= p.nprim) return;
-  p.visits[prim] = prim >= p.prim0 && prim < p.prim1 &&
-                           quick_class(p, (const float*)(p.tri + 3 * (size_t)prim)) == Q_LIST
-                       ? 1u
-                       : 0u;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;  // index in the slice [prim0, prim1)
+  const uint32_t len = p.prim1 - p.prim0;
+  if (i < 8u) p.ctr[i] = 0u;          // the frame's counters (count / big passes, later launches)
+  if (i == 0u) p.visits[len] = 0u;    // the scan's last input
+  if (i >= len) return;
+  p.visits[i] = quick_class(p, (const float*)(p.tri + 3 * (size_t)(p.prim0 + i))) == Q_LIST ? 1u : 0u;
 }
 
 __global__ __launch_bounds__(256) void scatter_kernel(CandParams p) {
-  const uint32_t prim = blockIdx.x * blockDim.x + threadIdx.x;
-  if (prim > p.nprim) return;
-  if (prim == p.nprim) {
-    p.ctr[3] = p.off[prim];  // list length
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t len = p.prim1 - p.prim0;
+  if (i > len) return;
+  if (i == len) {
+    p.ctr[3] = p.off[len];  // list length
     return;
   }
-  if (p.visits[prim]) p.list[p.off[prim]] = prim;
+  if (p.visits[i]) p.list[p.off[i]] = p.prim0 + i;
 }
 
 // small footprint: few tile rows, counted here row by row; false: big
@@ -1458,16 +1457,18 @@ extern "C" int rt_cand_verify_host(const CandParams* p, const float* tri, const 
 extern "C" size_t rt_cand_footprint_bytes(void) { return sizeof(rtc::Footprint); }
 
 extern "C" hipError_t rt_cand_quick(const CandParams* p, hipStream_t s) {
-  if (p->nprim == 0) {  // no quick_kernel to zero the counters and the scan's last input
+  const uint32_t len = p->prim1 - p->prim0;
+  if (len == 0) {  // no quick_kernel to zero the counters and the scan's last input
     hipError_t e = hipMemsetAsync(p->ctr, 0, 8 * sizeof(uint32_t), s);
     return e != hipSuccess ? e : hipMemsetAsync(p->visits, 0, sizeof(uint32_t), s);
   }
-  hipLaunchKernelGGL(rtc::quick_kernel, dim3((p->nprim + RT_LIST_BLOCK - 1) / RT_LIST_BLOCK), dim3(RT_LIST_BLOCK), 0, s, *p);
+  hipLaunchKernelGGL(rtc::quick_kernel, dim3((len + RT_LIST_BLOCK - 1) / RT_LIST_BLOCK), dim3(RT_LIST_BLOCK), 0, s, *p);
   return hipGetLastError();
 }
 
 extern "C" hipError_t rt_cand_scatter(const CandParams* p, hipStream_t s) {
-  hipLaunchKernelGGL(rtc::scatter_kernel, dim3((p->nprim + 1 + 255) / 256), dim3(256), 0, s, *p);
+  const uint32_t len = p->prim1 - p->prim0;
+  hipLaunchKernelGGL(rtc::scatter_kernel, dim3((len + 1 + 255) / 256), dim3(256), 0, s, *p);
   return hipGetLastError();
 }
 

@@ -1221,13 +1221,16 @@ static int cand_build(rt_hip_ctx* c, CandParams& cp, hipStream_t s, uint32_t glo
   rc = ensure_tmp(c, tb);
   if (rc) return rc;
   // pass 0: flags -> compact list of the prims the float fast path leaves
+  // (over this build's slice of the prims only)
+  if (cp.prim1 > cp.nprim || cp.prim0 > cp.prim1) return rt_set_error(RT_EINVAL, "prim slice");
+  const uint32_t slice = cp.prim1 - cp.prim0;
   HIP_TRY(rt_cand_quick(&cp, s));
 #if RT_DEV_SCAN
-  HIP_TRY(rt_cand_scan_dev(c->d_cand_visits, c->d_cand_off, (uint32_t)np, nullptr, nullptr, c->d_scan_bsum, s));
+  HIP_TRY(rt_cand_scan_dev(c->d_cand_visits, c->d_cand_off, slice, nullptr, nullptr, c->d_scan_bsum, s));
   HIP_TRY(rt_cand_scatter(&cp, s));
 #else
   tb = c->scan_tmp_bytes;
-  HIP_TRY(rt_cand_scan(c->d_cand_visits, c->d_cand_off, (uint32_t)np, c->d_scan_tmp, &tb, s));
+  HIP_TRY(rt_cand_scan(c->d_cand_visits, c->d_cand_off, slice, c->d_scan_tmp, &tb, s));
   HIP_TRY(rt_cand_scatter(&cp, s));
   HIP_TRY(hipMemsetAsync(c->d_cand_visits, 0, (np + 1) * sizeof(uint32_t), s));
 #endif

@@ -998,15 +998,20 @@ __device__ bool staged_any(const KParams& p, const Ray& r, bool act, WaveCtx& w,
 
 // Traversal policy of an instantiation (RT_POLICY_*, rt_kernels.h).  The
 // default: closest-hit queries walk as a staged packet while at least
-// kPacketMin lanes query at a bounce depth <= kPacketMaxDepth (camera rays
-// and first reflections; deeper reflections are incoherent), else per lane;
+// kPacketMin lanes query at a bounce depth <= kPacketMaxDepth (camera rays;
+// reflections are incoherent), else per lane;
 // shadow queries walk per lane, except directional-light shadows (parallel
 // rays, cpu/light.c:53) under RT_POLICY_DIR_STAGED.
 static constexpr int kPacketMin = 8;
+// Camera rays only (round 4): the reflection rays of a wave diverge, and a
+// packet walks the union of their paths through cold nodes; per lane, the
+// longest items of an 8-way split (reflection-heavy tiles, tools/tile_cost.py)
+// finish sooner -- slowest of 8 ranks 3.13 -> 2.95 ms, C5 at N = 1 10.07 ->
+// 10.04 ms (profiles/r05s_packet_depth/; round 2 measured 0 and 1 equal at N = 1)
 #ifndef RT_PACKET_MAX_DEPTH
-#define RT_PACKET_MAX_DEPTH 1
+#define RT_PACKET_MAX_DEPTH 0
 #endif
-static constexpr int kPacketMaxDepth = RT_PACKET_MAX_DEPTH;  // 0 measured: the same (C5 13.73 vs 13.73 ms, r02n)
+static constexpr int kPacketMaxDepth = RT_PACKET_MAX_DEPTH;
 
 // Brute force: triangle-parallel when the list is long enough to fill the
 // lanes and at most kTpMaxLanes lanes query (ray-parallel streaming costs the
