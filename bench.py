@@ -203,7 +203,7 @@ def main():
                          "tiles over all triangles ('rank'), or triangle-parallel -- each rank "
                          "1/N of the triangles for every rank's tiles, one all-to-all "
                          "('partition', rt_hip_cand_produce / consume); default: partition "
-                         "when N > 1")
+                         "when N >= 4")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary (tools/pmc_traffic.py) to report as roofline.traffic")
     ap.add_argument("--valu-json", default=None,
@@ -263,9 +263,13 @@ def main():
                 raise
     ctx.set_count_work(False)
 
-    partition = (args.lists or ("partition" if world > 1 else "rank")) == "partition" and \
+    # N >= 4: the per-rank lists' fixed part (every triangle on every rank)
+    # outweighs the second sort and the exchange
+    partition = (args.lists or ("partition" if world >= 4 else "rank")) == "partition" and \
         wl["accel"] != "flat"
     send = [None]
+    part_ms = []  # host wall time of produce + exchange + consume enqueue, timed steps only
+    timed = [False]
 
     def exchange_lists():
         # triangle-parallel lists: this rank's slice of the triangles for
@@ -284,7 +288,10 @@ def main():
 
     def step():
         if partition:
+            t = time.perf_counter()
             exchange_lists()
+            if timed[0]:
+                part_ms.append((time.perf_counter() - t) * 1e3)
         ctx.render(frame, rank, world, tiles.data_ptr(), sh)
         if world > 1:
             dist.gather(tiles, list(gathered.view(world, per)) if rank == 0 else None, dst=0)
@@ -332,8 +339,10 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    timed[0] = True
     for _ in range(args.steps):
         step()
+    timed[0] = False
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -345,6 +354,8 @@ def main():
     shade_ms = sum(b for _, b, _ in kt) / len(kt)
     fold_ms = sum(c for _, _, c in kt) / len(kt)
     lists_ms = sum(a for a, _ in ft) / len(ft)
+    if part_ms:  # the render built no lists: the produce / all-to-all / consume wall time instead
+        lists_ms = sum(part_ms) / len(part_ms)
     kern_ms = sum(b for _, b in ft) / len(ft)
     tt = torch.tensor([el, kern_ms, lists_ms, trace_ms, shade_ms, fold_ms], dtype=torch.float64,
                       device=dev)
