@@ -542,7 +542,10 @@ extern "C" int rt_hip_create(int device, const rt_scene* scene, int accel, rt_hi
     rc = rt_set_error(RT_EHIP, "hipStreamCreate");
   rt_device_tree tree{};
   if (!rc && dev_build && fs.ntri) {
-    rt_device_build_opts o{12, 7};  // measured best on C5 (leaf cap 4..32)
+    // leaf cap 24 measured best on C5 with the trace / shade / fold split and
+    // the candidate lists (12: 10.01-10.06 ms, 20 / 24: 9.89, 28: 9.99, 32: 10.01;
+    // profiles/r05u_leaf_sweep/); clip level 7 (6 / 8 no better)
+    rt_device_build_opts o{24, 7};
     if (const char* e = std::getenv("RT_DEV_LEAF")) o.leaf_cap = std::atoi(e);  // tuning knobs
     if (const char* e = std::getenv("RT_DEV_CLIP")) o.clip_level = std::atoi(e);
     hipError_t he = rt_device_build_octree(c->d_tri, (uint32_t)fs.ntri, fs.scene_lo, fs.scene_hi,

@@ -398,6 +398,9 @@ __device__ __forceinline__ uint32_t mask_xor(uint32_t m, uint32_t dm) {
 // child's own (first, info) words from its box record, so a pop needs no
 // node fetch -- one dependent load per step instead of two.  (The per-lane
 // any-hit walk uses push_children_any: measured on C5, 16.18 vs 16.33 ms.)
+#ifndef RT_CHILD_AHEAD
+#define RT_CHILD_AHEAD 1
+#endif
 template <bool CLOSEST, bool COUNT>
 __device__ __forceinline__ void push_children(const float4* __restrict__ node, const Ray& r, f3 inv,
                                               uint32_t dm, uint32_t first, uint32_t info,
@@ -405,6 +408,51 @@ __device__ __forceinline__ void push_children(const float4* __restrict__ node, c
   uint32_t mask = RT_NODE_MASK(info);
   uint32_t mj = mask_xor(mask, dm);
   if (!mj) return;
+#if RT_CHILD_AHEAD >= 2
+  // two child boxes in flight while one is tested: a cold node (the per-lane
+  // reflection walks of an 8-way split's longest items) costs half the
+  // serialised load latencies of one-ahead
+  auto next_child = [&](uint32_t& ci) {
+    const int j = 31 - __clz(mj);
+    mj &= ~(1u << j);
+    ci = first + (uint32_t)__popc(mask & ((1u << ((uint32_t)j ^ dm)) - 1u));
+    if (COUNT) wc.nodes += lanes_distinct(ci);
+  };
+  uint32_t ca, cb = 0;
+  next_child(ca);
+  float4 alo = node[2 * ca], ahi = node[2 * ca + 1], blo, bhi;
+  bool hb = mj != 0u;
+  if (hb) {
+    next_child(cb);
+    blo = node[2 * cb];
+    bhi = node[2 * cb + 1];
+  }
+  for (;;) {
+    const float4 clo = alo, chi = ahi;
+    const uint32_t cc = ca;
+    const bool more = hb;
+    if (hb) {
+      alo = blo;
+      ahi = bhi;
+      ca = cb;
+      hb = mj != 0u;
+      if (hb) {
+        next_child(cb);
+        blo = node[2 * cb];
+        bhi = node[2 * cb + 1];
+      }
+    }
+    const float t0 = box_enter(r, inv, clo, chi);
+    if (CLOSEST) {
+      if (t0 != __builtin_inff() && !(best != __builtin_inff() && rt_prune(t0, r.dlen, best, r.eps)))
+        push(s, cc, t0, wc);
+    } else if (t0 != __builtin_inff()) {
+      push(s, __float_as_uint(clo.w), chi.w, wc);
+    }
+    if (!more) break;
+  }
+  return;
+#endif
   int j = 31 - __clz(mj);
   mj &= ~(1u << j);
   uint32_t ci = first + (uint32_t)__popc(mask & ((1u << ((uint32_t)j ^ dm)) - 1u));
@@ -469,10 +517,42 @@ __device__ __forceinline__ void push_children_any(const float4* __restrict__ nod
 
 // A leaf's records, software-pipelined: record k+1 is in flight while record
 // k is tested.  ANY: returns true at the first any-hit.
+#ifndef RT_REC_AHEAD
+#define RT_REC_AHEAD 1
+#endif
 template <bool ANY, bool COUNT>
 __device__ __forceinline__ bool leaf_lane(const float4* __restrict__ tri, uint32_t first,
                                           uint32_t cnt, const Ray& r, Best& b, LaneCount& wc) {
   const float4* q = tri + 3 * (size_t)first;
+#if RT_REC_AHEAD >= 2
+  if (!ANY) {  // closest hit: two records in flight while one is tested
+    float4 a0 = q[0], a1 = q[1], a2 = q[2], b0, b1, b2;
+    if (cnt > 1) {
+      b0 = q[3];
+      b1 = q[4];
+      b2 = q[5];
+    }
+    for (uint32_t k = 0; k < cnt; k++) {
+      const float4 q0 = a0, q1 = a1, q2 = a2;
+      if (k + 1 < cnt) {
+        a0 = b0;
+        a1 = b1;
+        a2 = b2;
+        if (k + 2 < cnt) {
+          b0 = q[3 * (k + 2)];
+          b1 = q[3 * (k + 2) + 1];
+          b2 = q[3 * (k + 2) + 2];
+        }
+      }
+      if (COUNT) {
+        wc.tris += lanes_distinct(first + k);
+        wc.ltris++;
+      }
+      consider(r, q0, q1, q2, b);
+    }
+    return false;
+  }
+#endif
   float4 n0 = q[0], n1 = q[1], n2 = q[2];
   for (uint32_t k = 0; k < cnt; k++) {
     float4 q0 = n0, q1 = n1, q2 = n2;

@@ -29,7 +29,8 @@ def main():
     ap.add_argument("--policy", type=int, default=0)
     ap.add_argument("--tag", default="c5")
     ap.add_argument("--all", action="store_true", help="every record: --stride calls, one per offset")
-    ap.add_argument("--exact", type=int, default=0, help="proven light buffers (rt_hip_set_exact_shadows)")
+    ap.add_argument("--exact", type=int, default=1,
+                    help="proven light buffers (1, the library default) or slack-grown (0) (rt_hip_set_exact_shadows)")
     ap.add_argument("--probe", type=int, default=0,
                     help="also this many grazing triangles x 50 adversarial origins per light (tools/grazing.py), "
                          "light buffer vs brute force")
@@ -37,8 +38,7 @@ def main():
     s = rtgpu.Scene.synthetic(a.grid, a.grid, 9776, seed=0x5EED, width=a.W, height=a.H)
     ctx = rtgpu.Context(s, "octree_gpu")
     ctx.set_policy(a.policy)
-    if a.exact:
-        ctx.set_exact_shadows(True)
+    ctx.set_exact_shadows(bool(a.exact))
     info = ctx.info()
     img, st = ctx.render_image(s.frame())
     t = time.perf_counter()
