@@ -7,7 +7,10 @@ renders its tiles, renders them again with its own per-rank lists, and rank 0
 prints one JSON line: every rank's tiles bit-identical and equal counts.
 
     python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 \
-        --master-port P tests/gpu_dist_worker.py
+        --master-port P tests/gpu_dist_worker.py [frame]
+
+`frame`: the whole frame as bench.py runs it (lists exchanged, tiles rendered,
+gathered to rank 0 and assembled there), compared with one rank's render.
 """
 import ctypes as C
 import json
@@ -35,9 +38,60 @@ def render_tiles(ctx, L, f, rank, n):
     return out, st
 
 
+def frame(rank, n, L):
+    """The whole N-rank frame as bench.py runs it (triangle-parallel lists,
+    render, gather of the tile buffers to rank 0, rt_hip_assemble), the
+    exchanges on gloo; rank 0 compares the assembled image with its own
+    single-rank render of the frame."""
+    s = rtgpu.Scene.synthetic(4, 4, 9776, seed=0x5EED, width=640, height=360)
+    f = s.frame()
+    ctx = rtgpu.Context(s, "octree_gpu", device=0)
+    counts, ng = ctx.cand_produce(f, rank, n)
+    ptr, m = ctx.cand_send_buffer()
+    send = np.empty((max(m, 1), 3), np.int32)
+    if m:
+        assert L.rt_hip_memcpy_d2h(send.ctypes.data_as(C.c_void_p), C.c_void_p(ptr), m * 12) == 0
+    recv, g = rtgpu.exchange_cand_entries(dist, torch.from_numpy(send), counts, ng)
+    recv = np.ascontiguousarray(recv.numpy())
+    dr = C.c_void_p()
+    assert L.rt_hip_malloc(0, max(recv.nbytes, 16), C.byref(dr)) == 0
+    if recv.size:
+        assert L.rt_hip_memcpy_h2d(dr, recv.ctypes.data_as(C.c_void_p), recv.nbytes) == 0
+    ctx.cand_consume(f, rank, n, dr.value, len(recv), g)
+    tiles, st = render_tiles(ctx, L, f, rank, n)
+    L.rt_hip_free(dr)
+    gathered = [torch.empty(len(tiles)) for _ in range(n)] if rank == 0 else None
+    dist.gather(torch.from_numpy(tiles), gathered, dst=0)
+    q = torch.tensor([st["closest"], st["shadow"]], dtype=torch.int64)
+    dist.reduce(q, dst=0)
+    if rank != 0:
+        return None
+    g_all = np.ascontiguousarray(torch.cat(gathered).numpy())
+    dg, drgb = C.c_void_p(), C.c_void_p()
+    assert L.rt_hip_malloc(0, g_all.nbytes, C.byref(dg)) == 0
+    assert L.rt_hip_malloc(0, f.width * f.height * 12, C.byref(drgb)) == 0
+    assert L.rt_hip_memcpy_h2d(dg, g_all.ctypes.data_as(C.c_void_p), g_all.nbytes) == 0
+    ctx.assemble(f, dg.value, n, drgb.value)
+    ctx.stats()  # waits
+    img = np.empty((f.height, f.width, 3), np.float32)
+    assert L.rt_hip_memcpy_d2h(img.ctypes.data_as(C.c_void_p), drgb, img.nbytes) == 0
+    L.rt_hip_free(dg)
+    L.rt_hip_free(drgb)
+    ref, st1 = ctx.render_image(f)
+    return {"ok": bool(np.array_equal(img.view(np.uint32), ref.view(np.uint32))) and
+            [int(x) for x in q.tolist()] == [st1["closest"], st1["shadow"]],
+            "queries": [int(x) for x in q.tolist()], "single": [st1["closest"], st1["shadow"]]}
+
+
 def main():
     dist.init_process_group("gloo")
     rank, n = dist.get_rank(), dist.get_world_size()
+    if len(sys.argv) > 1 and sys.argv[1] == "frame":
+        res = frame(rank, n, rtgpu.lib())
+        if rank == 0:
+            print(json.dumps(res), flush=True)
+        dist.destroy_process_group()
+        return
     L = rtgpu.lib()
     s = rtgpu.Scene.synthetic(4, 4, 9776, seed=0x5EED, width=640, height=360)
     f = s.frame()

@@ -581,6 +581,29 @@ def test_triangle_parallel_lists_two_processes(gpu):
     assert res["ok"], res
 
 
+def test_three_process_frame_gloo(gpu):
+    """The N-rank frame as bench.py runs it, in three processes on GPU 0 with
+    the collectives on gloo (RCCL needs a device per rank): triangle-parallel
+    lists exchanged, each rank's tiles rendered from them, the tile buffers
+    gathered to rank 0 and assembled there by rt_hip_assemble -- the image
+    equals rank 0's single-rank render bit for bit, with the same summed
+    query counts (tests/gpu_dist_worker.py frame)."""
+    import json
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "3",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port),
+                        os.path.join(REPO, "tests", "gpu_dist_worker.py"), "frame"],
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert line, r.stdout[-2000:]
+    res = json.loads(line[-1])
+    assert res["ok"], res
+
+
 def test_triangle_parallel_lists_c5_rank3(gpu):
     """The same on C5 itself for rank 3 of 8: the consumed lists' per-tile
     counts equal the per-rank build's and the rank's tiles are bit-identical."""
