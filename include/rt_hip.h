@@ -259,8 +259,8 @@ int rt_lightbuf_survey(const rt_scene *scene, unsigned light, int exact, unsigne
  * triangle (brute = 1, cpu/hit.c:93-109); hit[i] = 1 when shadowed. */
 int rt_hip_probe_shadows(rt_hip_ctx *ctx, unsigned light, const float *origins, size_t n, int brute,
                          unsigned char *hit);
-/* Octree traversal policy (default 0): 0 = staged packet walk for coherent
- * closest-hit queries, per-lane walks otherwise; 1 = every query per lane;
+/* Octree traversal policy (default 0): 0 = staged packet walk for camera
+ * rays (>= 8 querying lanes), per-lane walks otherwise; 1 = every query per lane;
  * 2 = every query as a staged packet; 3 = 0 plus staged packet walks for
  * directional-light shadow rays.  All are exact; 1-3 exist for tests and A/B
  * measurements (each is its own kernel, so the default has no switch). */
