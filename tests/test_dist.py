@@ -132,3 +132,33 @@ def test_triangle_parallel_list_exchange_gloo(world, tmp_path):
         assert p.exitcode == 0
     res = sorted(q.get(timeout=10) for _ in range(world))
     assert all(ok and gok for _, ok, gok in res), res
+
+
+@pytest.mark.parametrize("size,n", [((3840, 2160), 8), ((3840, 2160), 4), ((1920, 1080), 3), ((96, 54), 8),
+                                    ((640, 360), 2)])
+def test_triangle_parallel_route_keys(size, n):
+    """The routing of rt_hip_cand_produce (csrc/rt_cand.hip route_kernel,
+    mirrored with rtgpu.tile_local): every scanline tile of the one-rank build
+    maps to one (rank, local tile) with local < tpr, so the key
+    rank * (tpr + 1) + local is unique, below nranks * (tpr + 1), sorts by rank
+    first, and never takes the local slot tpr that marks a global triangle;
+    each rank receives exactly its own tiles (rt_hip_cand_consume's ntiles)."""
+    sys.path.insert(0, os.path.join(REPO, "raytracing-gpu_amd"))
+    import rtgpu
+    W, H = size
+    tx, ty = (W + 7) // 8, (H + 7) // 8
+    t = np.arange(tx * ty)
+    rk, loc = rtgpu.tile_local(t % tx, t // tx, n, W, H)
+    tpr = rtgpu.tiles_per_rank_host(W, H, n)
+    assert (loc < tpr).all() and (rk < n).all()
+    key = rk * (tpr + 1) + loc
+    assert len(np.unique(key)) == len(key) and key.max() < n * (tpr + 1)
+    assert ((key // (tpr + 1)) == rk).all()
+    for r in range(n):
+        mine = np.sort(loc[rk == r])
+        nt = rtgpu.rank_tile_count(W, H, r, n)
+        assert len(mine) <= nt and (mine < nt).all()
+        # the rank's real tiles are exactly its tile slots that hold a pixel
+        px = rtgpu.tile_pixels(W, H, r, n)
+        real = np.flatnonzero((px[..., 0] >= 0).any(axis=1)) if len(px) else np.array([], int)
+        assert np.array_equal(mine, real)
