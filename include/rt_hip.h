@@ -269,16 +269,32 @@ int rt_hip_set_policy(rt_hip_ctx *ctx, int policy);
  * proven bound of tools/mt_bound.py; smaller = a calibrated model, faster,
  * exactness then verified rather than proven: rt_hip_stats returns RT_EINEXACT). */
 int rt_hip_set_camera_bound_scale(rt_hip_ctx *ctx, double scale);
+/* Per-tile refinement of the candidate lists (default 1): the entries of a
+ * triangle whose footprint spans more than 2 tile rows or 32 tiles are kept
+ * only where the error bound evaluated for that tile's own rays (their
+ * directions, origins and grazing cosine) still reaches the tile
+ * (csrc/rt_cand.hip tile_keep) -- proven like the per-triangle bound, so the
+ * lists stay exact.  0: the per-triangle footprints alone (A/B timing). */
+int rt_hip_set_camera_refine(rt_hip_ctx *ctx, int enable);
 /* Host-only survey of the camera candidate lists of a scene's frame (no
  * device): out = {safe, footprint, global} triangle counts, tile entries,
  * then 16 log2 buckets of triangles by entries and 16 of their entries,
  * then 16 log2 buckets of footprint triangles by how far their error region
  * (grown by its distance error) reaches beyond the triangle, in units of the
- * walk's slack, and 16 of their entries; use_leaves: also accept triangles whose error region fits a leaf box of the
- * host-built octree. */
+ * walk's slack, and 16 of their entries; out[68] the entries with the per-tile
+ * refinement (rt_hip_set_camera_refine), [69] / [70] the refined footprints'
+ * entries before / after it; use_leaves: also accept triangles whose error
+ * region fits a leaf box of the host-built octree. */
 int rt_cand_survey(const rt_scene *scene, float eps_ulps, double bound_scale, int threads,
                    int use_leaves, unsigned long long out[72]);
 
+/* Host-only sample of the per-tile refinement (rt_hip_set_camera_refine) of
+ * a scene's frame: every stride-th entry of the refined footprints as (prim,
+ * tile x, tile y, kept) -- tests check each dropped entry against the
+ * reference's float test on every camera sample of its tile.  *n = entries
+ * written (at most cap), *total = entries sampled. */
+int rt_cand_refine_sample(const rt_scene *scene, float eps_ulps, double bound_scale, unsigned stride,
+                          unsigned *out, size_t cap, size_t *n, size_t *total);
 /* Test hook: after an rt_hip_render of (frame, rank, nranks) with exact
  * camera rays, re-derive its candidate lists on the host from the same code
  * and compare.  out = {listed prims, entries, footprint mismatches, tiles

@@ -338,6 +338,62 @@ static color render_pixel(const struct or_scene *scene, vec3 u, vec3 v, vec3 C, 
   return acc;
 }
 
+/* Camera samples (cpu/raytracer.c:50-61, the mapping of render_pixel) of
+ * the PPM pixels [row0, row0 + rows) x [col0, col0 + cols) tested against one
+ * triangle: out[0] = samples intersect() accepts (cpu/hit.c:15-44), out[1] =
+ * samples that pass its a, u and v tests (cpu/hit.c:19-29, t not checked). */
+static void camera_tri_accepts(const struct or_scene *scene, vec3 u, vec3 v, vec3 C,
+                               const struct or_triangle *tri, int row0, int col0, int rows, int cols,
+                               unsigned long long out[2])
+{
+  int W = scene->camera.width, H = scene->camera.height;
+  out[0] = out[1] = 0;
+  for (int row = row0; row < row0 + rows; row++)
+    for (int col = col0; col < col0 + cols; col++)
+    {
+      int ii = W - col, jj = H - row;
+      if (ii < 1 || ii > 2 * (W / 2) || jj < 1 || jj > 2 * (H / 2))
+        continue;
+      int i = ii - W / 2, j = jj - H / 2;
+      for (float k = i; k < i + 1; k += 0.5)
+        for (float l = j; l < j + 1; l += 0.5)
+        {
+          vec3 point = v_add(v_add(C, v_scale(u, k)), v_scale(v, l));
+          ray r = { point, v_normalize(v_sub(scene->camera.position, point)) };
+          vec3 hit, nrm;
+          out[0] += intersect(r, tri, &hit, &nrm) ? 1 : 0;
+          /* the a, u, v stages of intersect() alone */
+          const float eps = 0.0000001;
+          vec3 e1 = v_sub(tri->vertex[1], tri->vertex[0]);
+          vec3 e2 = v_sub(tri->vertex[2], tri->vertex[0]);
+          vec3 h = v_cross(r.direction, e2);
+          float a = v_dot(e1, h);
+          if (a > -eps && a < eps)
+            continue;
+          float f = 1 / a;
+          vec3 s = v_sub(r.origin, tri->vertex[0]);
+          float uu = f * v_dot(s, h);
+          if (uu < 0.0 || uu > 1.0)
+            continue;
+          vec3 q = v_cross(s, e1);
+          float vv = f * v_dot(r.direction, q);
+          if (vv < 0.0 || uu + vv > 1.0)
+            continue;
+          out[1]++;
+        }
+    }
+}
+
+void oracle_camera_tri_accepts(const struct or_scene *scene, const struct or_triangle *tris,
+                               const int *rects, size_t n, unsigned long long *out)
+{
+  vec3 u, v, C;
+  oracle_camera_frame(scene, &u, &v, &C);
+  for (size_t i = 0; i < n; i++)
+    camera_tri_accepts(scene, u, v, C, &tris[i], rects[4 * i], rects[4 * i + 1], rects[4 * i + 2],
+                       rects[4 * i + 3], out + 2 * i);
+}
+
 /* ---- gpu/rt compatibility mode ----
  * gpu/raytracer.cu:31-129, gpu/light.cu:12-126, gpu/colors.cu:3-49 as the
  * sources read (PARTITIONING_NONE order of gpu/hit.cu:83-116, which is

@@ -65,6 +65,13 @@ int oracle_render(const struct or_scene *scene, const int *pixels, size_t npix,
 int oracle_render_gpu(const struct or_scene *scene, const int *pixels, size_t npix,
                       int nthreads, unsigned char *out, struct or_counts *counts);
 
+/* Camera samples (cpu/raytracer.c:50-61) against one triangle each: for
+ * i < n, the PPM pixels [row0, row0 + rows) x [col0, col0 + cols) (rects[4i ..
+ * 4i + 3]) against tris[i]: out[2i] = samples cpu/hit.c:15-44 accepts,
+ * out[2i + 1] = samples passing its a, u, v tests (t not checked). */
+void oracle_camera_tri_accepts(const struct or_scene *scene, const struct or_triangle *tris,
+                               const int *rects, size_t n, unsigned long long *out);
+
 /* Single-function entry points, for unit known-answer tests. */
 struct or_color oracle_init_color(float r, float g, float b);
 struct or_color oracle_color_add(struct or_color a, struct or_color b);

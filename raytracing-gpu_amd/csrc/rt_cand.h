@@ -29,6 +29,7 @@ struct CandParams {
   double n[3];            // unit normal of the image plane (u x v)
   double plane;           // (C - pos) . n
   double ginv[3];         // inverse Gram matrix of (u, v): [g0 g1; g1 g2]
+  double k0, l0;          // image coordinates of pos - C: ginv (u . (pos - C), v . (pos - C))
   double gscale;          // a bound of its norm
   double lmax;            // max |o - pos| over the frame's camera origins
   double omax;            // max |o| over them
@@ -65,6 +66,11 @@ struct CandParams {
   uint32_t item_cap;
   uint32_t* wave_items;   // rt_cand_big_waves() + 1: items of each big_count wave ([last] = 0)
   const uint32_t* wave_base;  // its exclusive scan ([last] = all items)
+  // 1: the big footprints' entries are refined per tile (rt_cand.hip
+  // tile_keep); an entry it drops is written with key drop_key (= the tile
+  // count: it sorts after every tile and bounds_kernel leaves it out)
+  uint32_t refine;
+  uint32_t drop_key;
 };
 
 // Host mirror for surveys (same classify/raster code): safe / footprint /
@@ -74,6 +80,9 @@ struct CandParams {
 extern "C" int rt_cand_survey_host(const CandParams* p, const float* tri, const float* node,
                                    const uint32_t* prim_leaf, int threads,
                                    unsigned long long out[72]);
+// Host sample of the per-tile refinement's decisions (tests; see rt_cand.hip)
+extern "C" size_t rt_cand_refine_sample_host(const CandParams* p, const float* tri, uint32_t stride,
+                                             uint32_t* out, size_t cap, size_t* total);
 // Host check of one frame's device-built lists (tests; see rt_cand.hip)
 extern "C" int rt_cand_verify_host(const CandParams* p, const float* tri, const float* node,
                                    const uint32_t* prim_leaf, const uint32_t* list, uint32_t nlist,
@@ -120,14 +129,16 @@ extern "C" hipError_t rt_cand_bounds(const uint32_t* keys, uint32_t n, uint32_t*
 // Triangle-parallel multi-GPU lists (rt_hip_cand_produce / rt_hip_cand_consume):
 // a whole-frame build (one rank, scanline tiles) of a slice of the prims, its
 // entries routed to the N-rank tile map.  route: key = scanline tile ->
-// dest_rank * (tpr + 1) + rank-local tile (tpr = tiles per rank); globals:
+// dest_rank * (tpr + 1) + rank-local tile (tpr = tiles per rank), and
+// drop_key (an entry the refinement dropped) -> nranks * (tpr + 1); globals:
 // one entry per rank with the local slot tpr.  rank_bounds: start[d] = first
-// entry of rank d in the routed, sorted keys (start[n] = total).  pack: 3
+// entry of rank d in the routed, sorted keys (start[n] = the routed entries,
+// the dropped ones sort after them).  pack: 3
 // words per entry (local tile or tpr, prim, skip bits).  unpack (consumer):
 // keys = local tile (tpr -> ntiles: the globals sort last), idx = i.
 // gather: the sorted entries' prims and skip bounds.
 extern "C" hipError_t rt_cand_route(uint32_t* keys, uint32_t n, int tiles_x, int nranks, int blocks_x, int tb,
-                                    uint32_t tpr, hipStream_t s);
+                                    uint32_t tpr, uint32_t drop_key, hipStream_t s);
 extern "C" hipError_t rt_cand_route_globals(const uint32_t* global, uint32_t nglobal, int nranks, uint32_t tpr,
                                             uint32_t* keys, uint32_t* vals, hipStream_t s);
 extern "C" hipError_t rt_cand_rank_bounds(const uint32_t* keys, uint32_t n, uint32_t tpr, int nranks,

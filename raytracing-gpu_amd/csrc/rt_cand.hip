@@ -238,6 +238,22 @@ RTC_FN int classify(const CandParams& p, const float* r, const float* leafbox, F
   const double rT = pt_tri_dist(p.pos, v0, v1, v2);
   if (!(rT > 2.0 * p.dline + 1e-9)) return GLOBAL;
   const double c_band = fmin(1.0, (deye + p.dline + kmax_ch) / (rT - p.dline));
+#ifndef RT_CAND_CMIN
+#define RT_CAND_CMIN 1
+#endif
+#if RT_CAND_CMIN
+  // cpu/hit.c:19-20 rejects |a| < 1e-7, and |a| <= kDMax nl c + e_a: no
+  // line with c < c_min is accepted.  Every candidate line has c <= c_band,
+  // so c_min > c_band leaves none (with c_ok > 0 the lines below c_ok are
+  // unbounded and c_min < c_ok: no exit there)
+  if (c_ok == 0.0 && (kAMin - e_a) > c_band * (kDMax * nl) * (1.0 + 1e-6)) return SAFE;
+#endif
+#if defined(RT_SURVEY_DUMP) && !defined(__HIP_DEVICE_COMPILE__)
+  if (td) {
+    td[7] = nl; td[8] = deye; td[9] = rT; td[10] = c_band; td[11] = (kAMin - e_a) / (kDMax * nl);
+    td[12] = cl; td[13] = hreach; td[14] = kmax_ch; td[15] = e_a; td[16] = e_sh; td[17] = a_lb;
+  }
+#endif
   const double wide = p.lmax + p.dline + p.dorig;
   fp.b0 = dot3(nh, p.pos) - dot3(nh, p.C);
   fp.b1 = -dot3(nh, p.u);
@@ -658,6 +674,171 @@ __host__ __device__ inline uint32_t raster_count(const CandParams& p, const Foot
   return n;
 }
 
+// Per-tile refinement of a listed (prim, tile) entry.  classify() bounds the
+// error region T_D once per triangle, over every camera line that can reach
+// it: the smallest grazing cosine of any such line and the widest cone of
+// directions.  The rays of one 8x8 tile have nearly one direction, so the
+// same bound (tools/mt_bound.py, componentwise) evaluated with that tile's
+// own |d_i|, |o_i - v0_i| and |a| gives a T_D of the tile's rays alone;
+// false when the tile's samples, projected through the eye and widened by
+// the camera lines' float deviation (classify's dimg), provably miss it (or
+// no ray of the tile reaches |a| >= 1e-7).  true whenever unsure.
+// The triangle's part (once per footprint):
+struct TileTri {
+  double v0[3], e1[3], e2[3], ae1[3], ae2[3];
+  double nh[3];   // unit normal
+  double nl;      // |e1 x e2|
+  double l1, l2;  // |e1|, |e2|
+};
+RTC_FN bool tile_tri(const float* r, TileTri& t) {
+  for (int a = 0; a < 3; a++) {
+    t.v0[a] = r[a];
+    t.e1[a] = r[3 + a];
+    t.e2[a] = r[6 + a];
+    t.ae1[a] = fabs(t.e1[a]);
+    t.ae2[a] = fabs(t.e2[a]);
+  }
+  const double n[3] = {t.e1[1] * t.e2[2] - t.e1[2] * t.e2[1], t.e1[2] * t.e2[0] - t.e1[0] * t.e2[2],
+                       t.e1[0] * t.e2[1] - t.e1[1] * t.e2[0]};
+  t.nl = norm3(n);
+  t.l1 = norm3(t.e1);
+  t.l2 = norm3(t.e2);
+  if (!(t.nl > 0.0)) return false;
+  const double inl = 1.0 / t.nl;
+  for (int a = 0; a < 3; a++) t.nh[a] = n[a] * inl;
+  return true;
+}
+
+// The tile's part.  Division-light (the big emission runs it per entry, in
+// f64): the affine quantities' extremes over the tile's sample rectangle in
+// closed form (|f_c| + |f_k| hk + |f_l| hl), and T_D's projection tested in
+// homogeneous image coordinates (no per-corner division).
+RTC_FN bool tile_keep(const CandParams& p, const TileTri& t, int tx, int ty) {
+  // the tile's sample rectangle [kc -+ hk] x [lc -+ hl] (pixel_range's inverse)
+  const double hw = (double)(p.W / 2), hh = (double)(p.H / 2);
+  const int c0 = tx * 8, r0 = ty * 8;
+  double kc, hk, lc, hl;
+  if (p.compat) {
+    kc = c0 + 3.5 - hw;
+    hk = 3.5;
+    lc = r0 + 3.5 - hh;
+    hl = 3.5;
+  } else {
+    kc = hw - c0 - 3.25;
+    hk = 3.75;
+    lc = hh - r0 - 3.25;
+    hl = 3.75;
+  }
+  // per axis max |pos_i - o_i|, max |o_i - v0_i| (o = C + k u + l v); the
+  // grazing offset b = (pos - o) . nh over the rectangle: [bc - bw, bc + bw]
+  double pm[3], sm[3], po[3];
+  for (int a = 0; a < 3; a++) {
+    const double oc = p.C[a] + kc * p.u[a] + lc * p.v[a];
+    const double w = fabs(p.u[a]) * hk + fabs(p.v[a]) * hl;
+    po[a] = p.pos[a] - oc;
+    pm[a] = fabs(po[a]) + w;
+    sm[a] = (fabs(oc - t.v0[a]) + w + p.dorig) * (1.0 + 1e-9);
+  }
+  const double bc = dot3(po, t.nh), bw = fabs(dot3(p.u, t.nh)) * hk + fabs(dot3(p.v, t.nh)) * hl;
+  // |pos - o| within the centre's +- the tile's half diagonal
+  const double hd = hk * norm3(p.u) + hl * norm3(p.v);
+  const double rc = norm3(po);
+  const double rmn = rc - hd - p.dorig, rmx = (rc + hd + p.dorig) * (1.0 + 1e-9);
+  if (!(rmn > 1e-6)) return true;
+  const double irn = 1.0 / rmn;
+  // float origins within dorig, float directions within a few eps of pos - o
+  double dm[3];
+  for (int a = 0; a < 3; a++) dm[a] = fmin(1.0, (pm[a] + p.dorig) * irn + 8.0 * kEps) * kDMax;
+  double M[3], N[3];
+  for (int i = 0; i < 3; i++) {
+    const int j = (i + 1) % 3, k = (i + 2) % 3;
+    M[i] = dm[j] * t.ae2[k] + dm[k] * t.ae2[j];
+    N[i] = sm[j] * t.ae1[k] + sm[k] * t.ae1[j];
+  }
+  const double cw = p.c_dot / 8.6 * 6.01 * kEps, ca = p.c_a / 7.2 * 5.01 * kEps;
+  const double smax = norm3(sm);
+  const double e_sh = fmin(cw * (sm[0] * M[0] + sm[1] * M[1] + sm[2] * M[2]), p.c_dot * kEps * smax * kDMax * t.l2);
+  const double e_dq = fmin(cw * (dm[0] * N[0] + dm[1] * N[1] + dm[2] * N[2]), p.c_dot * kEps * smax * kDMax * t.l1);
+  const double e_a = fmin(ca * (t.ae1[0] * M[0] + t.ae1[1] * M[1] + t.ae1[2] * M[2]),
+                          p.c_a * kEps * t.l1 * t.l2 * kDMax);
+  // grazing cosine of the tile's rays: |b| over the rectangle is in [bl, bh]
+  const double bl = fmax(0.0, fabs(bc) - bw), bh = fabs(bc) + bw;
+  const double cmax = fmin(1.0, (bh + p.dorig) * irn + 8.0 * kEps);
+  if (kDMax * t.nl * cmax + e_a < kAMin) return false;  // |a| < 1e-7 for every ray of the tile
+  const double cmin = fmax(0.0, (bl - p.dorig) / rmx - 8.0 * kEps);
+  const double a_lb = fmax(kAMin, kDMin * t.nl * cmin - e_a);
+  const double ia = 1.0 / a_lb;
+  const double rho = e_a * ia;
+  if (!(rho < 0.5)) return true;
+  const double i1r = 1.0 / (1.0 - rho);
+  const double du = e_sh * ia * i1r, dv = e_dq * ia * i1r;
+  const double dw = (4.0 * kEps + (e_sh + e_dq) * ia + rho) * i1r;
+  // T_D's corners relative to the eye, Y_k = P_k - pos, and their image
+  // points in homogeneous form H_k = (K0 yn + plane alpha, L0 yn + plane
+  // beta, yn) ~ (K_k, L_k, 1) (yn = Y . n, alpha / beta = Y's image-axis
+  // coordinates through ginv): classify's lam = plane / yn, without dividing
+  double H[3][3], ymag = 1.0, ylo = 1e300, yhi = -1e300;
+  const double cu[3] = {-du, 1.0 + dw + dv, -du}, cv[3] = {-dv, -dv, 1.0 + dw + du};
+  for (int k = 0; k < 3; k++) {
+    double Y[3];
+    for (int a = 0; a < 3; a++) Y[a] = t.v0[a] + cu[k] * t.e1[a] + cv[k] * t.e2[a] - p.pos[a];
+    const double yn = dot3(Y, p.n), yu = dot3(Y, p.u), yv = dot3(Y, p.v);
+    H[k][0] = p.k0 * yn + p.plane * (p.ginv[0] * yu + p.ginv[1] * yv);
+    H[k][1] = p.l0 * yn + p.plane * (p.ginv[1] * yu + p.ginv[2] * yv);
+    H[k][2] = yn;
+    ymag = fmax(ymag, fabs(Y[0]) + fabs(Y[1]) + fabs(Y[2]));
+    ylo = fmin(ylo, yn);
+    yhi = fmax(yhi, yn);
+  }
+  // every corner strictly on one side of the eye plane; the nearest point of
+  // T_D is then at least min |yn| from the eye
+  if (!(ylo > 1e-6 * ymag || yhi < -1e-6 * ymag)) return true;
+  const double sg = ylo > 0.0 ? 1.0 : -1.0, rlo = fmin(fabs(ylo), fabs(yhi));
+  const double dimg = 1.5 * p.gscale * (p.dline * (1.0 + p.lmax / rlo) + p.dorig) + 1e-3;
+  const double x0 = kc - hk - dimg, x1 = kc + hk + dimg, y0 = lc - hl - dimg, y1 = lc + hl + dimg;
+  // separating axes: the rectangle's (K_k < x0 <=> sg H_k0 < sg x0 yn_k, ...)
+  {
+    bool lx = true, gx = true, ly = true, gy = true;
+    for (int k = 0; k < 3; k++) {
+      const double hx = sg * H[k][0], hy = sg * H[k][1], w = sg * H[k][2];  // w > 0
+      const double tx0 = 1e-9 * (fabs(hx) + fabs(x0) * w), tx1 = 1e-9 * (fabs(hx) + fabs(x1) * w);
+      const double ty0 = 1e-9 * (fabs(hy) + fabs(y0) * w), ty1 = 1e-9 * (fabs(hy) + fabs(y1) * w);
+      lx = lx && hx < x0 * w - tx0;
+      gx = gx && hx > x1 * w + tx1;
+      ly = ly && hy < y0 * w - ty0;
+      gy = gy && hy > y1 * w + ty1;
+    }
+    if (lx || gx || ly || gy) return false;
+  }
+  // and the triangle's edges: q = (x, y, 1) lies outside edge e -> f when
+  // det[H_e; H_f; q] has the sign opposite to det[H_0; H_1; H_2] sg
+  double c01[3], c12[3], c20[3];
+  auto cross3 = [](const double* a, const double* b, double* c) {
+    c[0] = a[1] * b[2] - a[2] * b[1];
+    c[1] = a[2] * b[0] - a[0] * b[2];
+    c[2] = a[0] * b[1] - a[1] * b[0];
+  };
+  cross3(H[0], H[1], c01);
+  cross3(H[1], H[2], c12);
+  cross3(H[2], H[0], c20);
+  const double orient = dot3(H[2], c01) * sg;
+  if (orient == 0.0) return true;
+  const double so = orient > 0.0 ? 1.0 : -1.0;
+  const double* C3[3] = {c01, c12, c20};
+  for (int e = 0; e < 3; e++) {
+    const double cx = so * C3[e][0], cy = so * C3[e][1], cz = so * C3[e][2];
+    const double mx = fmax(cx * x0, cx * x1) + fmax(cy * y0, cy * y1) + cz;  // largest over the rectangle
+    const double tol = 1e-9 * (fabs(cx) * fmax(fabs(x0), fabs(x1)) + fabs(cy) * fmax(fabs(y0), fabs(y1)) + fabs(cz));
+    if (mx < -tol) return false;
+  }
+  return true;
+}
+
+RTC_FN bool tile_keep(const CandParams& p, const float* r, int tx, int ty) {
+  TileTri t;
+  return !tile_tri(r, t) || tile_keep(p, t, tx, ty);
+}
+
 // A footprint is "big" -- counted and emitted by one wave, its tile rows
 // spread over the lanes -- when it spans more than kSmallRows tile rows or
 // has more than kSmallEntries entries; the others are counted and emitted by
@@ -710,6 +891,17 @@ __global__ __launch_bounds__(256) void scatter_kernel(CandParams p) {
     return;
   }
   if (p.visits[i]) p.list[p.off[i]] = p.prim0 + i;
+}
+
+// The footprints whose entries are refined per tile (CandParams::refine):
+// those spanning more than kSmallRows tile rows of the frame.  A property of
+// the footprint alone, not of a rank's share of its tiles, so a rank's own
+// lists and the triangle-parallel build (one whole-frame rank) refine the same
+// entries; all of them are big footprints (the big passes emit them).
+__host__ __device__ inline bool refined_rows(int r0, int r1) { return (r1 >> 3) - (r0 >> 3) + 1 > kSmallRows; }
+__host__ __device__ inline bool refined_footprint(const CandParams& p, const Footprint& fp) {
+  int r0, r1;
+  return raster_rows(p, fp, r0, r1) && refined_rows(r0, r1);
 }
 
 // small footprint: few tile rows, counted here row by row; false: big
@@ -850,7 +1042,7 @@ __global__ __launch_bounds__(64) void item_kernel(CandParams p) {
 // -- one division per block, none per tile.  Returns the count written at
 // keys/vals[o ..].
 __device__ __forceinline__ uint32_t emit_interval(const CandParams& p, int ty, int x0, int x1,
-                                                  uint32_t o, uint32_t prim) {
+                                                  uint32_t o, uint32_t prim, bool refine = false) {
   if (x0 > x1) return 0;
   const uint32_t n = (uint32_t)p.nranks, r = (uint32_t)p.rank;
   int f;
@@ -862,7 +1054,8 @@ __device__ __forceinline__ uint32_t emit_interval(const CandParams& p, int ty, i
     const int a = x0 > bx * tb ? x0 : bx * tb, b = x1 < bx * tb + tb - 1 ? x1 : bx * tb + tb - 1;
     const uint32_t base = ((by * (uint32_t)p.blocks_x + (uint32_t)bx) / n) * (uint32_t)(tb * tb) + row;
     for (int tx = a; tx <= b; tx++, k++) {
-      p.keys[o + k] = base + (uint32_t)(tx - bx * tb);
+      const bool keep = !refine || tile_keep(p, (const float*)(p.tri + 3 * (size_t)prim), tx, ty);
+      p.keys[o + k] = keep ? base + (uint32_t)(tx - bx * tb) : p.drop_key;
       p.vals[o + k] = prim;
     }
   }
@@ -872,15 +1065,15 @@ __device__ __forceinline__ uint32_t emit_interval(const CandParams& p, int ty, i
 // One tile row of a footprint (raster_row's tiles: [a0, a1] and the parts
 // of [b0, b1] outside it); returns the entries written.
 __device__ __forceinline__ uint32_t emit_row(const CandParams& p, const Footprint& fp, int ty, int r0,
-                                             int r1, uint32_t o, uint32_t prim) {
+                                             int r1, uint32_t o, uint32_t prim, bool refine = false) {
   int a0, a1, b0, b1;
   row_tiles(p, fp, ty, r0, r1, a0, a1, b0, b1);
-  uint32_t k = emit_interval(p, ty, a0, a1, o, prim);
+  uint32_t k = emit_interval(p, ty, a0, a1, o, prim, refine);
   if (a0 > a1) {
-    k += emit_interval(p, ty, b0, b1, o + k, prim);
+    k += emit_interval(p, ty, b0, b1, o + k, prim, refine);
   } else {
-    k += emit_interval(p, ty, b0, b1 < a0 - 1 ? b1 : a0 - 1, o + k, prim);
-    k += emit_interval(p, ty, b0 > a1 + 1 ? b0 : a1 + 1, b1, o + k, prim);
+    k += emit_interval(p, ty, b0, b1 < a0 - 1 ? b1 : a0 - 1, o + k, prim, refine);
+    k += emit_interval(p, ty, b0 > a1 + 1 ? b0 : a1 + 1, b1, o + k, prim, refine);
   }
   return k;
 }
@@ -931,8 +1124,9 @@ __global__ __launch_bounds__(64) void big_kernel(CandParams p) {
     else if (rows)
       for (int ty = ty0 + lane; ty <= ty1; ty += 64) cnt += count_row(p, fp, ty, r0, r1);
     uint32_t o = p.off[j] + wave_excl_scan(cnt, lane);
+    const bool refine = p.refine != 0u && rows && refined_rows(r0, r1);
     if (rows)
-      for (int ty = ty0 + lane; ty <= ty1; ty += 64) o += emit_row(p, fp, ty, r0, r1, o, prim);
+      for (int ty = ty0 + lane; ty <= ty1; ty += 64) o += emit_row(p, fp, ty, r0, r1, o, prim, refine);
   }
 }
 
@@ -971,6 +1165,8 @@ __global__ __launch_bounds__(64) void big_item_kernel(CandParams p) {
   const Footprint fp = p.fp[j];
   int r0, r1;
   if (!raster_rows(p, fp, r0, r1)) return;  // no entries, no items
+  TileTri tt;  // the triangle's part of the per-tile refinement, once per item
+  const bool refine = p.refine != 0u && refined_rows(r0, r1) && tile_tri((const float*)(p.tri + 3 * (size_t)prim), tt);
   uint32_t g0 = 0;  // entries of the footprint before this group of rows
   for (int gy = r0 >> 3; gy <= (r1 >> 3) && g0 < c1; gy += 64) {
     const int ty = gy + lane;
@@ -1012,8 +1208,10 @@ __global__ __launch_bounds__(64) void big_item_kernel(CandParams p) {
         }
         const int tx = kth_rank_col(p, rx[r][2 * iv], rx[r][2 * iv + 1], rf[r][iv], k);
         uint32_t rk;
-        p.keys[base + e] = rt_tile_local(tx, rty[r], (uint32_t)p.nranks, (uint32_t)p.blocks_x,
-                                         (uint32_t)p.tb, &rk);
+        const bool keep = !refine || tile_keep(p, tt, tx, rty[r]);
+        p.keys[base + e] = keep ? rt_tile_local(tx, rty[r], (uint32_t)p.nranks, (uint32_t)p.blocks_x,
+                                                (uint32_t)p.tb, &rk)
+                                : p.drop_key;
         p.vals[base + e] = prim;
       }
     }
@@ -1034,7 +1232,9 @@ __global__ __launch_bounds__(256) void prim_leaf_kernel(const float4* node, uint
   for (uint32_t k = 0; k < cnt; k++) atomicMin(prim_leaf + __float_as_uint(tri[3 * (size_t)(first + k) + 2].y), ni);
 }
 
-// start[t] = first entry of tile t in the tile-sorted keys; start[n] = total
+// start[t] = first entry of tile t in the tile-sorted keys; start[ntiles] =
+// the entries with a tile (the refinement's dropped entries, key ntiles, sort
+// after them)
 __global__ __launch_bounds__(256) void bounds_kernel(const uint32_t* keys, uint32_t n, uint32_t* start,
                                                      uint32_t ntiles) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1047,7 +1247,7 @@ __global__ __launch_bounds__(256) void bounds_kernel(const uint32_t* keys, uint3
     else
       hi = mid;
   }
-  start[t] = t == ntiles ? n : lo;
+  start[t] = lo;
 }
 
 // per list entry: the depth-skip bound of its prim (coalesced for the render
@@ -1062,10 +1262,14 @@ __global__ __launch_bounds__(256) void entry_skip_kernel(const uint32_t* cand, c
 // A whole-frame entry (scanline tile of the one-rank map) -> its rank d and
 // rank-local tile l under the N-rank block map: key d (tpr + 1) + l.
 __global__ __launch_bounds__(256) void route_kernel(uint32_t* keys, uint32_t n, int tiles_x, int nranks,
-                                                    int blocks_x, int tb, uint32_t tpr) {
+                                                    int blocks_x, int tb, uint32_t tpr, uint32_t drop_key) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t t = keys[i];
+  if (t == drop_key) {  // dropped by the refinement: after every rank's entries
+    keys[i] = (uint32_t)nranks * (tpr + 1u);
+    return;
+  }
   uint32_t d;
   const uint32_t l = rt_tile_local((int)(t % (uint32_t)tiles_x), (int)(t / (uint32_t)tiles_x), (uint32_t)nranks,
                                    (uint32_t)blocks_x, (uint32_t)tb, &d);
@@ -1082,7 +1286,8 @@ __global__ __launch_bounds__(256) void route_globals_kernel(const uint32_t* glob
   vals[i] = global[g];
 }
 
-// start[d] = first entry of rank d (keys sorted), start[nranks] = n
+// start[d] = first entry of rank d (keys sorted), start[nranks] = the routed
+// entries (the dropped ones, key nranks (tpr + 1), sort after them)
 __global__ __launch_bounds__(64) void rank_bounds_kernel(const uint32_t* keys, uint32_t n, uint32_t tpr,
                                                          int nranks, uint32_t* start) {
   const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1096,7 +1301,7 @@ __global__ __launch_bounds__(64) void rank_bounds_kernel(const uint32_t* keys, u
     else
       hi = mid;
   }
-  start[d] = d == (uint32_t)nranks ? n : lo;
+  start[d] = lo;
 }
 
 __global__ __launch_bounds__(256) void pack_kernel(const uint32_t* keys, const uint32_t* prims, const float* skip,
@@ -1275,19 +1480,34 @@ extern "C" int rt_cand_survey_host(const CandParams* p, const float* tri, const 
   std::vector<unsigned long long> part(72 * (size_t)threads, 0);
   std::vector<unsigned long long> bad((size_t)threads, 0);
   std::vector<std::thread> th;
+#ifdef RT_SURVEY_DUMP
+  std::vector<std::vector<double>> dump((size_t)threads);
+#endif
   for (int t = 0; t < threads; t++)
-    th.emplace_back([=, &part, &bad]() {
+    th.emplace_back([&, t]() {
       unsigned long long* o = &part[72 * (size_t)t];
       for (uint32_t i = (uint32_t)t; i < p->nprim; i += (uint32_t)threads) {
         rtc::Footprint fp;
         const float* lb = prim_leaf ? node + 8 * (size_t)prim_leaf[i] : nullptr;
-        double td[7];
+        double td[18];
         const float* rec = tri + 12 * (size_t)i;
         const int c = rtc::classify(*p, rec, lb, fp, td);
         o[c]++;
         if (c == rtc::FOOTPRINT) {
-          unsigned long long v = 0;
-          rtc::raster(*p, fp, [&](uint32_t) { v++; });
+          unsigned long long v = 0, kept = 0;
+          rtc::raster(*p, fp, [&](uint32_t tl) {
+            v++;
+            int tx, ty;
+            rt_tile_xy(tl, (uint32_t)p->rank, (uint32_t)p->nranks, (uint32_t)p->blocks_x, (uint32_t)p->tb, &tx, &ty);
+            kept += rtc::tile_keep(*p, rec, tx, ty) ? 1u : 0u;
+          });
+          if (rtc::refined_footprint(*p, fp)) {  // the device refines these (CandParams::refine)
+            o[68] += kept;
+            o[69] += v;
+            o[70] += kept;
+          } else {
+            o[68] += v;
+          }
           // big_count_kernel counts rows through row_ivs (big_item_kernel's intervals)
           unsigned long long vi = 0;
           int q0, q1;
@@ -1334,10 +1554,22 @@ extern "C" int rt_cand_survey_host(const CandParams* p, const float* tri, const 
           while (kg < 15 && g >= p->eps_avail * std::ldexp(1.0, kg - 7)) kg++;
           o[36 + kg]++;
           o[52 + kg] += v;
+#ifdef RT_SURVEY_DUMP
+          dump[t].push_back((double)i);
+          dump[t].push_back((double)v);
+          for (int q = 7; q < 18; q++) dump[t].push_back(td[q]);
+#endif
         }
       }
     });
   for (auto& x : th) x.join();
+#ifdef RT_SURVEY_DUMP
+  if (const char* fn = getenv("RT_SURVEY_DUMP_FILE")) {
+    FILE* fo = fopen(fn, "wb");
+    for (auto& d : dump) fwrite(d.data(), sizeof(double), d.size(), fo);
+    fclose(fo);
+  }
+#endif
   for (int k = 0; k < 72; k++) {
     out[k] = 0;
     for (int t = 0; t < threads; t++) out[k] += part[72 * (size_t)t + k];
@@ -1345,6 +1577,43 @@ extern "C" int rt_cand_survey_host(const CandParams* p, const float* tri, const 
   unsigned long long nbad = 0;
   for (int t = 0; t < threads; t++) nbad += bad[t];
   return nbad ? -1 : 0;
+}
+
+// Host sample of the per-tile refinement (tests: tests/test_exact.py checks
+// each dropped entry against the reference's float test on every camera
+// sample of its tile): every stride-th (prim, tile) entry of a refined
+// footprint (rtc::refined_footprint; no leaf boxes), 4 words each: prim, tx,
+// ty, kept.  Returns the entries written (at most cap); *total = all sampled.
+extern "C" size_t rt_cand_refine_sample_host(const CandParams* p, const float* tri, uint32_t stride,
+                                             uint32_t* out, size_t cap, size_t* total) {
+  const int threads = 8;
+  std::vector<std::vector<uint32_t>> part(threads);
+  std::vector<std::thread> th;
+  if (stride < 1) stride = 1;
+  for (int t = 0; t < threads; t++)
+    th.emplace_back([&, t]() {
+      for (uint32_t i = (uint32_t)t; i < p->nprim; i += (uint32_t)threads) {
+        rtc::Footprint fp;
+        const float* rec = tri + 12 * (size_t)i;
+        if (rtc::classify(*p, rec, nullptr, fp) != rtc::FOOTPRINT || !rtc::refined_footprint(*p, fp)) continue;
+        uint64_t k = 0;
+        rtc::raster(*p, fp, [&](uint32_t tl) {
+          if (((uint64_t)i * 7919u + k++) % stride != 0) return;
+          int tx, ty;
+          rt_tile_xy(tl, (uint32_t)p->rank, (uint32_t)p->nranks, (uint32_t)p->blocks_x, (uint32_t)p->tb, &tx, &ty);
+          const uint32_t e[4] = {i, (uint32_t)tx, (uint32_t)ty, rtc::tile_keep(*p, rec, tx, ty) ? 1u : 0u};
+          part[t].insert(part[t].end(), e, e + 4);
+        });
+      }
+    });
+  for (auto& x : th) x.join();
+  size_t n = 0, all = 0;
+  for (auto& v : part) {
+    all += v.size() / 4;
+    for (size_t j = 0; j + 4 <= v.size() && n < cap; j += 4, n++) std::memcpy(out + 4 * n, &v[j], 16);
+  }
+  *total = all;
+  return n;
 }
 
 // Host check of the device-built lists of one frame (tests): every prim the
@@ -1389,9 +1658,14 @@ extern "C" int rt_cand_verify_host(const CandParams* p, const float* tri, const 
           continue;
         }
         if (c != rtc::FOOTPRINT) continue;  // safe after all (leaf box): no tiles
+        // a tall footprint's tiles (rtc::refined_footprint) refined per tile when p->refine
+        const bool refine = p->refine && rtc::refined_footprint(*p, fp);
+        const float* rec = tri + 12 * (size_t)prim;
         uint32_t n = 0;
         rtc::raster(*p, fp, [&](uint32_t t) {
-          if (t < ntiles) pairs[ti].push_back((uint64_t)t << 32 | prim);
+          int tx, ty;
+          rt_tile_xy(t, (uint32_t)p->rank, (uint32_t)p->nranks, (uint32_t)p->blocks_x, (uint32_t)p->tb, &tx, &ty);
+          if (t < ntiles && (!refine || rtc::tile_keep(*p, rec, tx, ty))) pairs[ti].push_back((uint64_t)t << 32 | prim);
           n++;
         });
         if (n == 0) continue;  // the device keeps no footprint without tiles
@@ -1566,10 +1840,10 @@ extern "C" hipError_t rt_cand_bounds(const uint32_t* keys, uint32_t n, uint32_t*
 
 
 extern "C" hipError_t rt_cand_route(uint32_t* keys, uint32_t n, int tiles_x, int nranks, int blocks_x, int tb,
-                                    uint32_t tpr, hipStream_t s) {
+                                    uint32_t tpr, uint32_t drop_key, hipStream_t s) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(rtc::route_kernel, dim3((n + 255) / 256), dim3(256), 0, s, keys, n, tiles_x, nranks, blocks_x,
-                     tb, tpr);
+                     tb, tpr, drop_key);
   return hipGetLastError();
 }
 

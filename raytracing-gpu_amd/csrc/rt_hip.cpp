@@ -120,6 +120,13 @@ struct rt_hip_ctx {
   size_t tile_cycles_cap = 0, tile_cycles_n = 0;
   // exact camera rays (csrc/rt_cand.hip)
   int exact_camera = 1;
+  // the big footprints' entries refined per tile (rt_hip_set_camera_refine,
+  // default on; RT_CAND_REFINE=0 at context creation turns it off)
+#ifndef RT_CAND_REFINE_DEFAULT
+#define RT_CAND_REFINE_DEFAULT 1
+#endif
+  int cand_refine = RT_CAND_REFINE_DEFAULT;
+  const uint32_t* d_cand_valid = nullptr;  // device word: the last built lists' entries with a tile
   double bound_scale = 1.0;  // 1 = the proven float-MT error bound (tools/mt_bound.py)
   float4* d_tri_prim = nullptr;  // prim-order records (== d_tri for FLAT)
   uint32_t nprim = 0;
@@ -523,6 +530,7 @@ extern "C" int rt_hip_create(int device, const rt_scene* scene, int accel, rt_hi
   auto t1 = std::chrono::steady_clock::now();
 
   rt_hip_ctx* c = new rt_hip_ctx();
+  if (const char* e = std::getenv("RT_CAND_REFINE")) c->cand_refine = std::atoi(e) != 0;  // A/B knob
   c->device = device;
   c->accel = dev_build ? (fs.ntri ? RT_ACCEL_OCTREE : RT_ACCEL_FLAT) : accel;
   c->nrec = (uint32_t)fs.nrec;
@@ -724,10 +732,41 @@ extern "C" int rt_hip_set_policy(rt_hip_ctx* c, int policy) {
   return RT_OK;
 }
 
+extern "C" int rt_hip_set_camera_refine(rt_hip_ctx* c, int enable) {
+  if (!c) return rt_set_error(RT_EINVAL, "null context");
+  c->cand_refine = enable ? 1 : 0;
+  return RT_OK;
+}
+
 extern "C" int rt_hip_set_camera_bound_scale(rt_hip_ctx* c, double scale) {
   if (!c || !(scale > 0.0)) return rt_set_error(RT_EINVAL, "bad bound scale");
   c->bound_scale = scale;
   return RT_OK;
+}
+
+extern "C" int rt_cand_refine_sample(const rt_scene* scene, float eps_ulps, double bound_scale, unsigned stride,
+                                     unsigned* out, size_t cap, size_t* n, size_t* total) {
+  if (!scene || (!out && cap) || !n || !total) return rt_set_error(RT_EINVAL, "null argument");
+  rt_frame f;
+  int rc = rt_frame_from_camera(&scene->camera, &f);
+  if (rc) return rc;
+  rt_flat_scene fs;
+  rc = rt_flatten(scene, RT_ACCEL_FLAT, &fs);
+  if (rc) return rc;
+  float sc[3], sr = 0;
+  for (int a = 0; a < 3; a++) {  // as rt_hip_create
+    float lo = fs.ntri ? fs.scene_lo[a] : 0.0f, hi = fs.ntri ? fs.scene_hi[a] : 0.0f;
+    sc[a] = 0.5f * (lo + hi);
+    sr = std::fmax(sr, 0.5f * (hi - lo));
+  }
+  CandParams cp;
+  rc = cand_params(&f, sc, sr, eps_ulps, bound_scale, 0, 1, &cp);
+  if (!rc) {
+    cp.nprim = (uint32_t)fs.ntri;
+    *n = rt_cand_refine_sample_host(&cp, fs.tri, stride, out, cap, total);
+  }
+  rt_flat_free(&fs);
+  return rc;
 }
 
 extern "C" int rt_cand_survey(const rt_scene* scene, float eps_ulps, double bound_scale, int threads,
@@ -831,6 +870,8 @@ static int cand_verify(rt_hip_ctx* c, const rt_frame* f, KParams kp, int compat,
   if (rc) return rc;
   cp.nprim = c->nprim;
   const uint32_t nt = (uint32_t)cp.ntiles_local;
+  cp.refine = c->cand_refine ? 1u : 0u;
+  cp.drop_key = nt;
   uint32_t ctr[4];
   HIP_TRY(hipMemcpy(ctr, c->d_cand_ctr, sizeof ctr, hipMemcpyDeviceToHost));
   const uint32_t nlist = ctr[3];
@@ -1015,6 +1056,12 @@ static int cand_params(const rt_frame* f, const float scene_c[3], float scene_r,
   cp.ginv[1] = -g01 / det;
   cp.ginv[2] = g00 / det;
   cp.gscale = std::sqrt(cp.ginv[0] * cp.ginv[0] + 2 * cp.ginv[1] * cp.ginv[1] + cp.ginv[2] * cp.ginv[2]);
+  {
+    const double pc[3] = {-cpos[0], -cpos[1], -cpos[2]};
+    const double pu = d3dot(pc, u), pv = d3dot(pc, v);
+    cp.k0 = cp.ginv[0] * pu + cp.ginv[1] * pv;
+    cp.l0 = cp.ginv[1] * pu + cp.ginv[2] * pv;
+  }
   const int W = f->width, H = f->height;
   cp.compat = compat;
   if (compat) {
@@ -1221,6 +1268,8 @@ static int cand_build(rt_hip_ctx* c, CandParams& cp, hipStream_t s, uint32_t glo
   cp.item_cap = c->cand_item_cap < kItemCap ? c->cand_item_cap : kItemCap;
   cp.wave_items = c->d_cand_wave_items;
   cp.wave_base = c->d_cand_wave_base;
+  cp.refine = c->cand_refine ? 1u : 0u;
+  cp.drop_key = (uint32_t)cp.ntiles_local;  // sorts after the tiles (their keys are < ntiles_local)
   // (ctr[0 .. 7] and visits[np] are zeroed by quick_kernel)
   size_t tb = 0;
   HIP_TRY(rt_cand_scan(c->d_cand_visits, c->d_cand_off, (uint32_t)np, nullptr, &tb, s));
@@ -1311,9 +1360,10 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
   if (rc) return rc;
   rc = cand_tile_buffers(c, nt);
   if (rc) return rc;
-  // keys are tiles < nt (a key of nt would need one more bit: nt + 1 keys)
+  // keys are tiles < nt, or nt for an entry the refinement dropped: nt + 1 keys
   rc = cand_sort(c, c->d_cand_keys, c->d_cand_keys2, c->d_cand_vals, c->d_cand, total, nt + 1, s);
   if (rc) return rc;
+  // start[nt] = the entries with a tile (the dropped ones sort after them)
   HIP_TRY(rt_cand_bounds(c->d_cand_keys2, total, c->d_cand_start, (uint32_t)nt, s));
   // the sorted keys are spent: their buffer takes the per-entry skip bounds
   float* entry_skip = (float*)c->d_cand_keys2;
@@ -1325,7 +1375,8 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
   kp->cand_global = c->d_cand_global;
   kp->n_cand_global = nglobal;
   kp->cand_skip = entry_skip;
-  c->cand_entries = total;
+  c->cand_entries = total;  // until rt_hip_stats reads start[nt]
+  c->d_cand_valid = c->cand_refine ? c->d_cand_start + nt : nullptr;
   c->cand_global = nglobal;
   c->cand_prims = 0;  // not counted separately (entries and globals are)
   return RT_OK;
@@ -1356,12 +1407,14 @@ extern "C" int rt_hip_cand_produce(rt_hip_ctx* c, const rt_frame* f, int rank, i
   if (rc) return rc;
   const uint32_t tpr = (uint32_t)rt_hip_tiles_per_rank(f->width, f->height, nranks);
   const int tb = rt_block_side(nranks);
-  HIP_TRY(rt_cand_route(c->d_cand_keys, total, cp.tiles_x, nranks, rt_blocks_x(cp.tiles_x, tb), tb, tpr, s));
+  HIP_TRY(rt_cand_route(c->d_cand_keys, total, cp.tiles_x, nranks, rt_blocks_x(cp.tiles_x, tb), tb, tpr, cp.drop_key,
+                        s));
   HIP_TRY(rt_cand_route_globals(c->d_cand_global, nglobal, nranks, tpr, c->d_cand_keys + total,
                                 c->d_cand_vals + total, s));
   const uint32_t n = total + nglobal * (uint32_t)nranks;
+  // keys < nranks (tpr + 1), or that for an entry the refinement dropped
   rc = cand_sort(c, c->d_cand_keys, c->d_cand_keys2, c->d_cand_vals, c->d_cand, n,
-                 (size_t)nranks * (tpr + 1), s);
+                 (size_t)nranks * (tpr + 1) + 1, s);
   if (rc) return rc;
   if ((size_t)nranks + 1 > c->rstart_cap) {
     (void)hipFree(c->d_rstart);
@@ -1388,7 +1441,7 @@ extern "C" int rt_hip_cand_produce(rt_hip_ctx* c, const rt_frame* f, int rank, i
   HIP_TRY(hipStreamSynchronize(s));
   for (int d = 0; d < nranks; d++) counts[d] = c->h_rstart[d + 1] - c->h_rstart[d];
   *nglobal_out = nglobal;
-  c->send_n = n;
+  c->send_n = c->h_rstart[nranks];  // the routed entries (the refinement's dropped ones sort after them)
   return RT_OK;
 }
 
@@ -1526,6 +1579,7 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
     // renders nothing; its tile buffer (sized by rank 0) stays as it is and
     // gathers as padding.  Its stats read 0.
     c->cand_prims = c->cand_entries = c->cand_global = 0;
+    c->d_cand_valid = nullptr;
     hipEvent_t* ev = c->ev[c->frames % RT_TIMED_FRAMES];
     if (c->timing) HIP_TRY(hipEventRecord(ev[0], s));
     HIP_TRY(hipMemsetAsync(c->d_counter, 0, kFrameCounterBytes, s));
@@ -1594,6 +1648,7 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
     p.sh_omax = c->sh_omax;
   }
   c->cand_prims = c->cand_entries = c->cand_global = 0;
+  c->d_cand_valid = nullptr;
   hipEvent_t* ev = c->ev[c->frames % RT_TIMED_FRAMES];
   if (c->timing) HIP_TRY(hipEventRecord(ev[0], s));
   if (c->accel == RT_ACCEL_OCTREE && c->d_node && c->exact_camera) {
@@ -1606,6 +1661,7 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
       p.tile_order = c->ext.tile_order;
       p.tri_prim = c->ext.tri_prim;
       c->cand_entries = c->ext_total;
+      c->d_cand_valid = nullptr;
       c->cand_global = c->ext.n_cand_global;
       c->cand_prims = 0;
     } else {
@@ -1816,7 +1872,13 @@ extern "C" int rt_hip_stats(rt_hip_ctx* c, rt_stats* out) {
   hipStream_t s = c->last_stream ? c->last_stream : c->stream;
   HIP_TRY(hipMemcpyAsync(hs, c->d_stats, sizeof hs, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(hc, c->d_hit_count, sizeof hc, hipMemcpyDeviceToHost, s));
+  uint32_t valid = 0;
+  if (c->d_cand_valid) HIP_TRY(hipMemcpyAsync(&valid, c->d_cand_valid, sizeof valid, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  if (c->d_cand_valid) {
+    c->cand_entries = valid;
+    c->d_cand_valid = nullptr;
+  }
   for (int k = 0; k < RT_NSTATS; k++) {  // the copies of each counter (RT_STAT_SETS)
     h[k] = 0;
     for (int set = 0; set < RT_STAT_SETS; set++) h[k] += hs[set * RT_STAT_STRIDE + k];
@@ -2011,6 +2073,7 @@ extern "C" int rt_hip_render_compat(rt_hip_ctx* c, const rt_camera* cam, unsigne
   // exact camera rays in this mode too: the candidate lists of the 3x frame's
   // one-sample-per-pixel camera (csrc/rt_cand.hip CandParams::compat)
   c->cand_prims = c->cand_entries = c->cand_global = 0;
+  c->d_cand_valid = nullptr;
   if (c->accel == RT_ACCEL_OCTREE && c->d_node && c->exact_camera) {
     rc = cand_prepare(c, &f, &p, s, 1);
     if (rc) {

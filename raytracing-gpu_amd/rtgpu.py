@@ -173,6 +173,9 @@ _PROTOS = [
     ("rt_hip_frame_kernel_times", C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_float),
                                             C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     ("rt_hip_set_camera_bound_scale", C.c_int, [C.c_void_p, C.c_double]),
+    ("rt_hip_set_camera_refine", C.c_int, [C.c_void_p, C.c_int]),
+    ("rt_cand_refine_sample", C.c_int, [C.POINTER(SceneStruct), C.c_float, C.c_double, C.c_uint, C.c_void_p,
+                                        C.c_size_t, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]),
     ("rt_cand_survey", C.c_int, [C.POINTER(SceneStruct), C.c_float, C.c_double, C.c_int, C.c_int,
                                  C.POINTER(C.c_ulonglong)]),
     ("rt_hip_assemble", C.c_int, [C.c_void_p, C.POINTER(Frame), C.c_void_p, C.c_int, C.c_void_p,
@@ -375,12 +378,29 @@ def cand_survey(scene, eps_ulps=64.0, bound_scale=1.0, threads=8, leaves=False):
     _check(lib().rt_cand_survey(scene.ptr, eps_ulps, bound_scale, threads, 1 if leaves else 0, out),
            "cand_survey")
     r = dict(zip(("safe", "footprint", "global", "entries"), (int(x) for x in out[:4])))
+    # the entries the device lists hold with the per-tile refinement (big
+    # footprints refined, csrc/rt_cand.hip tile_keep); the big footprints'
+    # entries before and after it
+    r["refined"] = int(out[68])
+    r["big_entries"], r["big_kept"] = int(out[69]), int(out[70])
     r["hist"] = [(1 << k, int(out[4 + k]), int(out[20 + k])) for k in range(16) if out[4 + k]]
     # footprint prims by how far their T_D box reaches beyond the triangle, in
     # units of the walk's slack: (lower edge 2^(k-8), prims, entries)
     r["growth_hist"] = [(2.0 ** (k - 8) if k else 0.0, int(out[36 + k]), int(out[52 + k]))
                         for k in range(16) if out[36 + k]]
     return r
+
+
+def cand_refine_sample(scene, stride=1, cap=1 << 20, eps_ulps=64.0, bound_scale=1.0):
+    """Host-only: every stride-th entry of the refined candidate footprints
+    as rows (prim, tile x, tile y, kept) -- csrc/rt_cand.hip tile_keep -- and
+    the number sampled."""
+    import numpy as np
+    out = np.zeros((cap, 4), np.uint32)
+    n, total = C.c_size_t(0), C.c_size_t(0)
+    _check(lib().rt_cand_refine_sample(scene.ptr, eps_ulps, bound_scale, stride, out.ctypes.data, cap,
+                                       C.byref(n), C.byref(total)), "cand_refine_sample")
+    return out[:n.value], total.value
 
 
 def device_count():
@@ -494,6 +514,10 @@ class Context:
         """Octree traversal policy (rt_hip_set_policy): 0 default, 1 per-lane,
         2 staged packet, 3 default + staged directional shadows."""
         _check(lib().rt_hip_set_policy(self.h, int(policy)), "policy")
+
+    def set_camera_refine(self, on=True):
+        """Per-tile refinement of the big candidate footprints (default on)."""
+        _check(lib().rt_hip_set_camera_refine(self.h, 1 if on else 0), "camera_refine")
 
     def set_camera_bound_scale(self, scale):
         _check(lib().rt_hip_set_camera_bound_scale(self.h, float(scale)), "bound_scale")

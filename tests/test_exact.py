@@ -87,3 +87,32 @@ def test_candidate_survey_reference_scene(scene_dir):
     s.set_size(1920, 1080)
     r = rtgpu.cand_survey(s, 64.0, 1.0)
     assert r["safe"] + r["footprint"] + r["global"] == s.triangle_count
+
+
+@pytest.mark.parametrize("case", ["small", "c5"])
+def test_tile_refinement_drops_only_tiles_the_reference_never_accepts(case):
+    """The per-tile refinement of the camera candidate lists (csrc/rt_cand.hip
+    tile_keep) drops a (triangle, tile) entry only where its proof says no
+    camera sample of the tile can pass the float test.  Checked against the
+    oracle's restatement of cpu/hit.c:15-44 on every camera sample
+    (cpu/raytracer.c:50-61) of the dropped tiles: none may pass even the a, u,
+    v stages.  The kept entries include the tiles the triangle is really hit
+    in (the geometry of the tile mapping and projection is right).  c5: the
+    headline scene, every 200th refined entry."""
+    import rtgpu
+    import oracle as orc
+    if case == "small":
+        s = rtgpu.Scene.synthetic(4, 4, 1200, seed=0x5EED, width=480, height=270)
+        stride = 1
+    else:
+        s = rtgpu.Scene.synthetic(32, 32, 9776, seed=0x5EED, width=3840, height=2160)
+        stride = 200
+    rows, total = rtgpu.cand_refine_sample(s, stride=stride, cap=1 << 20)
+    assert len(rows) == total > 0
+    drop = rows[:, 3] == 0
+    assert drop.sum() > 0 and (~drop).sum() > 0
+    tris = s.triangles_array()
+    rects = np.stack([rows[:, 2] * 8, rows[:, 1] * 8, np.full(len(rows), 8), np.full(len(rows), 8)], 1)
+    acc = orc.camera_tri_accepts(s.ptr, tris[rows[:, 0]], rects)
+    assert int(acc[drop, 1].max()) == 0, rows[drop][acc[drop, 1] > 0][:8]
+    assert int((acc[~drop, 0] > 0).sum()) > 0  # real hits live in kept tiles
