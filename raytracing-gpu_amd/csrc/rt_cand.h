@@ -30,6 +30,7 @@ struct CandParams {
   double plane;           // (C - pos) . n
   double ginv[3];         // inverse Gram matrix of (u, v): [g0 g1; g1 g2]
   double k0, l0;          // image coordinates of pos - C: ginv (u . (pos - C), v . (pos - C))
+  double tile_hd;         // world half diagonal of a tile's sample rectangle, hk |u| + hl |v|
   double gscale;          // a bound of its norm
   double lmax;            // max |o - pos| over the frame's camera origins
   double omax;            // max |o| over them

@@ -740,8 +740,8 @@ RTC_FN bool tile_keep(const CandParams& p, const TileTri& t, int tx, int ty) {
     sm[a] = (fabs(oc - t.v0[a]) + w + p.dorig) * (1.0 + 1e-9);
   }
   const double bc = dot3(po, t.nh), bw = fabs(dot3(p.u, t.nh)) * hk + fabs(dot3(p.v, t.nh)) * hl;
-  // |pos - o| within the centre's +- the tile's half diagonal
-  const double hd = hk * norm3(p.u) + hl * norm3(p.v);
+  // |pos - o| within the centre's +- the tile's half diagonal (hk |u| + hl |v|)
+  const double hd = p.tile_hd;
   const double rc = norm3(po);
   const double rmn = rc - hd - p.dorig, rmx = (rc + hd + p.dorig) * (1.0 + 1e-9);
   if (!(rmn > 1e-6)) return true;
@@ -755,24 +755,29 @@ RTC_FN bool tile_keep(const CandParams& p, const TileTri& t, int tx, int ty) {
     M[i] = dm[j] * t.ae2[k] + dm[k] * t.ae2[j];
     N[i] = sm[j] * t.ae1[k] + sm[k] * t.ae1[j];
   }
+  // the componentwise bounds alone (each of them and classify's Cauchy-Schwarz
+  // ones is a bound on its own; for a tile's narrow cone these are the
+  // smaller)
   const double cw = p.c_dot / 8.6 * 6.01 * kEps, ca = p.c_a / 7.2 * 5.01 * kEps;
-  const double smax = norm3(sm);
-  const double e_sh = fmin(cw * (sm[0] * M[0] + sm[1] * M[1] + sm[2] * M[2]), p.c_dot * kEps * smax * kDMax * t.l2);
-  const double e_dq = fmin(cw * (dm[0] * N[0] + dm[1] * N[1] + dm[2] * N[2]), p.c_dot * kEps * smax * kDMax * t.l1);
-  const double e_a = fmin(ca * (t.ae1[0] * M[0] + t.ae1[1] * M[1] + t.ae1[2] * M[2]),
-                          p.c_a * kEps * t.l1 * t.l2 * kDMax);
+  const double e_sh = cw * (sm[0] * M[0] + sm[1] * M[1] + sm[2] * M[2]);
+  const double e_dq = cw * (dm[0] * N[0] + dm[1] * N[1] + dm[2] * N[2]);
+  const double e_a = ca * (t.ae1[0] * M[0] + t.ae1[1] * M[1] + t.ae1[2] * M[2]);
   // grazing cosine of the tile's rays: |b| over the rectangle is in [bl, bh]
   const double bl = fmax(0.0, fabs(bc) - bw), bh = fabs(bc) + bw;
   const double cmax = fmin(1.0, (bh + p.dorig) * irn + 8.0 * kEps);
   if (kDMax * t.nl * cmax + e_a < kAMin) return false;  // |a| < 1e-7 for every ray of the tile
-  const double cmin = fmax(0.0, (bl - p.dorig) / rmx - 8.0 * kEps);
-  const double a_lb = fmax(kAMin, kDMin * t.nl * cmin - e_a);
-  const double ia = 1.0 / a_lb;
-  const double rho = e_a * ia;
-  if (!(rho < 0.5)) return true;
-  const double i1r = 1.0 / (1.0 - rho);
-  const double du = e_sh * ia * i1r, dv = e_dq * ia * i1r;
-  const double dw = (4.0 * kEps + (e_sh + e_dq) * ia + rho) * i1r;
+  // a_lb = max(kAMin, dmin nl cmin - e_a), cmin = (bl - dorig) / rmx - 8 eps,
+  // kept as the fraction num / rmx; rho = e_a / a_lb < 1/2 <=> 2 e_a < a_lb
+  const double num = kDMin * t.nl * (bl - p.dorig - 8.0 * kEps * rmx) - e_a * rmx;
+  const bool clamp = !(num > kAMin * rmx);
+  if (clamp ? !(2.0 * e_a < kAMin) : !(2.0 * e_a * rmx < num)) return true;
+  // 1 / (a_lb (1 - rho)) = 1 / (a_lb - e_a): du = e_sh / (a_lb - e_a), and
+  // dw = (4 eps + (e_sh + e_dq) / a_lb + rho) / (1 - rho)
+  //    = 4 eps / (1 - rho) + (e_sh + e_dq + e_a) / (a_lb - e_a)
+  //   <= 8 eps + (e_sh + e_dq + e_a) / (a_lb - e_a)
+  const double iq = clamp ? 1.0 / (kAMin - e_a) : rmx / (num - e_a * rmx);
+  const double du = e_sh * iq, dv = e_dq * iq;
+  const double dw = 8.0 * kEps + (e_sh + e_dq + e_a) * iq;
   // T_D's corners relative to the eye, Y_k = P_k - pos, and their image
   // points in homogeneous form H_k = (K0 yn + plane alpha, L0 yn + plane
   // beta, yn) ~ (K_k, L_k, 1) (yn = Y . n, alpha / beta = Y's image-axis

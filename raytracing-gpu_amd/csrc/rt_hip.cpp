@@ -1062,6 +1062,10 @@ static int cand_params(const rt_frame* f, const float scene_c[3], float scene_r,
     cp.k0 = cp.ginv[0] * pu + cp.ginv[1] * pv;
     cp.l0 = cp.ginv[1] * pu + cp.ginv[2] * pv;
   }
+  // a tile's sample rectangle: 3.75 (3.5 in the compatibility mode) samples
+  // either side of its centre on each axis (rt_cand.hip tile_keep)
+  const double half = compat ? 3.5 : 3.75;
+  cp.tile_hd = (half * std::sqrt(d3dot(u, u)) + half * std::sqrt(d3dot(v, v))) * (1.0 + 1e-12);
   const int W = f->width, H = f->height;
   cp.compat = compat;
   if (compat) {
