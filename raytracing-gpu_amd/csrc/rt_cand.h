@@ -30,7 +30,13 @@ struct CandParams {
   double plane;           // (C - pos) . n
   double ginv[3];         // inverse Gram matrix of (u, v): [g0 g1; g1 g2]
   double k0, l0;          // image coordinates of pos - C: ginv (u . (pos - C), v . (pos - C))
-  double tile_hd;         // world half diagonal of a tile's sample rectangle, hk |u| + hl |v|
+  // tile (tx, ty)'s sample rectangle (rt_cand.hip tile_keep): centre (k00 +
+  // tx dk, l00 + ty dl), half sides hk, hl; pos - its film centre = p00 - tx du
+  // - ty dv (du = dk u, dv = dl v); per axis |u_i| hk + |v_i| hl; the world
+  // half diagonal hk |u| + hl |v|
+  double tile_k00, tile_l00, tile_dk, tile_dl, tile_hk, tile_hl;
+  double tile_p00[3], tile_du[3], tile_dv[3], tile_w[3];
+  double tile_hd;
   double gscale;          // a bound of its norm
   double lmax;            // max |o - pos| over the frame's camera origins
   double omax;            // max |o| over them

@@ -683,29 +683,75 @@ __host__ __device__ inline uint32_t raster_count(const CandParams& p, const Foot
 // false when the tile's samples, projected through the eye and widened by
 // the camera lines' float deviation (classify's dimg), provably miss it (or
 // no ray of the tile reaches |a| >= 1e-7).  true whenever unsure.
-// The triangle's part (once per footprint):
+// The triangle's part (once per footprint; the big emission keeps it in LDS).
+// With Y = P - pos for a point P = v0 + cu e1 + cv e2 of the triangle's
+// plane, the homogeneous image point of P (classify's projection through the
+// eye, H = (k0 yn + plane (g0 yu + g1 yv), l0 yn + plane (g1 yu + g2 yv), yn),
+// yn / yu / yv = Y . n / u / v) is linear in (cu, cv): H = B0 + cu B1 + cv B2.
 struct TileTri {
-  double v0[3], e1[3], e2[3], ae1[3], ae2[3];
-  double nh[3];   // unit normal
-  double nl;      // |e1 x e2|
-  double l1, l2;  // |e1|, |e2|
+  double pv0[3];           // pos - v0
+  double ae1[3], ae2[3];   // |e1_i|, |e2_i|
+  double nl;               // |e1 x e2|
+  double bcp, bcx, bcy;    // grazing offset (pos - o) . nh at tile (tx, ty): bcp - tx bcx - ty bcy
+  double bw;               // its spread over a tile's rectangle
+  double B[3][3];          // H of v0 - pos, e1, e2 (as points / directions)
+  double ym[3];            // L1 norms of v0 - pos, e1, e2 (bounds of |Y|)
 };
-RTC_FN bool tile_tri(const float* r, TileTri& t) {
+// The frame's part (CandParams' tile_* constants and the bound's terms).
+struct TileFrame {
+  double k00, l00, dk, dl, hk, hl, hd;
+  double p00[3], du[3], dv[3], w[3];
+  double dorig, cw, ca, gscale, dline, lmax;
+};
+RTC_FN void tile_frame(const CandParams& p, TileFrame& f) {
+  f.k00 = p.tile_k00;
+  f.l00 = p.tile_l00;
+  f.dk = p.tile_dk;
+  f.dl = p.tile_dl;
+  f.hk = p.tile_hk;
+  f.hl = p.tile_hl;
+  f.hd = p.tile_hd;
   for (int a = 0; a < 3; a++) {
-    t.v0[a] = r[a];
-    t.e1[a] = r[3 + a];
-    t.e2[a] = r[6 + a];
-    t.ae1[a] = fabs(t.e1[a]);
-    t.ae2[a] = fabs(t.e2[a]);
+    f.p00[a] = p.tile_p00[a];
+    f.du[a] = p.tile_du[a];
+    f.dv[a] = p.tile_dv[a];
+    f.w[a] = p.tile_w[a];
   }
-  const double n[3] = {t.e1[1] * t.e2[2] - t.e1[2] * t.e2[1], t.e1[2] * t.e2[0] - t.e1[0] * t.e2[2],
-                       t.e1[0] * t.e2[1] - t.e1[1] * t.e2[0]};
+  f.dorig = p.dorig;
+  f.cw = p.c_dot / 8.6 * 6.01 * kEps;
+  f.ca = p.c_a / 7.2 * 5.01 * kEps;
+  f.gscale = p.gscale;
+  f.dline = p.dline;
+  f.lmax = p.lmax;
+}
+RTC_FN bool tile_tri(const CandParams& p, const float* r, TileTri& t) {
+  double v0[3], e1[3], e2[3];
+  for (int a = 0; a < 3; a++) {
+    v0[a] = r[a];
+    e1[a] = r[3 + a];
+    e2[a] = r[6 + a];
+    t.pv0[a] = p.pos[a] - v0[a];
+    t.ae1[a] = fabs(e1[a]);
+    t.ae2[a] = fabs(e2[a]);
+  }
+  const double n[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
   t.nl = norm3(n);
-  t.l1 = norm3(t.e1);
-  t.l2 = norm3(t.e2);
   if (!(t.nl > 0.0)) return false;
   const double inl = 1.0 / t.nl;
-  for (int a = 0; a < 3; a++) t.nh[a] = n[a] * inl;
+  const double nh[3] = {n[0] * inl, n[1] * inl, n[2] * inl};
+  t.bcp = dot3(p.tile_p00, nh);
+  t.bcx = dot3(p.tile_du, nh);
+  t.bcy = dot3(p.tile_dv, nh);
+  t.bw = fabs(dot3(p.u, nh)) * p.tile_hk + fabs(dot3(p.v, nh)) * p.tile_hl;
+  const double* V[3] = {t.pv0, e1, e2};
+  for (int k = 0; k < 3; k++) {
+    const double sgn = k == 0 ? -1.0 : 1.0;  // v0 - pos = -(pos - v0)
+    const double yn = sgn * dot3(V[k], p.n), yu = sgn * dot3(V[k], p.u), yv = sgn * dot3(V[k], p.v);
+    t.B[k][0] = p.k0 * yn + p.plane * (p.ginv[0] * yu + p.ginv[1] * yv);
+    t.B[k][1] = p.l0 * yn + p.plane * (p.ginv[1] * yu + p.ginv[2] * yv);
+    t.B[k][2] = yn;
+    t.ym[k] = fabs(V[k][0]) + fabs(V[k][1]) + fabs(V[k][2]);
+  }
   return true;
 }
 
@@ -713,94 +759,76 @@ RTC_FN bool tile_tri(const float* r, TileTri& t) {
 // f64): the affine quantities' extremes over the tile's sample rectangle in
 // closed form (|f_c| + |f_k| hk + |f_l| hl), and T_D's projection tested in
 // homogeneous image coordinates (no per-corner division).
-RTC_FN bool tile_keep(const CandParams& p, const TileTri& t, int tx, int ty) {
-  // the tile's sample rectangle [kc -+ hk] x [lc -+ hl] (pixel_range's inverse)
-  const double hw = (double)(p.W / 2), hh = (double)(p.H / 2);
-  const int c0 = tx * 8, r0 = ty * 8;
-  double kc, hk, lc, hl;
-  if (p.compat) {
-    kc = c0 + 3.5 - hw;
-    hk = 3.5;
-    lc = r0 + 3.5 - hh;
-    hl = 3.5;
-  } else {
-    kc = hw - c0 - 3.25;
-    hk = 3.75;
-    lc = hh - r0 - 3.25;
-    hl = 3.75;
-  }
-  // per axis max |pos_i - o_i|, max |o_i - v0_i| (o = C + k u + l v); the
-  // grazing offset b = (pos - o) . nh over the rectangle: [bc - bw, bc + bw]
+RTC_FN bool tile_keep(const TileFrame& p, const TileTri& t, int tx, int ty) {
+  // the tile's sample rectangle [kc -+ hk] x [lc -+ hl] (pixel_range's
+  // inverse, CandParams::tile_*), its centre o_c = C + kc u + lc v, and per
+  // axis max |pos_i - o_i| and max |o_i - v0_i| over it
+  // (fused multiply-adds throughout: these are bounds of our own, each
+  // rounding far inside their margins, and fma is exact IEEE on host and device)
+  const double dtx = (double)tx, dty = (double)ty;
+  const double kc = fma(dtx, p.dk, p.k00), lc = fma(dty, p.dl, p.l00);
   double pm[3], sm[3], po[3];
   for (int a = 0; a < 3; a++) {
-    const double oc = p.C[a] + kc * p.u[a] + lc * p.v[a];
-    const double w = fabs(p.u[a]) * hk + fabs(p.v[a]) * hl;
-    po[a] = p.pos[a] - oc;
-    pm[a] = fabs(po[a]) + w;
-    sm[a] = (fabs(oc - t.v0[a]) + w + p.dorig) * (1.0 + 1e-9);
+    po[a] = fma(-dtx, p.du[a], fma(-dty, p.dv[a], p.p00[a]));  // pos - o_c
+    pm[a] = fabs(po[a]) + p.w[a];
+    sm[a] = (fabs(t.pv0[a] - po[a]) + p.w[a] + p.dorig) * (1.0 + 1e-9);
   }
-  const double bc = dot3(po, t.nh), bw = fabs(dot3(p.u, t.nh)) * hk + fabs(dot3(p.v, t.nh)) * hl;
   // |pos - o| within the centre's +- the tile's half diagonal (hk |u| + hl |v|)
-  const double hd = p.tile_hd;
-  const double rc = norm3(po);
-  const double rmn = rc - hd - p.dorig, rmx = (rc + hd + p.dorig) * (1.0 + 1e-9);
+  const double rc = sqrt(fma(po[0], po[0], fma(po[1], po[1], po[2] * po[2])));
+  const double rmn = rc - p.hd - p.dorig, rmx = (rc + p.hd + p.dorig) * (1.0 + 1e-9);
   if (!(rmn > 1e-6)) return true;
   const double irn = 1.0 / rmn;
   // float origins within dorig, float directions within a few eps of pos - o
   double dm[3];
-  for (int a = 0; a < 3; a++) dm[a] = fmin(1.0, (pm[a] + p.dorig) * irn + 8.0 * kEps) * kDMax;
+  for (int a = 0; a < 3; a++) dm[a] = fmin(1.0, fma(pm[a] + p.dorig, irn, 8.0 * kEps)) * kDMax;
   double M[3], N[3];
   for (int i = 0; i < 3; i++) {
     const int j = (i + 1) % 3, k = (i + 2) % 3;
-    M[i] = dm[j] * t.ae2[k] + dm[k] * t.ae2[j];
-    N[i] = sm[j] * t.ae1[k] + sm[k] * t.ae1[j];
+    M[i] = fma(dm[j], t.ae2[k], dm[k] * t.ae2[j]);
+    N[i] = fma(sm[j], t.ae1[k], sm[k] * t.ae1[j]);
   }
   // the componentwise bounds alone (each of them and classify's Cauchy-Schwarz
   // ones is a bound on its own; for a tile's narrow cone these are the
   // smaller)
-  const double cw = p.c_dot / 8.6 * 6.01 * kEps, ca = p.c_a / 7.2 * 5.01 * kEps;
-  const double e_sh = cw * (sm[0] * M[0] + sm[1] * M[1] + sm[2] * M[2]);
-  const double e_dq = cw * (dm[0] * N[0] + dm[1] * N[1] + dm[2] * N[2]);
-  const double e_a = ca * (t.ae1[0] * M[0] + t.ae1[1] * M[1] + t.ae1[2] * M[2]);
+  const double cw = p.cw, ca = p.ca;
+  auto dotf = [](const double* a, const double* b) { return fma(a[0], b[0], fma(a[1], b[1], a[2] * b[2])); };
+  const double e_sh = cw * dotf(sm, M);
+  const double e_dq = cw * dotf(dm, N);
+  const double e_a = ca * dotf(t.ae1, M);
   // grazing cosine of the tile's rays: |b| over the rectangle is in [bl, bh]
-  const double bl = fmax(0.0, fabs(bc) - bw), bh = fabs(bc) + bw;
-  const double cmax = fmin(1.0, (bh + p.dorig) * irn + 8.0 * kEps);
+  const double bc = fma(-dtx, t.bcx, fma(-dty, t.bcy, t.bcp));
+  const double bl = fmax(0.0, fabs(bc) - t.bw), bh = fabs(bc) + t.bw;
+  const double cmax = fmin(1.0, fma(bh + p.dorig, irn, 8.0 * kEps));
   if (kDMax * t.nl * cmax + e_a < kAMin) return false;  // |a| < 1e-7 for every ray of the tile
   // a_lb = max(kAMin, dmin nl cmin - e_a), cmin = (bl - dorig) / rmx - 8 eps,
   // kept as the fraction num / rmx; rho = e_a / a_lb < 1/2 <=> 2 e_a < a_lb
-  const double num = kDMin * t.nl * (bl - p.dorig - 8.0 * kEps * rmx) - e_a * rmx;
+  const double num = fma(kDMin * t.nl, bl - p.dorig - 8.0 * kEps * rmx, -e_a * rmx);
   const bool clamp = !(num > kAMin * rmx);
   if (clamp ? !(2.0 * e_a < kAMin) : !(2.0 * e_a * rmx < num)) return true;
   // 1 / (a_lb (1 - rho)) = 1 / (a_lb - e_a): du = e_sh / (a_lb - e_a), and
   // dw = (4 eps + (e_sh + e_dq) / a_lb + rho) / (1 - rho)
   //    = 4 eps / (1 - rho) + (e_sh + e_dq + e_a) / (a_lb - e_a)
   //   <= 8 eps + (e_sh + e_dq + e_a) / (a_lb - e_a)
-  const double iq = clamp ? 1.0 / (kAMin - e_a) : rmx / (num - e_a * rmx);
+  const double iq = clamp ? 1.0 / (kAMin - e_a) : rmx / fma(-e_a, rmx, num);
   const double du = e_sh * iq, dv = e_dq * iq;
-  const double dw = 8.0 * kEps + (e_sh + e_dq + e_a) * iq;
-  // T_D's corners relative to the eye, Y_k = P_k - pos, and their image
-  // points in homogeneous form H_k = (K0 yn + plane alpha, L0 yn + plane
-  // beta, yn) ~ (K_k, L_k, 1) (yn = Y . n, alpha / beta = Y's image-axis
-  // coordinates through ginv): classify's lam = plane / yn, without dividing
-  double H[3][3], ymag = 1.0, ylo = 1e300, yhi = -1e300;
+  const double dw = fma(e_sh + e_dq + e_a, iq, 8.0 * kEps);
+  // T_D's corners (cu, cv) and their homogeneous image points H_k = B0 + cu
+  // B1 + cv B2 ~ (K_k, L_k, 1): classify's lam = plane / yn, without dividing
   const double cu[3] = {-du, 1.0 + dw + dv, -du}, cv[3] = {-dv, -dv, 1.0 + dw + du};
+  double H[3][3], ymag = 1.0, ylo = 1e300, yhi = -1e300;
   for (int k = 0; k < 3; k++) {
-    double Y[3];
-    for (int a = 0; a < 3; a++) Y[a] = t.v0[a] + cu[k] * t.e1[a] + cv[k] * t.e2[a] - p.pos[a];
-    const double yn = dot3(Y, p.n), yu = dot3(Y, p.u), yv = dot3(Y, p.v);
-    H[k][0] = p.k0 * yn + p.plane * (p.ginv[0] * yu + p.ginv[1] * yv);
-    H[k][1] = p.l0 * yn + p.plane * (p.ginv[1] * yu + p.ginv[2] * yv);
-    H[k][2] = yn;
-    ymag = fmax(ymag, fabs(Y[0]) + fabs(Y[1]) + fabs(Y[2]));
-    ylo = fmin(ylo, yn);
-    yhi = fmax(yhi, yn);
+    for (int c = 0; c < 3; c++) H[k][c] = fma(cu[k], t.B[1][c], fma(cv[k], t.B[2][c], t.B[0][c]));
+    ymag = fmax(ymag, fma(fabs(cu[k]), t.ym[1], fma(fabs(cv[k]), t.ym[2], t.ym[0])));
+    ylo = fmin(ylo, H[k][2]);
+    yhi = fmax(yhi, H[k][2]);
   }
   // every corner strictly on one side of the eye plane; the nearest point of
   // T_D is then at least min |yn| from the eye
   if (!(ylo > 1e-6 * ymag || yhi < -1e-6 * ymag)) return true;
   const double sg = ylo > 0.0 ? 1.0 : -1.0, rlo = fmin(fabs(ylo), fabs(yhi));
   const double dimg = 1.5 * p.gscale * (p.dline * (1.0 + p.lmax / rlo) + p.dorig) + 1e-3;
-  const double x0 = kc - hk - dimg, x1 = kc + hk + dimg, y0 = lc - hl - dimg, y1 = lc + hl + dimg;
+  const double x0 = kc - p.hk - dimg, x1 = kc + p.hk + dimg;
+  const double y0 = lc - p.hl - dimg, y1 = lc + p.hl + dimg;
   // separating axes: the rectangle's (K_k < x0 <=> sg H_k0 < sg x0 yn_k, ...)
   {
     bool lx = true, gx = true, ly = true, gy = true;
@@ -819,14 +847,14 @@ RTC_FN bool tile_keep(const CandParams& p, const TileTri& t, int tx, int ty) {
   // det[H_e; H_f; q] has the sign opposite to det[H_0; H_1; H_2] sg
   double c01[3], c12[3], c20[3];
   auto cross3 = [](const double* a, const double* b, double* c) {
-    c[0] = a[1] * b[2] - a[2] * b[1];
-    c[1] = a[2] * b[0] - a[0] * b[2];
-    c[2] = a[0] * b[1] - a[1] * b[0];
+    c[0] = fma(a[1], b[2], -a[2] * b[1]);
+    c[1] = fma(a[2], b[0], -a[0] * b[2]);
+    c[2] = fma(a[0], b[1], -a[1] * b[0]);
   };
   cross3(H[0], H[1], c01);
   cross3(H[1], H[2], c12);
   cross3(H[2], H[0], c20);
-  const double orient = dot3(H[2], c01) * sg;
+  const double orient = dotf(H[2], c01) * sg;
   if (orient == 0.0) return true;
   const double so = orient > 0.0 ? 1.0 : -1.0;
   const double* C3[3] = {c01, c12, c20};
@@ -841,7 +869,9 @@ RTC_FN bool tile_keep(const CandParams& p, const TileTri& t, int tx, int ty) {
 
 RTC_FN bool tile_keep(const CandParams& p, const float* r, int tx, int ty) {
   TileTri t;
-  return !tile_tri(r, t) || tile_keep(p, t, tx, ty);
+  TileFrame f;
+  tile_frame(p, f);
+  return !tile_tri(p, r, t) || tile_keep(f, t, tx, ty);
 }
 
 // A footprint is "big" -- counted and emitted by one wave, its tile rows
@@ -1170,8 +1200,6 @@ __global__ __launch_bounds__(64) void big_item_kernel(CandParams p) {
   const Footprint fp = p.fp[j];
   int r0, r1;
   if (!raster_rows(p, fp, r0, r1)) return;  // no entries, no items
-  TileTri tt;  // the triangle's part of the per-tile refinement, once per item
-  const bool refine = p.refine != 0u && refined_rows(r0, r1) && tile_tri((const float*)(p.tri + 3 * (size_t)prim), tt);
   uint32_t g0 = 0;  // entries of the footprint before this group of rows
   for (int gy = r0 >> 3; gy <= (r1 >> 3) && g0 < c1; gy += 64) {
     const int ty = gy + lane;
@@ -1213,14 +1241,46 @@ __global__ __launch_bounds__(64) void big_item_kernel(CandParams p) {
         }
         const int tx = kth_rank_col(p, rx[r][2 * iv], rx[r][2 * iv + 1], rf[r][iv], k);
         uint32_t rk;
-        const bool keep = !refine || tile_keep(p, tt, tx, rty[r]);
-        p.keys[base + e] = keep ? rt_tile_local(tx, rty[r], (uint32_t)p.nranks, (uint32_t)p.blocks_x,
-                                                (uint32_t)p.tb, &rk)
-                                : p.drop_key;
+        p.keys[base + e] = rt_tile_local(tx, rty[r], (uint32_t)p.nranks, (uint32_t)p.blocks_x,
+                                         (uint32_t)p.tb, &rk);
         p.vals[base + e] = prim;
       }
     }
     g0 += gt;
+  }
+}
+
+// The per-tile refinement (CandParams::refine) as its own pass over
+// big_item_kernel's items: each wave re-reads its chunk's keys and rewrites
+// the dropped ones with drop_key.  A pass of its own, with the triangle's and
+// the frame's parts in LDS and re-read per entry, runs at 80 VGPRs and 6
+// waves per SIMD; inside big_item_kernel the same test held 137-175 VGPRs (2-3
+// waves) and the frame took 0.1 ms longer on C5 (profiles/r06e/ab.log).
+__global__ __launch_bounds__(64) void refine_kernel(CandParams p) {
+  const int lane = threadIdx.x;
+  const uint2 it = p.items[blockIdx.x];
+  const uint32_t j = p.big[it.x], prim = p.list[j];
+  const Footprint fp = p.fp[j];
+  int r0, r1;
+  if (!raster_rows(p, fp, r0, r1) || !refined_rows(r0, r1)) return;
+  const uint32_t base = p.off[j], total = p.off[j + 1] - base;
+  const uint32_t c0 = it.y * kChunk, c1 = c0 + kChunk < total ? c0 + kChunk : total;
+  __shared__ TileTri tt;
+  __shared__ TileFrame tf;
+  __shared__ int tt_ok;
+  if (lane == 0) {
+    tt_ok = tile_tri(p, (const float*)(p.tri + 3 * (size_t)prim), tt) ? 1 : 0;
+    tile_frame(p, tf);
+  }
+  __syncthreads();
+  if (!tt_ok) return;
+  for (uint32_t e = c0 + (uint32_t)lane; e < c1; e += 64) {
+    // re-read the LDS inputs per entry instead of holding them live across
+    // the loop (a compiler memory barrier; 161 -> 80 VGPRs)
+    __asm__ volatile("" ::: "memory");
+    int tx, ty;
+    rt_tile_xy(p.keys[base + e], (uint32_t)p.rank, (uint32_t)p.nranks, (uint32_t)p.blocks_x, (uint32_t)p.tb, &tx, &ty);
+    if (!tile_keep(tf, tt, tx, ty)) p.keys[base + e] = p.drop_key;
   }
 }
 
@@ -1787,6 +1847,7 @@ extern "C" hipError_t rt_cand_items(const CandParams* p, hipStream_t s) {
 extern "C" hipError_t rt_cand_big_items(const CandParams* p, uint32_t nitems, hipStream_t s) {
   if (nitems == 0) return hipSuccess;
   hipLaunchKernelGGL(rtc::big_item_kernel, dim3(nitems), dim3(64), 0, s, *p);
+  if (p->refine) hipLaunchKernelGGL(rtc::refine_kernel, dim3(nitems), dim3(64), 0, s, *p);
   return hipGetLastError();
 }
 

@@ -1062,10 +1062,24 @@ static int cand_params(const rt_frame* f, const float scene_c[3], float scene_r,
     cp.k0 = cp.ginv[0] * pu + cp.ginv[1] * pv;
     cp.l0 = cp.ginv[1] * pu + cp.ginv[2] * pv;
   }
-  // a tile's sample rectangle: 3.75 (3.5 in the compatibility mode) samples
-  // either side of its centre on each axis (rt_cand.hip tile_keep)
-  const double half = compat ? 3.5 : 3.75;
-  cp.tile_hd = (half * std::sqrt(d3dot(u, u)) + half * std::sqrt(d3dot(v, v))) * (1.0 + 1e-12);
+  // a tile's sample rectangle (rt_cand.hip tile_keep): cpu/rt's samples k in
+  // [W/2 - c, W/2 - c + 1/2] for the tile's columns c = 8 tx .. 8 tx + 7, so
+  // centre W/2 - 8 tx - 3.25 and half side 3.75 (likewise l); compatibility
+  // mode: k = c - W/2, centre 8 tx + 3.5 - W/2, half side 3.5
+  {
+    const double hw = (double)(f->width / 2), hh = (double)(f->height / 2);
+    cp.tile_hk = cp.tile_hl = compat ? 3.5 : 3.75;
+    cp.tile_k00 = compat ? 3.5 - hw : hw - 3.25;
+    cp.tile_l00 = compat ? 3.5 - hh : hh - 3.25;
+    cp.tile_dk = cp.tile_dl = compat ? 8.0 : -8.0;
+    for (int a = 0; a < 3; a++) {
+      cp.tile_p00[a] = pos[a] - (C[a] + cp.tile_k00 * u[a] + cp.tile_l00 * v[a]);
+      cp.tile_du[a] = cp.tile_dk * u[a];
+      cp.tile_dv[a] = cp.tile_dl * v[a];
+      cp.tile_w[a] = std::fabs(u[a]) * cp.tile_hk + std::fabs(v[a]) * cp.tile_hl;
+    }
+    cp.tile_hd = (cp.tile_hk * std::sqrt(d3dot(u, u)) + cp.tile_hl * std::sqrt(d3dot(v, v))) * (1.0 + 1e-12);
+  }
   const int W = f->width, H = f->height;
   cp.compat = compat;
   if (compat) {
