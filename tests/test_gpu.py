@@ -862,3 +862,28 @@ def test_light_buffer_entries_match_host_survey(gpu, exact):
     if exact:
         assert info["lightbuf_band"] == sum(h["band"] for h in host)
         assert info["lightbuf_never"] == sum(h["never"] for h in host)
+
+
+@pytest.mark.parametrize("accel", ["octree_gpu", "octree"])
+def test_camera_refine_on_off(gpu, accel):
+    """The per-tile refinement of the candidate lists (rt_hip_set_camera_refine,
+    csrc/rt_cand.hip tile_keep) only drops entries no camera ray of their tile
+    can accept: the frame is bit-identical with it off, with fewer entries on;
+    the host re-derivation matches the device lists both ways (the host applies
+    the same refinement), N = 1 and rank 2 of 3."""
+    s = gpu.Scene.synthetic(8, 6, 9776, seed=0x5EED, width=1920, height=1080)
+    f = s.frame()
+    ctx = gpu.Context(s, accel)
+    img_on, st_on = ctx.render_image(f)
+    ctx.set_camera_refine(False)
+    img_off, st_off = ctx.render_image(f)
+    assert np.array_equal(img_on.view(np.uint32), img_off.view(np.uint32))
+    assert st_on["closest"] == st_off["closest"] and st_on["shadow"] == st_off["shadow"]
+    assert 0 < st_on["cand_entries"] < st_off["cand_entries"], (st_on["cand_entries"], st_off["cand_entries"])
+    for on in (False, True):
+        ctx.set_camera_refine(on)
+        for nranks, rank in ((1, 0), (3, 2)):
+            _tiles_of_rank(ctx, f, rank, nranks)
+            v = ctx.cand_verify(f, rank, nranks)
+            assert v["fp_mismatch"] == 0 and v["tile_mismatch"] == 0, (on, nranks, rank, v)
+            assert v["filter_violation"] == 0, (on, nranks, rank, v)
