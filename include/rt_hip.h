@@ -291,10 +291,11 @@ int rt_cand_survey(const rt_scene *scene, float eps_ulps, double bound_scale, in
 /* Host-only sample of the per-tile refinement (rt_hip_set_camera_refine) of
  * a scene's frame: every stride-th entry of the refined footprints as (prim,
  * tile x, tile y, kept) -- tests check each dropped entry against the
- * reference's float test on every camera sample of its tile.  *n = entries
- * written (at most cap), *total = entries sampled. */
+ * reference's float test on every camera sample of its tile.  compat: the
+ * gpu/rt compatibility mode's frame (3x the camera, one ray per pixel).
+ * *n = entries written (at most cap), *total = entries sampled. */
 int rt_cand_refine_sample(const rt_scene *scene, float eps_ulps, double bound_scale, unsigned stride,
-                          unsigned *out, size_t cap, size_t *n, size_t *total);
+                          int compat, unsigned *out, size_t cap, size_t *n, size_t *total);
 /* Test hook: after an rt_hip_render of (frame, rank, nranks) with exact
  * camera rays, re-derive its candidate lists on the host from the same code
  * and compare.  out = {listed prims, entries, footprint mismatches, tiles

@@ -50,6 +50,8 @@ def lib():
         L.oracle_render_gpu.restype = C.c_int
         L.oracle_camera_tri_accepts.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
         L.oracle_camera_tri_accepts.restype = None
+        L.oracle_camera_tri_accepts_gpu.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
+        L.oracle_camera_tri_accepts_gpu.restype = None
         L.oracle_init_color.argtypes = [C.c_float, C.c_float, C.c_float]
         L.oracle_init_color.restype = ColorS
         L.oracle_color_add.argtypes = [ColorS, ColorS]
@@ -153,11 +155,12 @@ def render(scene_ptr, width, height, pixels=None, threads=0):
     return out, counts
 
 
-def camera_tri_accepts(scene_ptr, tris, rects):
+def camera_tri_accepts(scene_ptr, tris, rects, gpu=False):
     """cpu/rt's camera samples of pixel rectangles against one triangle each
     (oracle_camera_tri_accepts).  tris: (n, 6, 3) float32 (vertices, normals
     as rt_scene holds them); rects: (n, 4) (row0, col0, rows, cols).  Returns
-    (n, 2): samples accepted, samples passing the a, u, v tests."""
+    (n, 2): samples accepted, samples passing the a, u, v tests.  gpu: gpu/rt's
+    rays, one per pixel of the 3x frame (rects in its pixels)."""
     tris = np.ascontiguousarray(tris, dtype=np.float32)
     rects = np.ascontiguousarray(rects, dtype=np.int32)
     assert tris.shape[1:] == (6, 3) and rects.shape == (len(tris), 4)
@@ -165,7 +168,8 @@ def camera_tri_accepts(scene_ptr, tris, rects):
     ptr = scene_ptr.ptr if isinstance(scene_ptr, OracleScene) else scene_ptr
     if not isinstance(ptr, C.c_void_p):
         ptr = C.cast(ptr, C.c_void_p)
-    lib().oracle_camera_tri_accepts(ptr, tris.ctypes.data, rects.ctypes.data, len(tris), out.ctypes.data)
+    fn = lib().oracle_camera_tri_accepts_gpu if gpu else lib().oracle_camera_tri_accepts
+    fn(ptr, tris.ctypes.data, rects.ctypes.data, len(tris), out.ctypes.data)
     return out
 
 

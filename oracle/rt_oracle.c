@@ -394,6 +394,55 @@ void oracle_camera_tri_accepts(const struct or_scene *scene, const struct or_tri
                        rects[4 * i + 3], out + 2 * i);
 }
 
+/* The same for gpu/rt's camera rays (gpu/raytracer.cu:97-103, the mapping
+ * of gpu_ray_pixel): one ray per pixel (px, py) of the 3x frame (gpu/rt.cpp:
+ * 72-83), rects in that frame's pixels: (py0, px0, rows, cols). */
+void oracle_camera_tri_accepts_gpu(const struct or_scene *scene, const struct or_triangle *tris,
+                                   const int *rects, size_t n, unsigned long long *out)
+{
+  struct or_scene hi = *scene;
+  hi.camera.width = 3 * scene->camera.width;
+  hi.camera.height = 3 * scene->camera.height;
+  vec3 u, v, C;
+  oracle_camera_frame(&hi, &u, &v, &C);
+  const int W = hi.camera.width, H = hi.camera.height;
+  const float eps = 0.0000001;
+  for (size_t i = 0; i < n; i++)
+  {
+    const struct or_triangle *tri = &tris[i];
+    const int *rc = rects + 4 * i;
+    unsigned long long acc = 0, uv = 0;
+    for (int py = rc[0]; py < rc[0] + rc[2]; py++)
+      for (int px = rc[1]; px < rc[1] + rc[3]; px++)
+      {
+        if (px < 0 || px >= W || py < 0 || py >= H)
+          continue;
+        vec3 point = v_add(v_add(C, v_scale(u, (float)(px - W / 2))), v_scale(v, (float)(py - H / 2)));
+        ray r = { point, v_normalize(v_sub(scene->camera.position, point)) };
+        vec3 hit, nrm;
+        acc += intersect(r, tri, &hit, &nrm) ? 1 : 0;
+        vec3 e1 = v_sub(tri->vertex[1], tri->vertex[0]);
+        vec3 e2 = v_sub(tri->vertex[2], tri->vertex[0]);
+        vec3 h = v_cross(r.direction, e2);
+        float a = v_dot(e1, h);
+        if (a > -eps && a < eps)
+          continue;
+        float f = 1 / a;
+        vec3 s = v_sub(r.origin, tri->vertex[0]);
+        float uu = f * v_dot(s, h);
+        if (uu < 0.0 || uu > 1.0)
+          continue;
+        vec3 q = v_cross(s, e1);
+        float vv = f * v_dot(r.direction, q);
+        if (vv < 0.0 || uu + vv > 1.0)
+          continue;
+        uv++;
+      }
+    out[2 * i] = acc;
+    out[2 * i + 1] = uv;
+  }
+}
+
 /* ---- gpu/rt compatibility mode ----
  * gpu/raytracer.cu:31-129, gpu/light.cu:12-126, gpu/colors.cu:3-49 as the
  * sources read (PARTITIONING_NONE order of gpu/hit.cu:83-116, which is

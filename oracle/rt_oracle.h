@@ -72,6 +72,11 @@ int oracle_render_gpu(const struct or_scene *scene, const int *pixels, size_t np
 void oracle_camera_tri_accepts(const struct or_scene *scene, const struct or_triangle *tris,
                                const int *rects, size_t n, unsigned long long *out);
 
+/* The same for gpu/rt's camera rays (gpu/raytracer.cu:97-103): one ray per
+ * pixel (px, py) of the 3x frame; rects[4i .. 4i + 3] = (py0, px0, rows, cols). */
+void oracle_camera_tri_accepts_gpu(const struct or_scene *scene, const struct or_triangle *tris,
+                                   const int *rects, size_t n, unsigned long long *out);
+
 /* Single-function entry points, for unit known-answer tests. */
 struct or_color oracle_init_color(float r, float g, float b);
 struct or_color oracle_color_add(struct or_color a, struct or_color b);

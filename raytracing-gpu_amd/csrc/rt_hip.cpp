@@ -745,10 +745,15 @@ extern "C" int rt_hip_set_camera_bound_scale(rt_hip_ctx* c, double scale) {
 }
 
 extern "C" int rt_cand_refine_sample(const rt_scene* scene, float eps_ulps, double bound_scale, unsigned stride,
-                                     unsigned* out, size_t cap, size_t* n, size_t* total) {
+                                     int compat, unsigned* out, size_t cap, size_t* n, size_t* total) {
   if (!scene || (!out && cap) || !n || !total) return rt_set_error(RT_EINVAL, "null argument");
   rt_frame f;
-  int rc = rt_frame_from_camera(&scene->camera, &f);
+  rt_camera cam = scene->camera;
+  if (compat) {  // gpu/rt's frame: the camera's width and height times 3 (gpu/rt.cpp:72-83)
+    cam.width *= 3;
+    cam.height *= 3;
+  }
+  int rc = rt_frame_from_camera(&cam, &f);
   if (rc) return rc;
   rt_flat_scene fs;
   rc = rt_flatten(scene, RT_ACCEL_FLAT, &fs);
@@ -760,7 +765,7 @@ extern "C" int rt_cand_refine_sample(const rt_scene* scene, float eps_ulps, doub
     sr = std::fmax(sr, 0.5f * (hi - lo));
   }
   CandParams cp;
-  rc = cand_params(&f, sc, sr, eps_ulps, bound_scale, 0, 1, &cp);
+  rc = cand_params(&f, sc, sr, eps_ulps, bound_scale, 0, 1, &cp, compat ? 1 : 0);
   if (!rc) {
     cp.nprim = (uint32_t)fs.ntri;
     *n = rt_cand_refine_sample_host(&cp, fs.tri, stride, out, cap, total);

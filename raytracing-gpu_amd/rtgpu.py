@@ -174,8 +174,8 @@ _PROTOS = [
                                             C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     ("rt_hip_set_camera_bound_scale", C.c_int, [C.c_void_p, C.c_double]),
     ("rt_hip_set_camera_refine", C.c_int, [C.c_void_p, C.c_int]),
-    ("rt_cand_refine_sample", C.c_int, [C.POINTER(SceneStruct), C.c_float, C.c_double, C.c_uint, C.c_void_p,
-                                        C.c_size_t, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]),
+    ("rt_cand_refine_sample", C.c_int, [C.POINTER(SceneStruct), C.c_float, C.c_double, C.c_uint, C.c_int,
+                                        C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]),
     ("rt_cand_survey", C.c_int, [C.POINTER(SceneStruct), C.c_float, C.c_double, C.c_int, C.c_int,
                                  C.POINTER(C.c_ulonglong)]),
     ("rt_hip_assemble", C.c_int, [C.c_void_p, C.POINTER(Frame), C.c_void_p, C.c_int, C.c_void_p,
@@ -391,15 +391,15 @@ def cand_survey(scene, eps_ulps=64.0, bound_scale=1.0, threads=8, leaves=False):
     return r
 
 
-def cand_refine_sample(scene, stride=1, cap=1 << 20, eps_ulps=64.0, bound_scale=1.0):
+def cand_refine_sample(scene, stride=1, cap=1 << 20, eps_ulps=64.0, bound_scale=1.0, compat=False):
     """Host-only: every stride-th entry of the refined candidate footprints
     as rows (prim, tile x, tile y, kept) -- csrc/rt_cand.hip tile_keep -- and
-    the number sampled."""
+    the number sampled (compat: the gpu/rt mode's 3x frame)."""
     import numpy as np
     out = np.zeros((cap, 4), np.uint32)
     n, total = C.c_size_t(0), C.c_size_t(0)
-    _check(lib().rt_cand_refine_sample(scene.ptr, eps_ulps, bound_scale, stride, out.ctypes.data, cap,
-                                       C.byref(n), C.byref(total)), "cand_refine_sample")
+    _check(lib().rt_cand_refine_sample(scene.ptr, eps_ulps, bound_scale, stride, 1 if compat else 0,
+                                       out.ctypes.data, cap, C.byref(n), C.byref(total)), "cand_refine_sample")
     return out[:n.value], total.value
 
 

@@ -116,3 +116,22 @@ def test_tile_refinement_drops_only_tiles_the_reference_never_accepts(case):
     acc = orc.camera_tri_accepts(s.ptr, tris[rows[:, 0]], rects)
     assert int(acc[drop, 1].max()) == 0, rows[drop][acc[drop, 1] > 0][:8]
     assert int((acc[~drop, 0] > 0).sum()) > 0  # real hits live in kept tiles
+
+
+def test_tile_refinement_compat_drops_only_never_accepted_tiles():
+    """test_tile_refinement_drops_only_tiles_the_reference_never_accepts for
+    the gpu/rt compatibility mode's lists (one ray per pixel of the 3x frame,
+    gpu/raytracer.cu:97-103; tile_keep's compat sample rectangle), checked
+    with the oracle's restatement of those rays."""
+    import rtgpu
+    import oracle as orc
+    s = rtgpu.Scene.synthetic(4, 4, 1200, seed=0x5EED, width=160, height=90)
+    rows, total = rtgpu.cand_refine_sample(s, stride=1, cap=1 << 20, compat=True)
+    assert len(rows) == total > 0
+    drop = rows[:, 3] == 0
+    assert drop.sum() > 0 and (~drop).sum() > 0
+    tris = s.triangles_array()
+    rects = np.stack([rows[:, 2] * 8, rows[:, 1] * 8, np.full(len(rows), 8), np.full(len(rows), 8)], 1)
+    acc = orc.camera_tri_accepts(s.ptr, tris[rows[:, 0]], rects, gpu=True)
+    assert int(acc[drop, 1].max()) == 0, rows[drop][acc[drop, 1] > 0][:8]
+    assert int((acc[~drop, 0] > 0).sum()) > 0
