@@ -494,7 +494,7 @@ def main():
                 "candidate_lists": ("triangle-parallel: rt_hip_cand_produce over 1/N of the "
                                     "triangles, RCCL all-to-all, rt_hip_cand_consume" if partition
                                     else "per rank: every triangle, this rank's tiles"),
-                "exactness": {"camera_rays": "proven (candidate lists)",
+                "exactness": {"camera_rays": "proven (candidate lists, refined per tile)",
                               "shadow_rays": ("measured (slack-grown light buffers)"
                                               if args.exact_shadows == 0 else
                                               "proven (light buffers + off-box brute force)")},
