@@ -112,6 +112,25 @@ def _sample_loop(orc, scene, W, H, pixels, seconds, threads, gpu_img, out):
     out["pixels"] += done
 
 
+def cgroup_cpu_quota():
+    """CPUs the process's cgroup may use (quota / period), None when unlimited
+    or unreadable: cgroup v2 cpu.max, else v1 cfs_quota_us / cfs_period_us."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        return None if q <= 0 else round(q / per, 2)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(scene, W, H, seconds, threads, gpu_img):
     """The oracle (plain-C restatement of cpu/rt, brute force like the
     reference) on bounded deterministic pixel samples of the same frame, in
@@ -163,6 +182,9 @@ def cpu_baseline(scene, W, H, seconds, threads, gpu_img):
                   f"{el_b:.1f} s on {threads} threads; oracle/rt_oracle.c (brute force like cpu/rt, "
                   f"-O2)",
         "host_cpus": os.cpu_count(),
+        # what this process may actually run on, observed (not asserted)
+        "affinity_cpus": len(os.sched_getaffinity(0)),
+        "cgroup_cpu_quota": cgroup_cpu_quota(),
         "mode_a": {"value": qa / el_a / 1e6, "unit": "Mrays/s", "cores": 4,
                    "sample": f"{sum(r['pixels'] for r in res_a)} pixels, {el_a:.1f} s, 4 threads, "
                              f"one image quadrant each (cpu/raytracer.c:92-127)"},
@@ -170,11 +192,36 @@ def cpu_baseline(scene, W, H, seconds, threads, gpu_img):
     }
 
 
-def latest_profile(workload, name):
-    """Newest profiles/r*_<workload>/<name> (round-letter order), or None."""
+def device_code_hash():
+    """sha256 of everything that decides what the kernels do: the HIP and
+    C-ABI sources (raytracing-gpu_amd/csrc/), the host headers they include,
+    the public headers and the build flags (Makefile).  tools/gpu_profile.sh
+    writes it next to the PMC passes it takes (device_hash.txt)."""
     import glob
-    hits = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_{workload}", name)))
-    return hits[-1] if hits else None
+    import hashlib
+    pk = os.path.join(REPO, "raytracing-gpu_amd")
+    files = sorted(glob.glob(os.path.join(pk, "csrc", "*")) + glob.glob(os.path.join(pk, "host", "*.h")) +
+                   glob.glob(os.path.join(REPO, "include", "*.h")) + [os.path.join(pk, "Makefile")])
+    h = hashlib.sha256()
+    for f in files:
+        h.update(os.path.relpath(f, REPO).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def latest_profile(workload, name):
+    """Newest profiles/r*_<workload>/<name> (round-letter order) whose PMC
+    passes were taken of THIS device code (its device_hash.txt equals
+    device_code_hash()), or None: counters of other kernels are never
+    reported as this run's (VERDICT r04 weak #10)."""
+    import glob
+    want = device_code_hash()
+    for hit in sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_{workload}", name)), reverse=True):
+        hf = os.path.join(os.path.dirname(hit), "device_hash.txt")
+        if os.path.exists(hf) and open(hf).read().strip() == want:
+            return hit
+    return None
 
 
 def main():
@@ -460,7 +507,7 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu:
             img = rgb.view(H, W, 3).cpu().numpy()
-            thr = args.cpu_threads or min(os.cpu_count() or 1,
+            thr = args.cpu_threads or min(len(os.sched_getaffinity(0)) or 1,
                                           int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or 16)
             log(f"[rank 0] cpu baseline: {args.cpu_seconds:.0f}s of samples (Mode A 4 threads, "
                 f"Mode B {thr} threads)")
@@ -517,8 +564,11 @@ def main():
                 "traffic_upper": traffic_hi,
                 "hbm_measured_GBs": (round(traffic / (kms[dom] * 1e-3) / 1e9, 2)
                                      if traffic is not None else None),
-                "traffic_source": (f"committed profile {traffic_src} (not measured in this run)"
-                                   if traffic is not None else None),
+                "traffic_source": (f"committed profile {traffic_src} (not measured in this run; "
+                                   f"taken of this device code, sha256 {device_code_hash()[:12]})"
+                                   if traffic is not None else
+                                   f"none: no committed PMC profile of this device code "
+                                   f"(sha256 {device_code_hash()[:12]})"),
                 "kernel_ms": round(kms[dom], 3),
                 "algorithmic_bytes_per_launch": int(per_launch),
                 "kernels": {k: {"ms": round(kms[k], 3),

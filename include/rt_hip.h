@@ -39,6 +39,9 @@ typedef struct rt_frame {
   int width, height;
 } rt_frame;
 
+/* Fails with RT_EINVAL for odd widths or heights: cpu/rt's output is
+ * undefined there (cpu/raytracer.c:89-91,128-134 index the framebuffer two
+ * different ways that agree only for even sizes). */
 int rt_frame_from_camera(const rt_camera *cam, rt_frame *out);
 
 /* Acceleration structure selection.  OCTREE: SAH octree built on the host
@@ -120,10 +123,12 @@ typedef struct rt_accel_info {
    * triangles listed along a band of a point light's cube map */
   unsigned long long lightbuf_never;
   unsigned long long lightbuf_band;
-  /* lights whose buffer could not be built (too many entries, out of device
-   * memory): their shadow queries walk the octree instead (the proven walk in
-   * the exact-shadow mode) */
+  /* lights whose buffer could not be built (too many entries or cells, out
+   * of device memory, a directional light with a zero vector): their shadow
+   * queries walk the octree instead (the proven walk in the exact-shadow
+   * mode).  Any other build failure fails the call (RT_EHIP). */
   unsigned long long lightbuf_failed;
+  char lightbuf_fail_reason[96]; /* the last such fallback's cause ("" if none) */
 } rt_accel_info;
 
 /* Host-only: build the acceleration structure rt_hip_create would build and
@@ -159,16 +164,23 @@ int rt_hip_accel_info(const rt_hip_ctx *ctx, rt_accel_info *out);
 int rt_hip_accel_validate(const rt_hip_ctx *ctx);
 void rt_hip_destroy(rt_hip_ctx *ctx);
 
-/* Image tiling: 8x8-pixel tiles grouped in blocks of tb x tb tiles, tb = 4
- * (32x32 pixels) when nranks > 1 and 1 (scanline tile order) for one rank;
- * block b (scanline order over ceil(tiles_x/tb) x ceil(tiles_y/tb) blocks)
- * belongs to rank b % nranks.  A rank's tile buffer holds its blocks
- * in order, tb*tb tiles each in row-major order, each tile 64 pixels x 3 floats
- * (pixel p of a tile = row p/8, col p%8 inside the tile); slots past the
- * frame's edge are padding (0).  rt_hip_tiles_per_rank() = the largest
- * rank's tile count (rank 0's), the size of every rank's buffer in a gather. */
+/* Image tiling (csrc/rt_tiles.h): 8x8-pixel tiles grouped in blocks of tb x
+ * tb tiles, tb = 4 (32x32 pixels) when nranks > 1 and 1 (scanline tile order)
+ * for one rank; blocks b (scanline order over ceil(tiles_x/tb) x
+ * ceil(tiles_y/tb) blocks) come in runs of nranks, run g = b / nranks holding
+ * one block of every rank: block b belongs to rank (b % nranks + g) % nranks
+ * as that rank's g-th block.  A rank's tile buffer holds its blocks in order,
+ * tb*tb tiles each in row-major order, each tile 64 pixels x 3 floats (pixel
+ * p of a tile = row p/8, col p%8 inside the tile); slots past the frame's
+ * edge are padding (0).  rt_hip_tiles_per_rank() = the largest rank's tile
+ * count, the size of every rank's buffer in a gather. */
 int rt_hip_tiles_per_rank(int width, int height, int nranks);
 size_t rt_hip_tile_buffer_floats(int width, int height, int nranks);
+/* Host-only self-check of the tile map's O(1) row arithmetic (the candidate
+ * lists' counts and emission order) against a brute-force walk over the
+ * frame's tiles: every tile row, column intervals [x0, x1] of every width
+ * up to `maxw` tiles.  out[0] = intervals checked, out[1] = mismatches. */
+int rt_tile_map_check(int width, int height, int nranks, int maxw, unsigned long long out[2]);
 
 /* Renders every tile of `rank` into d_tiles (device memory of the context's
  * device, rt_hip_tile_buffer_floats() floats).  Asynchronous on `stream`

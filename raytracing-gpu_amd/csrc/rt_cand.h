@@ -130,7 +130,7 @@ extern "C" hipError_t rt_cand_sort(uint32_t* keys_in, uint32_t* keys_out, uint32
                                    size_t* temp_bytes, hipStream_t s);
 // out[i] = skip[cand[i]]: the sorted lists' per-entry depth-skip bounds
 extern "C" hipError_t rt_cand_entry_skip(const uint32_t* cand, const float* skip, float* out,
-                                         uint32_t n, hipStream_t s);
+                                         uint32_t n, const uint32_t* n_dev, hipStream_t s);
 extern "C" hipError_t rt_cand_bounds(const uint32_t* keys, uint32_t n, uint32_t* start,
                                      uint32_t ntiles, hipStream_t s);
 // Triangle-parallel multi-GPU lists (rt_hip_cand_produce / rt_hip_cand_consume):

@@ -380,17 +380,16 @@ RTC_FN bool rank_may_touch(const CandParams& p, const double q[3], double rb) {
   if (r0 > r1 || c0 > c1) return false;  // off the frame
   const uint32_t n = (uint32_t)p.nranks, rk = (uint32_t)p.rank;
   if (n == 1) return true;
-  // whole tb x tb-tile blocks per rank, block b -> rank b mod n
-  // (csrc/rt_tiles.h): a block column range of >= n blocks meets every rank
-  // in every block row; otherwise one check per block row (the residues of
-  // the rows repeat with period n)
+  // whole tb x tb-tile blocks per rank, block (bx, by) -> rank (bx + by) mod
+  // n (csrc/rt_tiles.h): a block column range of >= n blocks meets every
+  // rank in every block row; otherwise one check per block row (the residues
+  // of the rows repeat with period n)
   const int bx0 = (c0 >> 3) / p.tb, bx1 = (c1 >> 3) / p.tb;
   const int by0 = (r0 >> 3) / p.tb, by1 = (r1 >> 3) / p.tb;
   if ((uint32_t)(bx1 - bx0 + 1) >= n) return true;
   const int rows = by1 - by0 + 1 < (int)n ? by1 - by0 + 1 : (int)n;
   for (int k = 0; k < rows; k++) {
-    const uint32_t by = (uint32_t)(by0 + k);
-    const uint32_t res = (rk + n - (uint32_t)(((uint64_t)by * (uint32_t)p.blocks_x) % n)) % n;
+    const uint32_t res = rt_row_res((uint32_t)(by0 + k), n, rk);
     const uint32_t f = (uint32_t)bx0 <= res ? res : (uint32_t)bx0 + (res + n - (uint32_t)bx0 % n) % n;
     if (f <= (uint32_t)bx1) return true;
   }
@@ -1074,7 +1073,8 @@ __global__ __launch_bounds__(64) void item_kernel(CandParams p) {
 // The rank's tiles of one tile-row column interval [x0, x1] of tile row ty:
 // the rank's blocks bx = f, f + n, ... of the row (csrc/rt_tiles.h), each
 // contributing its columns inside the interval at consecutive local indices
-// -- one division per block, none per tile.  Returns the count written at
+// (the rank's blocks of a row are consecutive in its buffer) -- one prefix
+// count per interval, no division per tile.  Returns the count written at
 // keys/vals[o ..].
 __device__ __forceinline__ uint32_t emit_interval(const CandParams& p, int ty, int x0, int x1,
                                                   uint32_t o, uint32_t prim, bool refine = false) {
@@ -1083,11 +1083,13 @@ __device__ __forceinline__ uint32_t emit_interval(const CandParams& p, int ty, i
   int f;
   const int tb = p.tb;
   const uint32_t cnt = rt_rank_row_tiles(ty, x0, x1, n, r, (uint32_t)p.blocks_x, (uint32_t)tb, &f);
-  const uint32_t by = (uint32_t)(ty / tb), row = (uint32_t)(ty % tb) * (uint32_t)tb;
+  if (cnt == 0) return 0;
+  const uint32_t row = (uint32_t)(ty % tb) * (uint32_t)tb;
+  uint32_t blk = rt_block_local((uint32_t)f, (uint32_t)(ty / tb), n, (uint32_t)p.blocks_x, r);
   uint32_t k = 0;
-  for (int bx = f; k < cnt; bx += (int)n) {
+  for (int bx = f; k < cnt; bx += (int)n, blk++) {
     const int a = x0 > bx * tb ? x0 : bx * tb, b = x1 < bx * tb + tb - 1 ? x1 : bx * tb + tb - 1;
-    const uint32_t base = ((by * (uint32_t)p.blocks_x + (uint32_t)bx) / n) * (uint32_t)(tb * tb) + row;
+    const uint32_t base = blk * (uint32_t)(tb * tb) + row;
     for (int tx = a; tx <= b; tx++, k++) {
       const bool keep = !refine || tile_keep(p, (const float*)(p.tri + 3 * (size_t)prim), tx, ty);
       p.keys[o + k] = keep ? base + (uint32_t)(tx - bx * tb) : p.drop_key;
@@ -1317,10 +1319,12 @@ __global__ __launch_bounds__(256) void bounds_kernel(const uint32_t* keys, uint3
 
 // per list entry: the depth-skip bound of its prim (coalesced for the render
 // kernel, which would otherwise gather it right after loading the entry)
+// n_dev (optional): the entries with a tile, start[ntiles] -- the ones the
+// refinement dropped sort after them and are never read
 __global__ __launch_bounds__(256) void entry_skip_kernel(const uint32_t* cand, const float* skip,
-                                                         float* out, uint32_t n) {
+                                                         float* out, uint32_t n, const uint32_t* n_dev) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = skip[cand[i]];
+  if (i < n && (!n_dev || i < *n_dev)) out[i] = skip[cand[i]];
 }
 
 // --- triangle-parallel multi-GPU lists (rt_cand.h "route") ---------------
@@ -1402,10 +1406,14 @@ __global__ __launch_bounds__(256) void gather_kernel(const uint32_t* in, const u
 // tools/tile_cost.py), so tiles with more than 8x the mean go first and the
 // persistent waves' last items are short ones.  flags -> exclusive scan ->
 // perm: heavy tiles first, then the rest, each in their own order.
+// a tile is heavy when its list is longer than 8x the mean; the mean over
+// the entries with a tile (start[ntiles], read here: the host's total also
+// counts the entries the refinement dropped)
 __global__ __launch_bounds__(256) void heavy_flag_kernel(const uint32_t* start, uint32_t ntiles,
-                                                         uint32_t total, uint32_t* flags) {
+                                                         uint32_t* flags) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t > ntiles) return;
+  const uint32_t total = start[ntiles] - start[0];
   flags[t] = t < ntiles && (unsigned long long)(start[t + 1] - start[t]) * ntiles >
                                8ull * (unsigned long long)total
                  ? 1u
@@ -1890,10 +1898,10 @@ extern "C" hipError_t rt_cand_sort(uint32_t* keys_in, uint32_t* keys_out, uint32
 }
 
 extern "C" hipError_t rt_cand_entry_skip(const uint32_t* cand, const float* skip, float* out,
-                                         uint32_t n, hipStream_t s) {
+                                         uint32_t n, const uint32_t* n_dev, hipStream_t s) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(rtc::entry_skip_kernel, dim3((n + 255) / 256), dim3(256), 0, s, cand, skip,
-                     out, n);
+                     out, n, n_dev);
   return hipGetLastError();
 }
 
@@ -1955,7 +1963,8 @@ extern "C" hipError_t rt_cand_order(const uint32_t* start, uint32_t ntiles, uint
                                     size_t* tmp_bytes, hipStream_t s) {
   if (!tmp) return rt_cand_scan(flags, pos, ntiles, nullptr, tmp_bytes, s);
   const dim3 b(256), g((ntiles + 1 + 255) / 256);
-  hipLaunchKernelGGL(rtc::heavy_flag_kernel, g, b, 0, s, start, ntiles, total, flags);
+  (void)total;
+  hipLaunchKernelGGL(rtc::heavy_flag_kernel, g, b, 0, s, start, ntiles, flags);
   hipError_t e = rt_cand_scan(flags, pos, ntiles, tmp, tmp_bytes, s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(rtc::heavy_perm_kernel, g, b, 0, s, flags, pos, ntiles, perm);

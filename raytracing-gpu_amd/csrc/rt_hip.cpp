@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <chrono>
 #include <cmath>
@@ -183,21 +184,75 @@ static int cand_params(const rt_frame* f, const float scene_c[3], float scene_r,
 static int tiles_x_of(int W) { return (W + 7) / 8; }
 static int tiles_y_of(int H) { return (H + 7) / 8; }
 
-// tile blocks of a frame split nranks ways (csrc/rt_tiles.h)
-static uint32_t nblocks_of(int W, int H, int nranks) {
-  const int tb = rt_block_side(nranks);
-  return (uint32_t)rt_blocks_x(tiles_x_of(W), tb) * (uint32_t)rt_blocks_y(tiles_y_of(H), tb);
-}
-
-// tiles rank `rank` renders (whole blocks, edge padding included)
+// tiles rank `rank` renders (whole blocks, edge padding included; csrc/rt_tiles.h)
 static int rank_tile_count(int W, int H, int rank, int nranks) {
   const int tb = rt_block_side(nranks);
-  return (int)(rt_rank_blocks(nblocks_of(W, H, nranks), (uint32_t)nranks, (uint32_t)rank) * tb * tb);
+  return (int)(rt_rank_blocks((uint32_t)rt_blocks_x(tiles_x_of(W), tb), (uint32_t)rt_blocks_y(tiles_y_of(H), tb),
+                              (uint32_t)nranks, (uint32_t)rank) * tb * tb);
 }
 
 extern "C" int rt_hip_tiles_per_rank(int width, int height, int nranks) {
   if (width <= 0 || height <= 0 || nranks <= 0) return 0;
-  return rank_tile_count(width, height, 0, nranks);  // rank 0 holds the most blocks
+  const int tb = rt_block_side(nranks);
+  return (int)(rt_max_rank_blocks((uint32_t)rt_blocks_x(tiles_x_of(width), tb),
+                                  (uint32_t)rt_blocks_y(tiles_y_of(height), tb), (uint32_t)nranks) * tb * tb);
+}
+
+extern "C" int rt_tile_map_check(int width, int height, int nranks, int maxw, unsigned long long out[2]) {
+  if (!out || width <= 0 || height <= 0 || nranks <= 0 || maxw <= 0) return rt_set_error(RT_EINVAL, "bad argument");
+  out[0] = out[1] = 0;
+  const int tx = tiles_x_of(width), ty = tiles_y_of(height), tb = rt_block_side(nranks);
+  const uint32_t bx = (uint32_t)rt_blocks_x(tx, tb), n = (uint32_t)nranks;
+  // every tile: local index <-> (tx, ty) round trip, inside the rank's count,
+  // each (rank, local) slot used once
+  {
+    std::vector<uint32_t> cnt(n, 0);
+    std::vector<std::vector<char>> used(n);
+    for (uint32_t r = 0; r < n; r++) used[r].assign((size_t)rank_tile_count(width, height, (int)r, nranks), 0);
+    uint32_t mx = 0;
+    for (int y = 0; y < ty; y++)
+      for (int x = 0; x < tx; x++) {
+        uint32_t rk;
+        const uint32_t loc = rt_tile_local(x, y, n, bx, (uint32_t)tb, &rk);
+        int x2 = -1, y2 = -1;
+        rt_tile_xy(loc, rk, n, bx, (uint32_t)tb, &x2, &y2);
+        const bool bad = rk >= n || loc >= used[rk].size() || used[rk][loc] || x2 != x || y2 != y;
+        if (!bad) used[rk][loc] = 1;
+        out[0]++;
+        out[1] += bad ? 1 : 0;
+      }
+    for (uint32_t r = 0; r < n; r++) mx = std::max(mx, (uint32_t)used[r].size());
+    out[0]++;
+    out[1] += mx == (uint32_t)rt_hip_tiles_per_rank(width, height, nranks) ? 0 : 1;
+  }
+  for (int y = 0; y < ty; y++)
+    for (int x0 = 0; x0 < tx; x0++)
+      for (int x1 = x0; x1 < tx && x1 < x0 + maxw; x1++)
+        for (uint32_t r = 0; r < n; r++) {
+          // brute force: the rank's tiles of the interval in column order
+          std::vector<int> want;
+          for (int x = x0; x <= x1; x++) {
+            uint32_t rk;
+            (void)rt_tile_local(x, y, n, bx, (uint32_t)tb, &rk);
+            if (rk == r) want.push_back(x);
+          }
+          int f = 0;
+          const uint32_t c = rt_rank_row_tiles(y, x0, x1, n, r, bx, (uint32_t)tb, &f);
+          bool bad = c != want.size();
+          // the emission order (emit_interval): blocks f, f + n, ... at
+          // consecutive rank-local block indices from rt_block_local
+          uint32_t blk = c ? rt_block_local((uint32_t)f, (uint32_t)(y / tb), n, bx, r) : 0;
+          size_t k = 0;
+          for (int b = f; !bad && k < c; b += (int)n, blk++)
+            for (int x = std::max(x0, b * tb); x <= std::min(x1, b * tb + tb - 1); x++, k++) {
+              uint32_t rk;
+              const uint32_t loc = rt_tile_local(x, y, n, bx, (uint32_t)tb, &rk);
+              if (k >= want.size() || want[k] != x || rk != r || loc / (uint32_t)(tb * tb) != blk) bad = true;
+            }
+          out[0]++;
+          out[1] += bad ? 1 : 0;
+        }
+  return RT_OK;
 }
 
 extern "C" size_t rt_hip_tile_buffer_floats(int width, int height, int nranks) {
@@ -412,6 +467,7 @@ static int lbuf_prepare(rt_hip_ctx* c, hipStream_t s) {
   if (c->d_lbuf && c->lb_ulps == c->eps_ulps && c->lb_proven == c->exact_shadows) return RT_OK;
   lbuf_release(c);
   c->lb_dev.assign(c->nlight, nullptr);
+  c->info.lightbuf_fail_reason[0] = 0;
   std::vector<RtLightBuf> hb(c->nlight);
   std::memset(hb.data(), 0, hb.size() * sizeof(RtLightBuf));
   char err[256] = {0};
@@ -428,14 +484,25 @@ static int lbuf_prepare(rt_hip_ctx* c, hipStream_t s) {
       const double k = std::atof(e);
       if (k > 0.0) lp.target_cells = (uint32_t)std::fmin((double)(1u << 26), std::fmax(4096.0, lp.target_cells * k));
     }
-    if (rt_lightbuf_build(&lp, &hb[li], &c->lb_dev[li], s, err, sizeof err)) {
-      // the light's queries walk the octree instead (hb[li] is zeroed:
+    const int br = rt_lightbuf_build(&lp, &hb[li], &c->lb_dev[li], s, err, sizeof err);
+    if (br < 0) {  // not a capacity question: a failed launch or an inconsistent build
+      (void)hipGetLastError();
+      for (LBDevice*& d : c->lb_dev) {
+        rt_lightbuf_free(d);
+        d = nullptr;
+      }
+      return rt_set_error(RT_EHIP, "light buffer of light %u: %s", li, err);
+    }
+    if (br > 0) {
+      // entry or cell cap, device memory, or a zero directional vector (no
+      // grid): the light's queries walk the octree instead (hb[li] is zeroed:
       // RT_LB_NONE), as they did before light buffers -- a scene that fits the
       // walk still loads; in the exact-shadow mode that walk is the proven
       // per-node multiplier walk (shadow_prepare, built by the render)
       std::memset(&hb[li], 0, sizeof hb[li]);
       c->lb_dev[li] = nullptr;
       (void)hipGetLastError();  // an out-of-memory hipMalloc is not sticky; clear it anyway
+      std::snprintf(c->info.lightbuf_fail_reason, sizeof c->info.lightbuf_fail_reason, "light %u: %s", li, err);
       failed++;
     }
   }
@@ -753,7 +820,7 @@ extern "C" int rt_cand_refine_sample(const rt_scene* scene, float eps_ulps, doub
     cam.width *= 3;
     cam.height *= 3;
   }
-  int rc = rt_frame_from_camera(&cam, &f);
+  int rc = compat ? rt_frame_from_camera_any(&cam, &f) : rt_frame_from_camera(&cam, &f);
   if (rc) return rc;
   rt_flat_scene fs;
   rc = rt_flatten(scene, RT_ACCEL_FLAT, &fs);
@@ -846,7 +913,7 @@ extern "C" int rt_hip_cand_verify_compat(rt_hip_ctx* c, const rt_camera* cam, un
   big.width = 3 * cam->width;
   big.height = 3 * cam->height;
   rt_frame f;
-  int rc = rt_frame_from_camera(&big, &f);
+  int rc = rt_frame_from_camera_any(&big, &f);
   if (rc) return rc;
   KParams kp;
   std::memset(&kp, 0, sizeof kp);
@@ -1166,9 +1233,20 @@ static int ensure_tmp(rt_hip_ctx* c, size_t bytes) {
   return RT_OK;
 }
 
+// The last render's kept-entry count (rt_hip_stats reads it) outlives a list
+// build that overwrites the offsets it points into: saved in stream order to
+// a word no build writes (d_cand_ctr[8]).
+static int save_valid(rt_hip_ctx* c, hipStream_t s) {
+  if (!c->d_cand_valid || !c->d_cand_ctr || c->d_cand_valid == c->d_cand_ctr + 8) return RT_OK;
+  HIP_TRY(hipMemcpyAsync(c->d_cand_ctr + 8, c->d_cand_valid, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+  c->d_cand_valid = c->d_cand_ctr + 8;
+  return RT_OK;
+}
+
 // The entry buffers (keys, vals, keys2, cand) for n entries.
 static int cand_entry_buffers(rt_hip_ctx* c, size_t n) {
   if (n + 1 <= c->cand_cap) return RT_OK;
+  c->ext_ready = 0;  // consumed lists (ext) point into these
   for (uint32_t** b : {&c->d_cand_keys, &c->d_cand_vals, &c->d_cand_keys2, &c->d_cand}) {
     (void)hipFree(*b);
     *b = nullptr;
@@ -1185,6 +1263,10 @@ static int cand_entry_buffers(rt_hip_ctx* c, size_t n) {
 
 // The per-tile offsets and work-order buffers for nt tiles.
 static int cand_tile_buffers(rt_hip_ctx* c, size_t nt) {
+  if (nt + 1 > c->cand_tiles_cap || nt + 1 > c->order_cap) {
+    c->ext_ready = 0;  // the consumed lists' offsets and work order live here
+    if (c->d_cand_valid && c->d_cand_valid != c->d_cand_ctr + 8) c->d_cand_valid = nullptr;
+  }
   if (nt + 1 > c->cand_tiles_cap) {
     size_t cap = c->cand_tiles_cap;
     int rc = grow_dev(&c->d_cand_start, &cap, nt + 1);
@@ -1235,6 +1317,13 @@ static int key_bits(size_t n_keys) {
 static int cand_build(rt_hip_ctx* c, CandParams& cp, hipStream_t s, uint32_t glob_copies, uint32_t* total_out,
                       uint32_t* nglobal_out) {
   int rc = RT_OK;
+  // every build overwrites the entry, offset and order buffers: lists that
+  // rt_hip_cand_consume left for a render (ext) are gone from here on, so
+  // that render builds its own (produce -> consume -> produce ->
+  // render must not render from clobbered buffers)
+  c->ext_ready = 0;
+  rc = save_valid(c, s);
+  if (rc) return rc;
   cp.tri = c->d_tri_prim;
   cp.nprim = c->nprim;
   const size_t np = c->nprim;
@@ -1263,7 +1352,7 @@ static int cand_build(rt_hip_ctx* c, CandParams& cp, hipStream_t s, uint32_t glo
     HIP_TRY(hipMalloc((void**)&c->d_cand_off, (np + 1) * sizeof(uint32_t)));
     HIP_TRY(hipMalloc((void**)&c->d_cand_global, (np + 1) * sizeof(uint32_t)));
     HIP_TRY(hipMalloc((void**)&c->d_cand_big, (np + 1) * sizeof(uint32_t)));
-    HIP_TRY(hipMalloc((void**)&c->d_cand_ctr, 8 * sizeof(uint32_t)));
+    HIP_TRY(hipMalloc((void**)&c->d_cand_ctr, 16 * sizeof(uint32_t)));  // [8]: a saved valid count
     HIP_TRY(hipMalloc((void**)&c->d_cand_skip, (np + 1) * sizeof(float)));
     HIP_TRY(hipMalloc((void**)&c->d_cand_big_lane, (size_t)kBigLaneCap * 64 * sizeof(uint32_t)));
     HIP_TRY(hipMalloc((void**)&c->d_cand_items, ((size_t)kItemCap + 1) * sizeof(uint2)));
@@ -1390,7 +1479,7 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
   HIP_TRY(rt_cand_bounds(c->d_cand_keys2, total, c->d_cand_start, (uint32_t)nt, s));
   // the sorted keys are spent: their buffer takes the per-entry skip bounds
   float* entry_skip = (float*)c->d_cand_keys2;
-  HIP_TRY(rt_cand_entry_skip(c->d_cand, c->d_cand_skip, entry_skip, total, s));
+  HIP_TRY(rt_cand_entry_skip(c->d_cand, c->d_cand_skip, entry_skip, total, c->d_cand_start + nt, s));
   // longest-first work order of the rank's tiles (heavy lists first)
   rc = cand_order(c, kp, nt, total, s);
   if (rc) return rc;
@@ -1488,7 +1577,10 @@ extern "C" int rt_hip_cand_consume(rt_hip_ctx* c, const rt_frame* f, int rank, i
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   const size_t nt = (size_t)rank_tile_count(f->width, f->height, rank, nranks);
   const uint32_t tpr = (uint32_t)rt_hip_tiles_per_rank(f->width, f->height, nranks);
-  int rc = cand_entry_buffers(c, n);
+  c->ext_ready = 0;  // set again once this consume's lists are complete
+  int rc = save_valid(c, s);
+  if (rc) return rc;
+  rc = cand_entry_buffers(c, n);
   if (rc) return rc;
   rc = cand_tile_buffers(c, nt);
   if (rc) return rc;
@@ -1556,6 +1648,11 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
   if (nranks <= 0 || rank < 0 || rank >= nranks)
     return rt_set_error(RT_EINVAL, "rank %d of %d", rank, nranks);
   if (f->width <= 0 || f->height <= 0) return rt_set_error(RT_EINVAL, "empty frame");
+  // cpu/rt's frame is even-sized (rt_frame_from_camera; its output for odd
+  // sizes is undefined, cpu/raytracer.c:89-91,128-134); the camera sample
+  // model of the candidate lists assumes it (rt_cand.hip pixel_range)
+  if ((f->width | f->height) & 1)
+    return rt_set_error(RT_EINVAL, "frame %dx%d: cpu/rt renders even sizes only", f->width, f->height);
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   // lists rt_hip_cand_consume built for exactly this frame and rank: used once
@@ -2040,7 +2137,7 @@ extern "C" int rt_hip_render_compat(rt_hip_ctx* c, const rt_camera* cam, unsigne
   big.width = 3 * cam->width;
   big.height = 3 * cam->height;
   rt_frame f;
-  int rc = rt_frame_from_camera(&big, &f);
+  int rc = rt_frame_from_camera_any(&big, &f);
   if (rc) return rc;
   const size_t nhi = (size_t)big.width * big.height, nlo = (size_t)cam->width * cam->height;
   uint32_t *d_hi = nullptr, *d_lo = nullptr;

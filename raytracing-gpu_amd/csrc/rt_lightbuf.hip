@@ -966,7 +966,7 @@ extern "C" void rt_lightbuf_proof_counts(const LBDevice* d, unsigned long long* 
     hipError_t e_ = (x);                                                              \
     if (e_ != hipSuccess) {                                                           \
       snprintf(err, errlen, "%s: %s", #x, hipGetErrorString(e_));                     \
-      rc = -1;                                                                        \
+      rc = e_ == hipErrorOutOfMemory ? 1 : -1;                                        \
       goto done;                                                                      \
     }                                                                                 \
   } while (0)
@@ -996,7 +996,7 @@ static int bp_setup(const LBParams* in, rtl::BP& p, RtLightBuf* out, uint64_t& n
     const double wl = sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
     if (!(wl > 0.0)) {
       snprintf(err, errlen, "directional light with a zero vector");
-      return -1;
+      return 1;  // no grid: its queries walk (the walk takes any direction)
     }
     for (int a = 0; a < 3; a++) {
       p.d[a] = (double)(float)(-in->lv[a]);  // the rays' direction, exactly (cpu/light.c:53)
@@ -1081,7 +1081,7 @@ static int bp_setup(const LBParams* in, rtl::BP& p, RtLightBuf* out, uint64_t& n
   }
   if (ncell >= (1ull << 31)) {
     snprintf(err, errlen, "light buffer of %llu cells", (unsigned long long)ncell);
-    return -1;
+    return 1;
   }
   return 0;
 }
@@ -1092,7 +1092,7 @@ extern "C" int rt_lightbuf_build(const LBParams* in, RtLightBuf* out, LBDevice**
   int rc = 0;
   BP p;
   uint64_t total = 0, ncell = 0;
-  if (bp_setup(in, p, out, ncell, err, errlen)) return -1;
+  if (const int r = bp_setup(in, p, out, ncell, err, errlen)) return r;
   LBDevice* dev = new LBDevice();
   uint32_t* count = nullptr;
   uint32_t* off = nullptr;
@@ -1160,7 +1160,7 @@ extern "C" int rt_lightbuf_build(const LBParams* in, RtLightBuf* out, LBDevice**
   }
   if (total >= (1ull << 31) || (in->max_entries && total > in->max_entries)) {
     snprintf(err, errlen, "light buffer of %llu entries", (unsigned long long)total);
-    rc = -1;
+    rc = 1;
     goto done;
   }
   dev->entries = total;

@@ -1,18 +1,28 @@
 // rt_tiles.h -- how the frame's 8x8-pixel tiles are dealt to ranks, shared
 // by the device kernels (render, candidate lists, assemble) and their host
-// mirrors (rt_hip.cpp, the host re-derivation of the candidate lists).
+// mirrors (rt_hip.cpp, the host re-derivation of the candidate lists,
+// rtgpu.py's tile_xy / tile_local).
 //
 // Tiles are grouped into blocks of tb x tb tiles, tb = rt_block_side(nranks):
 // 4 (32 x 32 pixels) when the frame is split, 1 (plain scanline tile order)
-// for one rank.  Block b (scanline order, blocks_x = ceil(tiles_x / tb) per
-// row) belongs to rank b mod nranks.  A rank's tile buffer holds its blocks
-// in order, each as tb^2 tiles in row-major order (tiles past the frame's
-// edge are padding: their pixels are invalid and written as 0).  With whole blocks a
-// camera-ray candidate footprint (csrc/rt_cand.hip) of a few tiles touches
-// one or two ranks instead of one rank per 8-pixel column (the round-2
-// interleave t mod nranks made every rank classify every footprint wider
-// than 8 nranks pixels), and every rank still holds 1/nranks of every block
-// row, so the per-rank cost stays balanced.
+// for one rank.  Block (bx, by) (blocks_x = ceil(tiles_x / tb) per row)
+// belongs to rank (bx + by) mod n: diagonals.  A rank's tile buffer holds its
+// blocks in scanline order, each as tb^2 tiles in row-major order (tiles past
+// the frame's edge are padding: their pixels are invalid and written as 0).
+//
+// Why whole blocks: a camera-ray candidate footprint (csrc/rt_cand.hip) of a
+// few tiles touches one or two ranks instead of one rank per 8-pixel column
+// (round 2's interleave t mod n made every rank classify every footprint
+// wider than 8 n pixels).  Why diagonals: rounds 3-4 dealt block b (scanline)
+// to rank b mod n, and at 4K blocks_x = 120 is a multiple of 2, 4 and 8, so
+// every rank owned the same block columns in every block row -- pure 32-pixel
+// column stripes, and a scene whose cost varies by column (C5's grid of
+// spheres) loaded one rank 25 % above the mean at N = 8 (VERDICT r04 weak
+// #5).  On diagonals every rank holds 1/n of every block row (up to one
+// block) and of every block column (up to one block per n rows) whatever
+// blocks_x is, so a cost that varies by row or by column alone spreads
+// evenly.  Every n consecutive block rows give each rank exactly blocks_x
+// blocks, which keeps the rank-local index arithmetic O(1).
 //
 // cpu/rt splits the frame into 4 quadrants for its 4 pthreads
 // (cpu/raytracer.c:92-127); this is the same idea sized for 8 GPUs x 256 CUs.
@@ -32,36 +42,88 @@ RT_TILES_FN int rt_block_side(int nranks) { return nranks > 1 ? RT_TB : 1; }
 RT_TILES_FN int rt_blocks_x(int tiles_x, int tb) { return (tiles_x + tb - 1) / tb; }
 RT_TILES_FN int rt_blocks_y(int tiles_y, int tb) { return (tiles_y + tb - 1) / tb; }
 
-// blocks of rank r (b = r, r + n, ... < nblocks)
-RT_TILES_FN uint32_t rt_rank_blocks(uint32_t nblocks, uint32_t n, uint32_t r) {
-  return nblocks > r ? (nblocks - r + n - 1) / n : 0u;
+// the first block column of rank r in block row by (then every n-th)
+RT_TILES_FN uint32_t rt_row_res(uint32_t by, uint32_t n, uint32_t r) { return (r + n - by % n) % n; }
+
+// #{t in [0, x) : t mod n < rm}
+RT_TILES_FN uint32_t rt_count_low(uint32_t x, uint32_t n, uint32_t rm) {
+  const uint32_t k = x % n;
+  return (x / n) * rm + (k < rm ? k : rm);
 }
 
-// (tx, ty) of rank-local tile t of rank r
+// Blocks of rank r in block rows [0, by): row y holds q + [res(y) < rm] of
+// them (blocks_x = q n + rm), and n consecutive rows hold blocks_x in all.
+RT_TILES_FN uint32_t rt_rank_rows_blocks(uint32_t by, uint32_t blocks_x, uint32_t n, uint32_t r) {
+  if (n == 1) return by * blocks_x;
+  const uint32_t q = blocks_x / n, rm = blocks_x % n, L = by % n;
+  // the last L rows of [0, by) have res = r - y' (mod n) for y' = 0 .. L-1:
+  // the integers r - L + 1 .. r, shifted by n to stay >= 0
+  const uint32_t part = rt_count_low(r + n + 1, n, rm) - rt_count_low(r + n + 1 - L, n, rm);
+  return (by / n) * blocks_x + (by % n) * q + part;
+}
+
+// blocks of rank r in a frame of blocks_x x blocks_y blocks
+RT_TILES_FN uint32_t rt_rank_blocks(uint32_t blocks_x, uint32_t blocks_y, uint32_t n, uint32_t r) {
+  return rt_rank_rows_blocks(blocks_y, blocks_x, n, r);
+}
+
+// the most blocks any rank holds (the tile buffers' stride; host side, O(n))
+RT_TILES_FN uint32_t rt_max_rank_blocks(uint32_t blocks_x, uint32_t blocks_y, uint32_t n) {
+  uint32_t m = 0;
+  for (uint32_t r = 0; r < n; r++) {
+    const uint32_t c = rt_rank_blocks(blocks_x, blocks_y, n, r);
+    m = c > m ? c : m;
+  }
+  return m;
+}
+
+// (tx, ty) of rank-local tile t of rank r: block j = t / tb^2 of the rank,
+// its row found by bisection over the rank's per-row prefix counts
 RT_TILES_FN void rt_tile_xy(uint32_t t, uint32_t r, uint32_t n, uint32_t blocks_x, uint32_t tb,
                             int* tx, int* ty) {
-  const uint32_t b = (t / (tb * tb)) * n + r, k = t % (tb * tb);
-  *tx = (int)((b % blocks_x) * tb + k % tb);
-  *ty = (int)((b / blocks_x) * tb + k / tb);
+  const uint32_t j = t / (tb * tb), k = t % (tb * tb);
+  if (n == 1) {  // one rank: scanline order
+    *tx = (int)((j % blocks_x) * tb + k % tb);
+    *ty = (int)((j / blocks_x) * tb + k / tb);
+    return;
+  }
+  // j lies in the period of n rows m = j / blocks_x (blocks_x blocks each)
+  uint32_t lo = (j / blocks_x) * n, hi = lo + n;  // rows(lo) <= j < rows(hi)
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) / 2;
+    if (rt_rank_rows_blocks(mid, blocks_x, n, r) <= j) lo = mid; else hi = mid;
+  }
+  const uint32_t by = lo, bx = rt_row_res(by, n, r) + (j - rt_rank_rows_blocks(by, blocks_x, n, r)) * n;
+  *tx = (int)(bx * tb + k % tb);
+  *ty = (int)(by * tb + k / tb);
 }
 
 // rank and rank-local index of tile (tx, ty)
 RT_TILES_FN uint32_t rt_tile_local(int tx, int ty, uint32_t n, uint32_t blocks_x, uint32_t tb,
                                    uint32_t* rank) {
-  const uint32_t b = (uint32_t)ty / tb * blocks_x + (uint32_t)tx / tb;
-  *rank = b % n;
-  return (b / n) * tb * tb + ((uint32_t)ty % tb) * tb + (uint32_t)tx % tb;
+  const uint32_t bx = (uint32_t)tx / tb, by = (uint32_t)ty / tb;
+  const uint32_t r = (bx + by) % n;
+  *rank = r;
+  return (rt_rank_rows_blocks(by, blocks_x, n, r) + bx / n) * tb * tb + ((uint32_t)ty % tb) * tb +
+         (uint32_t)tx % tb;
+}
+
+// rank-local index of block column bx of block row by, for the rank owning it
+RT_TILES_FN uint32_t rt_block_local(uint32_t bx, uint32_t by, uint32_t n, uint32_t blocks_x, uint32_t r) {
+  return rt_rank_rows_blocks(by, blocks_x, n, r) + bx / n;
 }
 
 // Rank r's tiles in tile row ty, columns [x0, x1] (x0 <= x1): the blocks of
-// the row whose index is r mod n, each contributing its columns inside the
-// interval.  first_bx (out, optional) = the first such block column.
+// the row whose column is res(by) mod n, each contributing its columns
+// inside the interval.  first_bx (out, optional) = the first such block
+// column; the next ones follow every n columns.  O(1).
 RT_TILES_FN uint32_t rt_rank_row_tiles(int ty, int x0, int x1, uint32_t n, uint32_t r,
                                        uint32_t blocks_x, uint32_t tb, int* first_bx) {
+  (void)blocks_x;
   const uint32_t by = (uint32_t)ty / tb;
   const uint32_t bx0 = (uint32_t)x0 / tb, bx1 = (uint32_t)x1 / tb;
-  // block columns bx with (by blocks_x + bx) mod n == r: bx = res + m n
-  const uint32_t res = (uint32_t)((r + n - (uint32_t)(((uint64_t)by * blocks_x) % n)) % n);
+  // block columns bx with (bx + by) mod n == r: bx = res + m n
+  const uint32_t res = rt_row_res(by, n, r);
   const uint32_t f = bx0 <= res ? res : bx0 + (res + n - bx0 % n) % n;  // first match >= bx0
   if (first_bx) *first_bx = (int)f;
   if (f > bx1) return 0;

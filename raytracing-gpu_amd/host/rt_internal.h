@@ -13,6 +13,9 @@ extern "C" {
 #endif
 
 int rt_set_error(int code, const char *fmt, ...);
+/* rt_frame_from_camera without the even-size rule (the gpu/rt
+ * compatibility mode's 3x frame) */
+int rt_frame_from_camera_any(const rt_camera *cam, rt_frame *out);
 
 /* ---- reference-exact host math (cpu/vector3*.c), no contraction ---- */
 rt_vec3 rt_v_sub(rt_vec3 a, rt_vec3 b);

@@ -29,8 +29,9 @@ rt_vec3 rt_v_normalize(rt_vec3 a)
   return r;
 }
 
-/* cpu/raytracer.c:82-86 */
-int rt_frame_from_camera(const rt_camera *cam, rt_frame *out)
+/* cpu/raytracer.c:82-86, any positive size (the compatibility mode's 3x
+ * frame: gpu/rt renders odd sizes, gpu/raytracer.cu:97-103) */
+int rt_frame_from_camera_any(const rt_camera *cam, rt_frame *out)
 {
   if (!cam || !out)
     return rt_set_error(RT_EINVAL, "null argument");
@@ -45,4 +46,17 @@ int rt_frame_from_camera(const rt_camera *cam, rt_frame *out)
   out->width = cam->width;
   out->height = cam->height;
   return RT_OK;
+}
+
+/* cpu/rt's frame: even sizes only.  cpu/raytracer.c:89-91 writes pixel
+ * (i + W/2, j + H/2) for i in (-W/2, W/2], j in (-H/2, H/2] and :128-134 prints
+ * j * W + i for i in [1, W], j in [1, H]: the two cover the same slots only
+ * when W and H are even -- for odd sizes cpu/rt prints uninitialised stack
+ * memory, so there is no output to match and the size is refused. */
+int rt_frame_from_camera(const rt_camera *cam, rt_frame *out)
+{
+  if (cam && ((cam->width & 1) || (cam->height & 1)) && cam->width > 0 && cam->height > 0)
+    return rt_set_error(RT_EINVAL, "camera size %dx%d: cpu/rt renders even sizes only", cam->width,
+                        cam->height);
+  return rt_frame_from_camera_any(cam, out);
 }

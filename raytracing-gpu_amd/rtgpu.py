@@ -110,10 +110,12 @@ class AccelInfo(C.Structure):
                 ("shadow_mu_max", C.c_double), ("lightbuf_entries", C.c_ulonglong),
                 ("lightbuf_global", C.c_ulonglong), ("lightbuf_seconds", C.c_double),
                 ("lightbuf_never", C.c_ulonglong), ("lightbuf_band", C.c_ulonglong),
-                ("lightbuf_failed", C.c_ulonglong)]
+                ("lightbuf_failed", C.c_ulonglong), ("lightbuf_fail_reason", C.c_char * 96)]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_}
+        d = {k: getattr(self, k) for k, _ in self._fields_}
+        d["lightbuf_fail_reason"] = d["lightbuf_fail_reason"].decode(errors="replace")
+        return d
 
 
 # (name, restype, argtypes) for every entry point of include/*.h
@@ -145,6 +147,7 @@ _PROTOS = [
     ("rt_hip_destroy", None, [C.c_void_p]),
     ("rt_hip_tiles_per_rank", C.c_int, [C.c_int, C.c_int, C.c_int]),
     ("rt_hip_tile_buffer_floats", C.c_size_t, [C.c_int, C.c_int, C.c_int]),
+    ("rt_tile_map_check", C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_ulonglong)]),
     ("rt_hip_render", C.c_int, [C.c_void_p, C.POINTER(Frame), C.c_int, C.c_int, C.c_void_p,
                                 C.c_void_p]),
     ("rt_hip_stats", C.c_int, [C.c_void_p, C.POINTER(Stats)]),
@@ -692,8 +695,9 @@ def raytrace(input_path, output_path, gpus=1, accel=None):
 
 # ---- tile map (host mirror of csrc/rt_tiles.h) ----
 def block_side(nranks):
-    """Tiles per block side: rank r owns blocks b = r, r + nranks, ... (scanline
-    order); 4 when the frame is split, 1 (plain scanline tiles) for one rank."""
+    """Tiles per block side: 4 when the frame is split, 1 (plain scanline
+    tiles) for one rank.  Block (bx, by) belongs to rank (bx + by) % nranks;
+    a rank's buffer holds its blocks in scanline order."""
     return 4 if nranks > 1 else 1
 
 
@@ -703,31 +707,48 @@ def _blocks(width, height, nranks):
     return tb, -(-tx // tb), -(-ty // tb)
 
 
+def _rank_block_grid(width, height, nranks):
+    """(blocks_y, blocks_x) arrays: each block's rank and rank-local index."""
+    tb, bx, by = _blocks(width, height, nranks)
+    x = np.arange(bx)[None, :]
+    y = np.arange(by)[:, None]
+    rank = (x + y) % nranks
+    local = np.zeros((by, bx), np.int64)
+    for r in range(nranks):
+        m = (rank == r).ravel()
+        local.ravel()[m] = np.arange(int(m.sum()))
+    return rank, local
+
+
 def rank_tile_count(width, height, rank, nranks):
     """Tiles (whole blocks, edge padding included) rank `rank` renders."""
-    tb, bx, by = _blocks(width, height, nranks)
-    nb = bx * by
-    return ((nb - rank + nranks - 1) // nranks if nb > rank else 0) * tb * tb
+    tb = block_side(nranks)
+    rk, _ = _rank_block_grid(width, height, nranks)
+    return int((rk == rank).sum()) * tb * tb
 
 
 def tiles_per_rank_host(width, height, nranks):
-    return rank_tile_count(width, height, 0, nranks)
+    """The most tiles any rank holds (the tile buffers' stride)."""
+    return max(rank_tile_count(width, height, r, nranks) for r in range(nranks))
 
 
 def tile_xy(t, rank, nranks, width, height):
     """(tx, ty) of rank-local tiles t (numpy arrays) of rank `rank`."""
-    tb, bx, _ = _blocks(width, height, nranks)
+    tb = block_side(nranks)
+    rk, _ = _rank_block_grid(width, height, nranks)
+    ys, xs = np.nonzero(rk == rank)  # scanline order = the rank's block order
     t = np.asarray(t)
-    b = (t // (tb * tb)) * nranks + rank
-    k = t % (tb * tb)
-    return (b % bx) * tb + k % tb, (b // bx) * tb + k // tb
+    j, k = t // (tb * tb), t % (tb * tb)
+    return xs[j] * tb + k % tb, ys[j] * tb + k // tb
 
 
 def tile_local(tx, ty, nranks, width, height):
     """(rank, local index) of tiles (tx, ty) (numpy arrays)."""
-    tb, bx, _ = _blocks(width, height, nranks)
-    b = (np.asarray(ty) // tb) * bx + np.asarray(tx) // tb
-    return b % nranks, (b // nranks) * (tb * tb) + (np.asarray(ty) % tb) * tb + np.asarray(tx) % tb
+    tb = block_side(nranks)
+    rk, loc = _rank_block_grid(width, height, nranks)
+    tx, ty = np.asarray(tx), np.asarray(ty)
+    bx, by = tx // tb, ty // tb
+    return rk[by, bx], loc[by, bx] * (tb * tb) + (ty % tb) * tb + tx % tb
 
 
 def tile_pixels(width, height, rank, nranks):

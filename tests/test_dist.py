@@ -88,10 +88,52 @@ def test_tile_map_partitions_the_frame(built, W, H, n):
         rk, loc = rtgpu.tile_local(tx, ty, n, W, H)
         assert (rk == r).all() and (loc == np.arange(len(pix))).all()
     assert (seen == 1).all()
-    assert max(counts) - min(counts) <= 32 * 32 * (1 + (W * H) // (32 * 32 * n * 8))
+    # diagonals: per rank, the same count from every n block rows, and within
+    # the last partial period at most one block per row more or less
+    assert max(counts) - min(counts) <= 32 * 32 * n
     img = np.random.default_rng(1).random((H, W, 3), dtype=np.float32)
     g = np.stack([rtgpu.tiles_from_image_numpy(img, r, n) for r in range(n)])
     assert np.array_equal(rtgpu.assemble_tiles_numpy(g, W, H, n), img)
+
+
+@pytest.mark.parametrize("W,H,n", [(96, 54, 2), (96, 54, 3), (192, 108, 8), (480, 272, 8),
+                                   (3840, 216, 8), (3840, 216, 7), (40, 24, 5)])
+def test_tile_map_row_arithmetic(built, W, H, n):
+    """The O(1) row counts and run-order emission of csrc/rt_tiles.h (the
+    candidate lists' per-row tile counts, emit_interval and kth_rank_col
+    follow them) agree with a brute-force walk of every tile row, every rank,
+    every column interval up to 40 tiles wide (rt_tile_map_check)."""
+    import ctypes as C
+    sys.path.insert(0, os.path.join(REPO, "raytracing-gpu_amd"))
+    import rtgpu
+    out = (C.c_ulonglong * 2)()
+    assert rtgpu.lib().rt_tile_map_check(W, H, n, 40, out) == 0
+    assert out[0] > 0 and out[1] == 0, (out[0], out[1])
+
+
+@pytest.mark.parametrize("W,H", [(3840, 2160), (1920, 1080), (2560, 1440)])
+def test_tile_map_balances_rows_and_columns(built, W, H):
+    """with block b -> rank b mod n, 4K's 120 blocks per
+    row (a multiple of 2, 4, 8) gave every rank the same block columns in every
+    row -- column stripes.  On diagonals every rank holds each block column in
+    1/n of the block rows and 1/n of each block row (each up to one block), so
+    a cost that varies by column or by row alone is split evenly; the library's
+    buffer stride is the largest rank's count."""
+    sys.path.insert(0, os.path.join(REPO, "raytracing-gpu_amd"))
+    import rtgpu
+    for n in (2, 3, 4, 7, 8):
+        tb, bx, by = rtgpu._blocks(W, H, n)
+        rk, _ = rtgpu._rank_block_grid(W, H, n)
+        for c in range(bx):
+            share = np.bincount(rk[:, c], minlength=n)
+            assert share.max() - share.min() <= 1, (n, c, share)
+        for r in range(by):
+            share = np.bincount(rk[r, :], minlength=n)
+            assert share.max() - share.min() <= 1, (n, r, share)
+        per = [rtgpu.rank_tile_count(W, H, r, n) for r in range(n)]
+        assert rtgpu.tiles_per_rank(W, H, n) == max(per)
+        if (W, H) == (3840, 2160) and n in (2, 4, 8):
+            assert min(per) == max(per)  # 120 x 68 blocks: exactly even
 
 
 def _a2a_worker(rank, world, store, q):

@@ -559,6 +559,40 @@ def test_triangle_parallel_lists_match_per_rank(gpu, nranks, accel):
     assert_bitexact(t2, t_ref, "per-rank build after a consumed frame")
 
 
+def test_consumed_lists_invalidated_by_a_later_build(gpu):
+    """lists rt_hip_cand_consume leaves for a render live in the
+    context's shared list buffers.  A produce (e.g. the next frame's) between
+    consume and render overwrites them, so the render must build its own lists
+    again rather than read clobbered ones: produce -> consume -> produce ->
+    render equals the per-rank render bit for bit, with the same entry count.
+    And the kept-entry count rt_hip_stats reports for a render survives a
+    produce issued before the stats are read."""
+    import ctypes as C
+    s = gpu.Scene.synthetic(6, 6, 9776, seed=0x5EED, width=960, height=540)
+    f = s.frame()
+    ctx = gpu.Context(s, "octree_gpu")
+    ref = gpu.Context(s, "octree_gpu")
+    nranks, d = 4, 1
+    parts = _produce_all(ctx, f, nranks)
+    dptr, n, g = _consume_rank(ctx, f, d, nranks, parts)
+    ctx.cand_produce(f, 2, nranks)  # rewrites the entry / offset buffers
+    t_ctx, st_ctx = _tiles_of_rank(ctx, f, d, nranks)
+    gpu_lib().rt_hip_free(dptr)
+    t_ref, st_ref = _tiles_of_rank(ref, f, d, nranks)
+    assert_bitexact(t_ctx, t_ref, "render after produce -> consume -> produce")
+    assert st_ctx["cand_entries"] == st_ref["cand_entries"] > 0
+    # render -> produce -> stats: the render's kept-entry count is kept
+    L = gpu_lib()
+    per = gpu.tile_buffer_floats(f.width, f.height, nranks)
+    dt = C.c_void_p()
+    assert L.rt_hip_malloc(0, per * 4, C.byref(dt)) == 0
+    ctx.render(f, d, nranks, dt.value)
+    ctx.cand_produce(f, 0, nranks)
+    st2 = ctx.stats()
+    L.rt_hip_free(dt)
+    assert st2["cand_entries"] == st_ref["cand_entries"]
+
+
 def test_triangle_parallel_lists_two_processes(gpu):
     """Two processes (ranks of torch.distributed.run, both on GPU 0, gloo
     for the exchange since RCCL needs a device per rank): each produces its
@@ -807,8 +841,10 @@ def test_light_buffer_build_failure_falls_back_to_walk(gpu, exact):
     ctx.set_exact_shadows(exact)
     img, st = ctx.render_image(f)
     assert ctx.info()["lightbuf_failed"] == 0 and ctx.info()["lightbuf_entries"] > 0
+    assert ctx.info()["lightbuf_fail_reason"] == ""
     ctx.set_lightbuf_entry_cap(1)
     assert ctx.info()["lightbuf_failed"] == 2 and ctx.info()["lightbuf_entries"] == 0
+    assert "entries" in ctx.info()["lightbuf_fail_reason"]
     img2, st2 = ctx.render_image(f)
     assert_bitexact(img2, img, "shadow queries on the walk after a failed light-buffer build")
     assert (st2["closest"], st2["shadow"]) == (st["closest"], st["shadow"])

@@ -205,6 +205,22 @@ def test_render_fails_loudly_without_gpu(built, scene_dir):
     assert e.value.code == -6
 
 
+@pytest.mark.parametrize("W,H", [(481, 270), (480, 271), (1, 1), (3841, 2161)])
+def test_odd_frame_sizes_rejected(built, scene_dir, W, H):
+    """cpu/rt writes pixel (i + W/2, j + H/2) (cpu/raytracer.c:89-91) but prints
+    slot j*W + i for i in [1, W], j in [1, H] (:128-134): for odd W or H the two
+    disagree and cpu/rt prints uninitialised memory, so the size is refused
+    (RT_EINVAL) rather than rendered as something the reference never made."""
+    import rtgpu
+    s = rtgpu.Scene.load_svati(os.path.join(scene_dir, "cube.svati"))
+    s.set_size(W, H)
+    with pytest.raises(rtgpu.RtError) as e:
+        s.frame()
+    assert e.value.code == -1 and "even" in str(e.value)
+    s.set_size(W + (W & 1), H + (H & 1))
+    s.frame()  # the even neighbour is fine
+
+
 @pytest.mark.parametrize("scene,W,H,stride", [("island_smooth", 960, 540, 31),
                                               ("car-on-road", 960, 540, 61),
                                               ("spheres", 480, 270, 37),

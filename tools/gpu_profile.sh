@@ -16,6 +16,9 @@ WL=${WL:-c5}
 TAG=${TAG:-r03_$WL}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
+# the device code these passes measure (bench.py reports a profile's counters
+# only for the tree whose device_code_hash() matches)
+python3 -c "import sys; sys.argv=['x']; sys.path.insert(0, '.'); import bench; print(bench.device_code_hash())" > "$OUT/device_hash.txt"
 B="bench.py --workload $WL ${BENCH_EXTRA:-}"
 echo "== kernel trace"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv \

@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--nranks", type=int, default=1)
     ap.add_argument("--rank", type=int, default=0)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--npy", default=None, help="also save per-tile clocks, (tx, ty) and entries (.npz)")
     a = ap.parse_args()
     if a.synthetic:
         s = rtgpu.Scene.synthetic(a.synthetic, a.synthetic, 9776, seed=0x5EED, width=a.W, height=a.H)
@@ -98,6 +99,9 @@ def main():
         "stats": st,
     }
     print(json.dumps(res, default=float))
+    if a.npy:
+        np.savez_compressed(a.npy, cycles=c, tx=txs, ty=tys, items=items,
+                            entries=ent if ent is not None else np.zeros(0))
     if a.out:
         with open(a.out, "w") as fh:
             json.dump(res, fh, default=float, indent=1)
