@@ -535,7 +535,8 @@ def main():
                                 "light_buffer_global": info["lightbuf_global"],
                                 "light_buffer_never": info["lightbuf_never"],
                                 "light_buffer_band": info["lightbuf_band"],
-                                "light_buffer_seconds": round(info["lightbuf_seconds"], 3)},
+                                "light_buffer_seconds": round(info["lightbuf_seconds"], 3),
+                                "persistent_grid": {"trace": info["trace_grid"], "shade": info["shade_grid"]}},
                 "parallelism": f"image tiles over {world} GPU(s) + RCCL gather" if world > 1
                                else "1 GPU",
                 # camera rays: candidate lists; shadow rays: proven light buffers

@@ -129,6 +129,8 @@ typedef struct rt_accel_info {
    * mode).  Any other build failure fails the call (RT_EHIP). */
   unsigned long long lightbuf_failed;
   char lightbuf_fail_reason[96]; /* the last such fallback's cause ("" if none) */
+  int trace_grid, shade_grid;    /* persistent one-wave workgroups of the default
+                                    trace / shade kernels (occupancy-derived) */
 } rt_accel_info;
 
 /* Host-only: build the acceleration structure rt_hip_create would build and
@@ -271,6 +273,13 @@ int rt_lightbuf_survey(const rt_scene *scene, unsigned light, int exact, unsigne
  * triangle (brute = 1, cpu/hit.c:93-109); hit[i] = 1 when shadowed. */
 int rt_hip_probe_shadows(rt_hip_ctx *ctx, unsigned light, const float *origins, size_t n, int brute,
                          unsigned char *hit);
+/* Closest-hit probe (tests, tools): n rays (origins[3 i..], dirs[3 i..],
+ * floats) queried as reflection rays are -- the per-lane octree walk at the
+ * secondary rays' culling slack (brute = 0; octree contexts) -- or by brute
+ * force over every triangle (brute = 1, cpu/hit.c:72-91).  prim[i] = the
+ * winner (object-major LIFO index, ~0 = no hit), dist[i] = its new_dist. */
+int rt_hip_probe_closest(rt_hip_ctx *ctx, const float *origins, const float *dirs, size_t n, int brute,
+                         unsigned *prim, float *dist);
 /* Octree traversal policy (default 0): 0 = staged packet walk for camera
  * rays (>= 8 querying lanes), per-lane walks otherwise; 1 = every query per lane;
  * 2 = every query as a staged packet; 3 = 0 plus staged packet walks for

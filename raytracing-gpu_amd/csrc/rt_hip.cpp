@@ -711,6 +711,8 @@ extern "C" int rt_hip_create(int device, const rt_scene* scene, int accel, rt_hi
         c->grid_of[tr][pol][cw] = g;
         gmax = g > gmax ? g : gmax;
       }
+  c->info.trace_grid = c->grid_of[1][RT_POLICY_DEFAULT][0];
+  c->info.shade_grid = c->grid_of[0][RT_POLICY_LBUF][0];
   // per-lane traversal stack spill area, [entry][lane] for the largest grid
   if (c->accel == RT_ACCEL_OCTREE &&
       hipMalloc((void**)&c->d_spill, (size_t)gmax * 64 * RT_SPILL_STACK * sizeof(uint2)) != hipSuccess) {
@@ -1939,6 +1941,62 @@ done:
 // of n host origins (x, y, z), through the context's light buffer (brute =
 // 0; built as the context's mode -- slack-grown or proven -- says) or by brute
 // force over every triangle (brute = 1).  hit[i] = 1: shadowed.
+extern "C" int rt_hip_probe_closest(rt_hip_ctx* c, const float* origins, const float* dirs, size_t n, int brute,
+                                    unsigned* prim, float* dist) {
+  if (!c || (n && (!origins || !dirs || !prim || !dist))) return rt_set_error(RT_EINVAL, "null argument");
+  if (!brute && (c->accel != RT_ACCEL_OCTREE || !c->d_node || !c->d_spill))
+    return rt_set_error(RT_EINVAL, "the walk probe needs an octree context");
+  if (!c->d_tri_prim) return rt_set_error(RT_EINVAL, "no triangles");
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  KParams p;
+  std::memset(&p, 0, sizeof p);
+  p.tri = c->d_tri;
+  p.node = c->d_node;
+  p.nrec = c->nrec;
+  p.tri_prim = c->d_tri_prim;
+  p.spill = c->d_spill;
+  p.scene_c = rt::f3{c->scene_c[0], c->scene_c[1], c->scene_c[2]};
+  p.scene_r = c->scene_r;
+  p.scene_cmag = std::fmax(std::fabs(c->scene_c[0]), std::fmax(std::fabs(c->scene_c[1]),
+                                                               std::fabs(c->scene_c[2])));
+  p.eps_rel = c->eps_ulps * 5.9604645e-8f;  // the secondary rays' slack (make_ray at depth > 0)
+  int gmax = 0;  // waves the spill area holds (rt_hip_create: the largest persistent grid)
+  for (auto& a : c->grid_of)
+    for (auto& b2 : a)
+      for (int g : b2) gmax = g > gmax ? g : gmax;
+  if (gmax < c->grid) gmax = c->grid;
+  const size_t chunk = (size_t)gmax * 64;
+  float *d_o = nullptr, *d_d = nullptr;
+  uint32_t* d_h = nullptr;
+  const size_t m = n < chunk ? n : chunk;
+  std::vector<uint32_t> h(2 * m + 2);
+  int rc = RT_OK;
+  if (hipMalloc((void**)&d_o, (m * 3 + 1) * sizeof(float)) != hipSuccess ||
+      hipMalloc((void**)&d_d, (m * 3 + 1) * sizeof(float)) != hipSuccess ||
+      hipMalloc((void**)&d_h, (2 * m + 2) * sizeof(uint32_t)) != hipSuccess)
+    rc = rt_set_error(RT_EHIP, "hipMalloc probe buffers");
+  for (size_t at = 0; rc == RT_OK && at < n; at += chunk) {  // the walk's spill area holds `chunk` rays
+    const size_t k = n - at < chunk ? n - at : chunk;
+    if (hipMemcpy(d_o, origins + 3 * at, k * 3 * sizeof(float), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d_d, dirs + 3 * at, k * 3 * sizeof(float), hipMemcpyHostToDevice) != hipSuccess ||
+        rt_launch_probe_closest(&p, d_o, d_d, (uint32_t)k, c->nprim, brute, d_h, gmax, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess ||
+        hipMemcpy(h.data(), d_h, 2 * k * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess) {
+      rc = rt_set_error(RT_EHIP, "closest probe: %s", hipGetErrorString(hipGetLastError()));
+      break;
+    }
+    for (size_t i = 0; i < k; i++) {
+      prim[at + i] = h[2 * i];
+      std::memcpy(&dist[at + i], &h[2 * i + 1], sizeof(float));
+    }
+  }
+  (void)hipFree(d_o);
+  (void)hipFree(d_d);
+  (void)hipFree(d_h);
+  return rc;
+}
+
 extern "C" int rt_hip_probe_shadows(rt_hip_ctx* c, unsigned light, const float* origins, size_t n, int brute,
                                     unsigned char* hit) {
   if (!c || (!origins && n) || (!hit && n)) return rt_set_error(RT_EINVAL, "null argument");

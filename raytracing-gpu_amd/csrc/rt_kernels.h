@@ -174,6 +174,12 @@ extern "C" hipError_t rt_launch_fold(const KParams* p, hipStream_t stream);
 // prim-order records p->tri_prim (brute = 1); out[i] = shadowed
 extern "C" hipError_t rt_launch_probe_shadow(const KParams* p, const float* org, uint32_t n, uint32_t li,
                                              uint32_t nprim, int brute, uint32_t* out, hipStream_t stream);
+// closest-hit probe: ray i = (org[i], dir[i]) through the per-lane walk of a
+// reflection ray (brute = 0) or brute force over nprim prim-order records
+// (brute = 1); out[2 i] = winner prim (~0: none), out[2 i + 1] = new_dist bits.
+// The walk's spill area p->spill holds `grid` waves: n <= 64 grid.
+extern "C" hipError_t rt_launch_probe_closest(const KParams* p, const float* org, const float* dir, uint32_t n,
+                                              uint32_t nprim, int brute, uint32_t* out, int grid, hipStream_t stream);
 // persistent grid (one-wave workgroups) of trace (trace = 1) or shade on `cus` CUs
 extern "C" hipError_t rt_render_grid(int trace, int accel, int count_work, int policy, int cus,
                                      int* grid);

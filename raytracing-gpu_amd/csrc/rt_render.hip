@@ -254,7 +254,10 @@ __device__ __forceinline__ bool any_hit_exact(const Ray& r, const float4& q0, co
 // Per-lane traversal stack: the first kLdsStack entries live in LDS, laid
 // out [entry][lane] so every lane hits its own bank; deeper entries spill to
 // a per-lane area in global memory (rare: typical depth is < 16).
-static constexpr int kLdsStack = 10;  // fills the 10 KB/workgroup LDS budget of 16 workgroups per CU
+#ifndef RT_LDS_STACK
+#define RT_LDS_STACK 10
+#endif
+static constexpr int kLdsStack = RT_LDS_STACK;  // per-lane stack entries in LDS (deeper: global spill)
 static constexpr int kSpillStack = RT_SPILL_STACK;
 
 struct Stack {
@@ -692,6 +695,7 @@ struct WaveCtx {
   float4* stk2;    // kStack2 x 2 float4
   uint64_t* stkm;  // kStack2 lane masks: lanes that wanted the pushed node
   float4* stage;   // kStageFlat / kStageOct float4
+  float4* stage2;  // a second kStageOct stage (the prefetching packet walk), or null
   int lane;
 };
 
@@ -964,6 +968,156 @@ __device__ __forceinline__ void stage_push_children(const Ray& r, f3 inv, uint32
   }
 }
 
+// Asynchronous global -> LDS copies (global_load_lds_dwordx4, "glds"): lane l
+// copies src[l] to dst[l] with no VGPR destination -- a node payload (<= 96
+// float4) in one or two wave instructions.  hipcc does not order the LDS
+// reads of dst after these copies (no s_waitcnt is inserted for them), so
+// every read of a glds buffer is preceded by glds_wait: vmcnt(k) retires
+// every vector-memory load but the last k issued.  The walk that uses them
+// issues no other vector-memory loads while one is in flight.
+#ifndef RT_PF_AHEAD
+#define RT_PF_AHEAD 1  // 0: glds copies of the popped node only (A/B)
+#endif
+#ifndef RT_PF_STAGE2
+#define RT_PF_STAGE2 96  // float4 of the second stage (72 = a 24-record leaf)
+#endif
+static constexpr int kStage2 = RT_PF_STAGE2;
+typedef __attribute__((address_space(3))) float4 lds_float4_t;
+// One glds wave instruction: lane l copies 16 bytes from its own global
+// address to dst + 16 l (dst wave-uniform, in M0).  Inline asm, so hipcc's
+// s_waitcnt bookkeeping does not see it: the builtin made hipcc wait
+// vmcnt(0) before every LDS read of the walk while a copy was in flight --
+// including a prefetch not yet needed (C5 trace 4.52 -> 5.57 ms).  An extra
+// vector-memory load the compiler does not know about only makes its own
+// vmcnt waits stricter (loads retire in order), so its loads stay safe; the
+// reads of a glds buffer are ordered by glds_wait.
+__device__ __forceinline__ void glds16(const float4* g, float4* dst) {
+  const uint32_t m = (uint32_t)(uintptr_t)(lds_float4_t*)dst;  // LDS byte address
+  uint32_t keep;
+  __asm__ volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep)
+                   : "v"(g), "s"(m)
+                   : "memory");
+}
+__device__ __forceinline__ int glds_issue(const float4* __restrict__ src, int n, float4* dst, int l) {
+  if (l < n) glds16(src + l, dst);
+  if (n <= 64) return 1;
+  if (l + 64 < n) glds16(src + 64 + l, dst + 64);
+  return 2;
+}
+__device__ __forceinline__ void glds_wait(int k) {  // k: glds instructions allowed to stay in flight
+  if (k <= 0)
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if (k == 1)
+    __asm__ volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  else
+    __asm__ volatile("s_waitcnt vmcnt(2)" ::: "memory");
+}
+
+// The packet walk with the next node's payload in flight while a leaf is
+// tested (round 5; VERDICT r04 "two nodes in flight").  After a leaf nothing
+// is pushed, so the next pop is the stack top: its payload (child boxes or
+// leaf records) is copied global -> LDS into the second stage (glds, no
+// registers) as soon as the leaf's own copy is under way, and the next
+// iteration finds it there.  Same pops in the same order, same tests, same
+// decisions as staged_closest; a prefetched node the pruning then skips
+// costs only its copy.
+template <bool COUNT>
+__device__ void staged_closest_pf(const KParams& p, const Ray& r, bool act, Best& b, WaveCtx& w,
+                                  WorkCount& wc) {
+  const float4* __restrict__ node = p.node;
+  const float4* __restrict__ tri = p.tri;
+  uint64_t am = __ballot(act);
+  if (am == 0) return;
+  f3 inv = inv_dir(r.d);
+  uint32_t dm = wave_near_octant(act, r.d, am);
+  int sp = 0;
+  wave_sync();
+  if (w.lane < 2) w.stk2[w.lane] = node[w.lane];
+  if (w.lane == 0) w.stkm[0] = am;
+  sp = 1;
+  float limit = rt_prune_limit(b.dist, r.eps);
+  float4* cur = w.stage;
+  float4* alt = w.stage2;
+  int pf = -1;  // the stack slot whose payload is in flight into alt (RT_PF_AHEAD)
+  if (!RT_PF_AHEAD) alt = w.stage;
+  while (sp > 0) {
+    --sp;
+    wave_sync();
+    float4 lo = w.stk2[2 * sp], hi = w.stk2[2 * sp + 1];
+    uint64_t lm = w.stkm[sp];
+    uint32_t first = uni(__float_as_uint(lo.w)), info = uni(__float_as_uint(hi.w));
+    bool leaf = (info & RT_NODE_LEAF) != 0;
+    uint32_t cnt = leaf ? RT_LEAF_COUNT(info) : RT_NODE_COUNT(info);
+    if (pf == sp) {
+      float4* t = cur;  // the payload is already on its way into alt
+      cur = alt;
+      alt = t;
+    } else {
+      const int nn = leaf ? 3 * (int)chunk<kOctRecs>(cnt, 0) : 2 * (int)cnt;
+      if (nn > kStage2 && cur != w.stage) {  // only the first stage holds kStageOct
+        alt = cur;
+        cur = w.stage;
+      }
+      __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // no LDS read of cur still pending
+      glds_issue(leaf ? tri + 3 * (size_t)first : node + 2 * (size_t)first, nn, cur, w.lane);
+    }
+    pf = -1;
+    // lanes that wanted it when pushed, re-tested against their best so far
+    bool want = ((lm >> w.lane) & 1) != 0;
+    if (want && b.dist != __builtin_inff()) {
+      float tn = box_enter(r, inv, lo, hi);
+      want = !(tn * r.dlen > limit);
+    }
+    if (__ballot(want) == 0) continue;
+    if (COUNT) {
+      wc.nodes++;
+      wc.cl_nodes += (uint32_t)__popcll(__ballot(want));
+    }
+    int behind = 0;  // glds instructions issued after cur's
+    if (RT_PF_AHEAD && leaf && sp > 0) {
+      // the next pop is the stack top: start its payload now
+      const float4 nlo = w.stk2[2 * (sp - 1)], nhi = w.stk2[2 * (sp - 1) + 1];
+      const uint32_t nf = uni(__float_as_uint(nlo.w)), ni = uni(__float_as_uint(nhi.w));
+      const bool nleaf = (ni & RT_NODE_LEAF) != 0;
+      const uint32_t nc = nleaf ? RT_LEAF_COUNT(ni) : RT_NODE_COUNT(ni);
+      const int nn = nleaf ? 3 * (int)chunk<kOctRecs>(nc, 0) : 2 * (int)nc;
+      if (nn <= kStage2) {  // (a payload larger than the second stage is fetched when popped)
+        __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        behind = glds_issue(nleaf ? tri + 3 * (size_t)nf : node + 2 * (size_t)nf, nn, alt, w.lane);
+        pf = sp - 1;
+      }
+    }
+    glds_wait(behind);
+    wave_sync();
+    if (leaf) {
+      for (uint32_t base = 0; base < cnt; base += kOctRecs) {
+        uint32_t m = chunk<kOctRecs>(cnt, base);
+        if (base) {  // a leaf of more than kOctRecs records: the rest synchronously
+          glds_wait(0);
+          pf = -1;
+          stage_load(tri + 3 * (size_t)(first + base), 3 * (int)m, w);
+          stage_test(r, want, m, b, w.stage);
+        } else {
+          stage_test(r, want, m, b, cur);
+        }
+      }
+      limit = rt_prune_limit(b.dist, r.eps);
+      if (COUNT) {
+        wc.tris += cnt;
+        wc.cl_tris += cnt * (uint32_t)__popcll(__ballot(want));
+      }
+    } else {
+      float4* keep = w.stage;
+      w.stage = cur;  // stage_push_children reads the child boxes from w.stage
+      stage_push_children<false>(r, inv, dm, info, want, limit, sp, w, wc);
+      w.stage = keep;
+    }
+  }
+  glds_wait(0);  // no copy may land in a stage after the walk
+  wave_sync();
+}
+
 template <bool COUNT>
 __device__ void staged_closest(const KParams& p, const Ray& r, bool act, Best& b, WaveCtx& w,
                                WorkCount& wc) {
@@ -1083,6 +1237,19 @@ __device__ bool staged_any(const KParams& p, const Ray& r, bool act, WaveCtx& w,
 // shadow queries walk per lane, except directional-light shadows (parallel
 // rays, cpu/light.c:53) under RT_POLICY_DIR_STAGED.
 static constexpr int kPacketMin = 8;
+// The camera packet walk with the next payload in flight (staged_closest_pf,
+// VERDICT r04 item 2a) -- measured and OFF (profiles/r07_prefetch/): with the
+// second stage in LDS the trace kernel holds fewer waves per CU (8,192 B per
+// workgroup: 18 resident instead of 21, tools/micro/lds_occupancy.hip; trace
+// 4.52 -> 5.53 ms), and at full occupancy (a 64-float4 second stage, or an
+// 8-entry per-lane stack) still 4.50 -> 4.66-4.70 ms: with 5 waves per SIMD
+// the other waves already cover the payload latency, and the prefetch adds
+// the stack-top read, its waits and the copies of nodes the pruning skips.
+// The same walk with glds copies and no prefetch runs at the baseline
+// (4.51 ms).
+#ifndef RT_WALK_PREFETCH
+#define RT_WALK_PREFETCH 0
+#endif
 // Camera rays only (round 4): the reflection rays of a wave diverge, and a
 // packet walks the union of their paths through cold nodes; per lane, the
 // longest items of an 8-way split (reflection-heavy tiles, tools/tile_cost.py)
@@ -1120,7 +1287,10 @@ __device__ __forceinline__ void closest_q(const KParams& p, const Ray& r, bool a
                 (POL != RT_POLICY_LANE && __popcll(__ballot(act)) >= kPacketMin &&
                  depth <= kPacketMaxDepth);
   if (staged) {
-    staged_closest<COUNT>(p, r, act, b, w, wc);
+    if (RT_WALK_PREFETCH && w.stage2)
+      staged_closest_pf<COUNT>(p, r, act, b, w, wc);
+    else
+      staged_closest<COUNT>(p, r, act, b, w, wc);
   } else {
     LaneCount lc = {0, 0, 0, 0, 0, 0, 0};
     if (act) oct_closest<COUNT>(p, r, b, s, lc);
@@ -1639,6 +1809,9 @@ __global__ __launch_bounds__(64, RT_TRACE_MIN_WAVES) void trace_kernel(KParams p
   // empty stack (wave_sync() at both ends orders the accesses).
   __shared__ float4 s_stack[ACCEL == RT_ACCEL_FLAT_D ? 1 : kStackArea];
   __shared__ float4 s_stage[ACCEL == RT_ACCEL_FLAT_D ? kStageFlat : kStageOct];
+  // the prefetching packet walk's second stage (8 KB of LDS per one-wave
+  // workgroup in all: 20 workgroups = 5 waves per SIMD fill the CU's 160 KB)
+  __shared__ float4 s_stage2[ACCEL == RT_ACCEL_FLAT_D || !RT_WALK_PREFETCH ? 1 : kStage2];
   const size_t gl = (size_t)blockIdx.x * 64 + (size_t)lane;
   Stack stk;
   stk.idx = (uint32_t*)s_stack;
@@ -1651,6 +1824,7 @@ __global__ __launch_bounds__(64, RT_TRACE_MIN_WAVES) void trace_kernel(KParams p
   w.stk2 = s_stack;
   w.stkm = (uint64_t*)(s_stack + 2 * kStack2);
   w.stage = s_stage;
+  w.stage2 = ACCEL == RT_ACCEL_FLAT_D || !RT_WALK_PREFETCH ? nullptr : s_stage2;
   w.lane = lane;
   // Work item = (tile t, sample s): the four samples of a tile run on four
   // waves, so a tile of long mirror paths (C2: the worst tile cost 7.7x a
@@ -1806,6 +1980,7 @@ __global__ __launch_bounds__(64, ACCEL == RT_ACCEL_FLAT_D ? RT_FLAT_SHADE_MIN_WA
   w.stk2 = s_stack;
   w.stkm = (uint64_t*)(s_stack + 2 * kStack2);
   w.stage = s_stage;
+  w.stage2 = nullptr;
   w.lane = lane;
   const uint32_t home = (uint32_t)blockIdx.x & 7u;
   uint32_t probe = 0;
@@ -2002,6 +2177,55 @@ __global__ __launch_bounds__(256) void probe_shadow_kernel(KParams p, const floa
   out[i] = hit ? 1u : 0u;
 }
 
+// Closest-hit probe (tests, tools): ray i = (org[i], dir[i]) as a
+// reflection ray queries it -- the per-lane octree walk at the secondary
+// rays' culling slack (closest_q at depth > 0, default policy), or brute force
+// over the nprim prim-order records (cpu/hit.c:72-91) -- out[2 i] = the
+// winner's prim (~0: none), out[2 i + 1] = its new_dist bits.  One-wave
+// workgroups: the walk's LDS stack is per wave, its spill area per lane.
+__global__ __launch_bounds__(64) void probe_closest_kernel(KParams p, const float* __restrict__ org,
+                                                           const float* __restrict__ dir, uint32_t n,
+                                                           uint32_t nprim, int brute, uint32_t* __restrict__ out) {
+  __shared__ float4 s_stack[kLaneStackArea];
+  const int lane = threadIdx.x & 63;
+  const uint32_t i = blockIdx.x * 64u + (uint32_t)lane;
+  Stack stk;
+  stk.idx = (uint32_t*)s_stack;
+  stk.tt = (float*)s_stack + kLdsStack * 64;
+  stk.spill = p.spill + (size_t)blockIdx.x * 64 + (size_t)lane;
+  stk.stride = gridDim.x * 64u;
+  stk.lane = lane;
+  stk.sp = 0;
+  const bool act = i < n;
+  f3 o{0.0f, 0.0f, 0.0f}, d{0.0f, 0.0f, 1.0f};
+  if (act) {
+    o = f3{org[3 * (size_t)i], org[3 * (size_t)i + 1], org[3 * (size_t)i + 2]};
+    d = f3{dir[3 * (size_t)i], dir[3 * (size_t)i + 1], dir[3 * (size_t)i + 2]};
+  }
+  const Ray r = make_ray(p, o, d, p.eps_rel);
+  Best b;
+  b.dist = __builtin_inff();
+  b.t_cut = __builtin_inff();
+  b.prim = 0xffffffffu;
+  b.obj = 0;
+  b.u = b.v = 0.0f;
+  b.t = 0.0f;
+  if (brute) {
+    if (act)
+      for (uint32_t k = 0; k < nprim; k++) {
+        const float4* t = p.tri_prim + 3 * (size_t)k;
+        consider(r, t[0], t[1], t[2], b);
+      }
+  } else {
+    LaneCount lc = {0, 0, 0, 0, 0, 0, 0};
+    if (act) oct_closest<false>(p, r, b, stk, lc);
+  }
+  if (act) {
+    out[2 * (size_t)i] = b.dist == __builtin_inff() ? 0xffffffffu : b.prim;
+    out[2 * (size_t)i + 1] = __float_as_uint(b.dist);
+  }
+}
+
 // A pixel's four samples (trace_kernel items 4t..4t+3): each sample's path
 // terms summed deepest-first, acc = color_add(reflected, term)
 // (cpu/raytracer.c:29-30), then acc = color_add(acc, color_mul(s, 0.25)) over
@@ -2142,6 +2366,7 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES) void compat_kernel(KParams p) {
   w.stk2 = s_stack;
   w.stkm = (uint64_t*)(s_stack + 2 * kStack2);
   w.stage = s_stage;
+  w.stage2 = nullptr;
   w.lane = lane;
   uint32_t* img = (uint32_t*)p.out;
   for (;;) {
@@ -2338,6 +2563,15 @@ extern "C" hipError_t rt_launch_probe_shadow(const KParams* p, const float* org,
   if (n == 0) return hipGetLastError();
   hipLaunchKernelGGL(rt::probe_shadow_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, *p, org, n, li, nprim,
                      brute, out);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t rt_launch_probe_closest(const KParams* p, const float* org, const float* dir, uint32_t n,
+                                              uint32_t nprim, int brute, uint32_t* out, int grid, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  const uint32_t g = (n + 63) / 64;
+  if (!brute && g > (uint32_t)grid) return hipErrorInvalidValue;  // the spill area holds `grid` waves
+  hipLaunchKernelGGL(rt::probe_closest_kernel, dim3(g), dim3(64), 0, stream, *p, org, dir, n, nprim, brute, out);
   return hipGetLastError();
 }
 

@@ -110,7 +110,8 @@ class AccelInfo(C.Structure):
                 ("shadow_mu_max", C.c_double), ("lightbuf_entries", C.c_ulonglong),
                 ("lightbuf_global", C.c_ulonglong), ("lightbuf_seconds", C.c_double),
                 ("lightbuf_never", C.c_ulonglong), ("lightbuf_band", C.c_ulonglong),
-                ("lightbuf_failed", C.c_ulonglong), ("lightbuf_fail_reason", C.c_char * 96)]
+                ("lightbuf_failed", C.c_ulonglong), ("lightbuf_fail_reason", C.c_char * 96),
+                ("trace_grid", C.c_int), ("shade_grid", C.c_int)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_}
@@ -167,6 +168,8 @@ _PROTOS = [
     ("rt_hip_set_lightbuf_entry_cap", C.c_int, [C.c_void_p, C.c_ulonglong]),
     ("rt_lightbuf_survey", C.c_int, [C.c_void_p, C.c_uint, C.c_int, C.c_uint, C.c_void_p]),
     ("rt_hip_probe_shadows", C.c_int, [C.c_void_p, C.c_uint, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]),
+    ("rt_hip_probe_closest", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p,
+                                       C.c_void_p]),
     ("rt_hip_tile_cycles", C.c_int, [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_size_t]),
     ("rt_hip_tile_phase_cycles", C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_ulonglong),
                                            C.c_size_t]),
@@ -506,6 +509,20 @@ class Context:
                                           1 if brute else 0, out.ctypes.data_as(C.c_void_p)),
                "probe_shadows")
         return out.astype(bool)
+
+    def probe_closest(self, origins, dirs, brute=False):
+        """Closest hits of (n, 3) rays queried as reflection rays (the per-lane
+        octree walk) or by brute force (rt_hip_probe_closest): (prim, dist)
+        arrays, prim = 0xffffffff for no hit."""
+        o = np.ascontiguousarray(origins, dtype=np.float32).reshape(-1, 3)
+        d = np.ascontiguousarray(dirs, dtype=np.float32).reshape(-1, 3)
+        assert len(o) == len(d)
+        prim = np.zeros(len(o), np.uint32)
+        dist = np.zeros(len(o), np.float32)
+        _check(lib().rt_hip_probe_closest(self.h, o.ctypes.data_as(C.c_void_p), d.ctypes.data_as(C.c_void_p),
+                                          len(o), 1 if brute else 0, prim.ctypes.data_as(C.c_void_p),
+                                          dist.ctypes.data_as(C.c_void_p)), "probe_closest")
+        return prim, dist
 
     def set_exact_shadows(self, on=True):
         """Shadow rays exact by proof (rt_hip_set_exact_shadows; default on):
