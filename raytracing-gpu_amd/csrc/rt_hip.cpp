@@ -59,7 +59,8 @@ static constexpr size_t kItemCounterBytes = 8 * 128;
 static_assert(RT_NSTATS <= RT_STAT_STRIDE, "stat copies overlap");
 static constexpr size_t kStatBytes = RT_STAT_SETS * RT_STAT_STRIDE * sizeof(unsigned long long);
 static constexpr size_t kHitCounterBytes = 2 * RT_HIT_REGIONS * 32 * sizeof(uint32_t);
-static constexpr size_t kFrameCounterBytes = kItemCounterBytes + kStatBytes + kHitCounterBytes;
+static constexpr size_t kSecCounterBytes = 2 * 32 * sizeof(uint32_t);  // secondary queue: append, chunk
+static constexpr size_t kFrameCounterBytes = kItemCounterBytes + kStatBytes + kHitCounterBytes + kSecCounterBytes;
 
 struct rt_hip_ctx {
   int device = 0;
@@ -93,6 +94,22 @@ struct rt_hip_ctx {
   size_t hit_need = 0;              // per region: what the last overflowing frame needed
   uint32_t* d_last = nullptr;       // per (item, lane): a path's deepest record
   size_t last_cap = 0;              // items
+  // secondary-ray queue (KParams::sec_q): one entry per camera ray at most
+// Measured and OFF (profiles/r07_secondary_queue/): with the reflection
+// paths queued and continued 64 to a wave by bounce_kernel after the camera
+// waves, C5 trace + bounce took 5.21 ms against 4.50 (N = 8 slowest rank 1.48
+// against 1.22 ms): a queue chunk gathers ~76 items' rays from all over the
+// frame (0.84 reflection rays per item), so its per-lane walks are incoherent
+// and the longest of them -- no longer hidden under other waves' camera
+// work -- sets the kernel's length.  RT_SEC_QUEUE=1 at context creation turns
+// it on (A/B).
+#ifndef RT_SEC_QUEUE_DEFAULT
+#define RT_SEC_QUEUE_DEFAULT 0
+#endif
+  int sec_queue = RT_SEC_QUEUE_DEFAULT;  // RT_SEC_QUEUE=0 at context creation: off (A/B)
+  float4* d_sec_q = nullptr;
+  uint32_t* d_sec_slot = nullptr;
+  size_t sec_cap = 0;
   int grid_of[2][5][2] = {};        // persistent grids [trace][policy][count_work] (policy 4: shade only)
   int cus = 0;                      // compute units of the device
   std::vector<uint32_t> light_type; // per light (rt_hip_verify_shadows)
@@ -294,6 +311,8 @@ extern "C" void rt_hip_destroy(rt_hip_ctx* c) {
   (void)hipFree(c->d_hit_prev);
   (void)hipFree(c->d_hit_term);
   (void)hipFree(c->d_last);
+  (void)hipFree(c->d_sec_q);
+  (void)hipFree(c->d_sec_slot);
   (void)hipFree(c->d_prim_mu);
   (void)hipFree(c->d_node_mu);
   (void)hipFree(c->d_oob);
@@ -598,6 +617,7 @@ extern "C" int rt_hip_create(int device, const rt_scene* scene, int accel, rt_hi
 
   rt_hip_ctx* c = new rt_hip_ctx();
   if (const char* e = std::getenv("RT_CAND_REFINE")) c->cand_refine = std::atoi(e) != 0;  // A/B knob
+  if (const char* e = std::getenv("RT_SEC_QUEUE")) c->sec_queue = std::atoi(e) != 0;      // A/B knob
   c->device = device;
   c->accel = dev_build ? (fs.ntri ? RT_ACCEL_OCTREE : RT_ACCEL_FLAT) : accel;
   c->nrec = (uint32_t)fs.nrec;
@@ -1625,6 +1645,16 @@ static int hit_buffers(rt_hip_ctx* c, size_t ntiles) {
     HIP_TRY(hipMalloc((void**)&c->d_last, items * 64 * sizeof(uint32_t)));
     c->last_cap = items;
   }
+  if (c->sec_queue && items * 64 > c->sec_cap) {  // one queue entry per camera ray at most
+    (void)hipFree(c->d_sec_q);
+    (void)hipFree(c->d_sec_slot);
+    c->d_sec_q = nullptr;
+    c->d_sec_slot = nullptr;
+    c->sec_cap = 0;
+    HIP_TRY(hipMalloc((void**)&c->d_sec_q, items * 64 * 2 * sizeof(float4)));
+    HIP_TRY(hipMalloc((void**)&c->d_sec_slot, items * 64 * sizeof(uint32_t)));
+    c->sec_cap = items * 64;
+  }
   size_t want = (2 * items * 64 + RT_HIT_REGIONS - 1) / RT_HIT_REGIONS + 1024;
   if (c->hit_need > want) want = c->hit_need;
   if (want > (1ull << 29) - 1) want = (1ull << 29) - 1;  // slot field of a record index
@@ -1724,6 +1754,13 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
   p.shade_counter = c->d_hit_count + RT_HIT_REGIONS * 32;
   p.hit_cap = (uint32_t)c->hit_cap;
   p.last = c->d_last;
+  if (c->sec_queue && c->d_sec_q) {
+    p.sec_q = c->d_sec_q;
+    p.sec_slot = c->d_sec_slot;
+    p.sec_cap = (uint32_t)c->sec_cap;
+    p.sec_count = (uint32_t*)((char*)c->d_counter + kItemCounterBytes + kStatBytes + kHitCounterBytes);
+    p.sec_head = p.sec_count + 32;
+  }
   if (c->count_work) {  // per-item clocks of the instrumented pass (rt_hip_tile_cycles)
     const size_t items = 4 * (size_t)p.ntiles_local;
     if (items > c->tile_cycles_cap) {

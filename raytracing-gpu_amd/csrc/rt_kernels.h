@@ -156,6 +156,15 @@ struct KParams {
   const float4* tri_prim;       // prim-order triangle records
   const float* cand_skip;       // per cand entry: lower bound of new_dist - |pos - o| (depth skip)
   const uint32_t* tile_order;   // trace_kernel's work order: position -> rank-local tile (NULL: identity)
+  // secondary-ray queue (NULL: camera waves follow their paths to the end):
+  // trace_kernel appends each camera path that goes on as {o.xyz, coef},
+  // {d.xyz, deepest record} plus its (item, lane) slot of last[];
+  // bounce_kernel continues them from depth 1
+  float4* sec_q;
+  uint32_t* sec_slot;
+  uint32_t* sec_count;          // appended entries (zeroed before the launch)
+  uint32_t* sec_head;           // bounce_kernel's chunk counter (zeroed before the launch)
+  uint32_t sec_cap;
 };
 
 // The three launches of one render (policy = RT_POLICY_*, octree only):

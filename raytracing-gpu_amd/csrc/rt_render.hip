@@ -1729,11 +1729,11 @@ __device__ __forceinline__ bool camera_sample(const KParams& p, uint32_t t, int 
 template <int ACCEL, bool COUNT, int POL>
 __device__ __forceinline__ uint32_t trace_path(const KParams& p, bool valid, f3 o, f3 d,
                                                uint32_t x, Stack& s, WaveCtx& w, WorkCount& wc,
-                                               uint32_t tile) {
-  int depth = 0;  // wave-uniform: queries so far on this path
+                                               uint32_t tile, int depth = 0, float coef = 1.0f,
+                                               uint32_t prev = RT_NO_REC, uint32_t path_slot = 0) {
+  // depth: wave-uniform, queries so far on this path (bounce_kernel resumes
+  // queued paths at depth 1 with their coefficient and deepest record)
   bool alive = valid;
-  float coef = 1.0f;
-  uint32_t prev = RT_NO_REC;
   for (;;) {
     alive = alive && !((double)coef < 0.01);  // checked before the query
     uint64_t am = __ballot(alive);
@@ -1796,6 +1796,29 @@ __device__ __forceinline__ uint32_t trace_path(const KParams& p, bool valid, f3 
     wc.overflow += (uint32_t)__popcll(__ballot(deep));
     alive = hit && depth + 1 < RT_MAX_BOUNCES;
     ++depth;
+    if (depth == 1 && p.sec_q) {
+      // camera paths end here: the lanes whose path goes on (checked as the
+      // loop would, coef >= 0.01) append their reflection ray to the
+      // secondary queue -- one atomic per wave -- and bounce_kernel continues
+      // them 64 to a wave, so a tile of long reflection paths no longer holds
+      // its camera wave (the N = 8 tail)
+      alive = alive && !((double)coef < 0.01);
+      const uint64_t qm = __ballot(alive);
+      if (qm) {
+        uint32_t qb = 0;
+        if (w.lane == 0) qb = atomicAdd(p.sec_count, (uint32_t)__popcll(qm));
+        qb = uni(qb);
+        if (alive) {
+          const uint32_t e = qb + (uint32_t)__popcll(qm & ((1ull << w.lane) - 1ull));
+          if (e < p.sec_cap) {  // (the queue holds every camera ray's: never full)
+            p.sec_q[2 * (size_t)e] = make_float4(o.x, o.y, o.z, coef);
+            p.sec_q[2 * (size_t)e + 1] = make_float4(d.x, d.y, d.z, __uint_as_float(prev));
+            p.sec_slot[e] = path_slot;
+          }
+        }
+      }
+      break;
+    }
   }
   return prev;
 }
@@ -1872,7 +1895,8 @@ __global__ __launch_bounds__(64, RT_TRACE_MIN_WAVES) void trace_kernel(KParams p
     const bool valid = camera_sample(p, t, smp, lane, point, dir);
     if (smp == 0) wc.pixels += (uint32_t)__popcll(__ballot(valid));
     p.last[(size_t)u * 64 + lane] =
-        trace_path<ACCEL, COUNT, POL>(p, valid, point, dir, x, stk, w, wc, t);
+        trace_path<ACCEL, COUNT, POL>(p, valid, point, dir, x, stk, w, wc, t, 0, 1.0f, RT_NO_REC,
+                                      u * 64u + (uint32_t)lane);
     if (COUNT && p.tile_cycles && lane == 0) {
       // [0] the item's clocks, [1..3] its phase clocks (camera walk, camera
       // candidates, secondary walks), planes of 4 * ntiles_local items
@@ -1884,6 +1908,59 @@ __global__ __launch_bounds__(64, RT_TRACE_MIN_WAVES) void trace_kernel(KParams p
       p.tile_cycles[u + 4 * items] = wc.sec_lane_nodes;
       p.tile_cycles[u + 5 * items] = wc.sec_lane_tris;
     }
+  }
+  flush_counts(p, wc, lane);
+}
+
+// bounce_kernel: the reflection paths trace_kernel queued (p.sec_q), 64 per
+// wave in queue order (neighbouring camera waves' rays, so still coherent),
+// each continued from depth 1 exactly as trace_path's loop would -- same
+// queries, same records, same links -- to its end; the path's deepest record
+// replaces the camera record in last[] when the path made further hits.
+// Persistent one-wave workgroups pull 64-entry chunks from one counter.
+template <int ACCEL, bool COUNT, int POL>
+__global__ __launch_bounds__(64, RT_TRACE_MIN_WAVES) void bounce_kernel(KParams p) {
+  const int lane = threadIdx.x & 63;
+  WorkCount wc = {};
+  __shared__ float4 s_stack[ACCEL == RT_ACCEL_FLAT_D ? 1 : kStackArea];
+  __shared__ float4 s_stage[ACCEL == RT_ACCEL_FLAT_D ? kStageFlat : kStageOct];
+  const size_t gl = (size_t)blockIdx.x * 64 + (size_t)lane;
+  Stack stk;
+  stk.idx = (uint32_t*)s_stack;
+  stk.tt = (float*)s_stack + kLdsStack * 64;
+  stk.spill = p.spill + gl;
+  stk.stride = gridDim.x * 64u;
+  stk.lane = lane;
+  stk.sp = 0;
+  WaveCtx w;
+  w.stk2 = s_stack;
+  w.stkm = (uint64_t*)(s_stack + 2 * kStack2);
+  w.stage = s_stage;
+  w.stage2 = nullptr;
+  w.lane = lane;
+  const uint32_t n = min(*p.sec_count, p.sec_cap);
+  const uint32_t x = (uint32_t)blockIdx.x & 7u;  // hit-record region
+  for (uint32_t q = blockIdx.x;; ) {
+    if (q * 64u >= n) break;
+    const uint32_t e = q * 64u + (uint32_t)lane;
+    const bool valid = e < n;
+    f3 o{0.0f, 0.0f, 0.0f}, d{0.0f, 0.0f, 1.0f};
+    float coef = 0.0f;
+    uint32_t prev = RT_NO_REC, slot = 0;
+    if (valid) {
+      const float4 a = p.sec_q[2 * (size_t)e], b = p.sec_q[2 * (size_t)e + 1];
+      o = f3{a.x, a.y, a.z};
+      coef = a.w;
+      d = f3{b.x, b.y, b.z};
+      prev = __float_as_uint(b.w);
+      slot = p.sec_slot[e];
+    }
+    const uint32_t deepest = trace_path<ACCEL, COUNT, POL>(p, valid, o, d, x, stk, w, wc, 0u, 1, coef, prev, slot);
+    if (valid && deepest != prev) p.last[slot] = deepest;
+    // the first chunk of every wave without an atomic, the rest through the counter
+    uint32_t nq = 0;
+    if (lane == 0) nq = atomicAdd(p.sec_head, 1u);
+    q = uni(nq) + gridDim.x;
   }
   flush_counts(p, wc, lane);
 }
@@ -2490,6 +2567,21 @@ __global__ __launch_bounds__(256) void assemble_kernel(const float* __restrict__
 // differ in the walks they use: trace has no shadow queries (policy 3 =
 // default there), shade has no closest-hit queries (policy 1 = default).
 template <bool TRACE>
+static const void* kernel_of(int accel, int count_work, int policy);
+
+// bounce_kernel of the same instantiation as trace_kernel
+static const void* bounce_of(int accel, int count_work, int policy) {
+  using namespace rt;
+  if (accel == RT_ACCEL_FLAT_D)
+    return count_work ? (const void*)bounce_kernel<RT_ACCEL_FLAT_D, true, 0>
+                      : (const void*)bounce_kernel<RT_ACCEL_FLAT_D, false, 0>;
+  if (policy == RT_POLICY_LANE) return (const void*)bounce_kernel<RT_ACCEL_OCTREE_D, false, RT_POLICY_LANE>;
+  if (policy == RT_POLICY_STAGED) return (const void*)bounce_kernel<RT_ACCEL_OCTREE_D, false, RT_POLICY_STAGED>;
+  return count_work ? (const void*)bounce_kernel<RT_ACCEL_OCTREE_D, true, RT_POLICY_DEFAULT>
+                    : (const void*)bounce_kernel<RT_ACCEL_OCTREE_D, false, RT_POLICY_DEFAULT>;
+}
+
+template <bool TRACE>
 static const void* kernel_of(int accel, int count_work, int policy) {
   using namespace rt;
   if (accel == RT_ACCEL_FLAT_D) {
@@ -2539,7 +2631,11 @@ static hipError_t launch_kernel(const void* k, int grid, const KParams* p, hipSt
 
 extern "C" hipError_t rt_launch_trace(const KParams* p, int accel, int count_work, int policy,
                                       int grid, hipStream_t stream) {
-  return launch_kernel(kernel_of<true>(accel, count_work, policy), grid, p, stream);
+  hipError_t e = launch_kernel(kernel_of<true>(accel, count_work, policy), grid, p, stream);
+  if (e != hipSuccess || !p->sec_q) return e;
+  // the queued reflection paths (the queue's length is on the device: every
+  // wave exits at once on an empty queue)
+  return launch_kernel(bounce_of(accel, count_work, policy), grid, p, stream);
 }
 
 extern "C" hipError_t rt_launch_shade(const KParams* p, int accel, int count_work, int policy,
