@@ -48,7 +48,7 @@
 #define RT_TRACE_MIN_WAVES 5
 #endif
 #ifndef RT_SHADE_MIN_WAVES
-#define RT_SHADE_MIN_WAVES 8
+#define RT_SHADE_MIN_WAVES 7  // 72 VGPRs: the light-buffer scan's record one ahead (rt_render.hip RT_LB_AHEAD)
 #endif
 // the staged test policies' shade kernels (packet any-hit walks, test / A/B
 // only) need more registers than 8 waves allow: their own, reachable, target

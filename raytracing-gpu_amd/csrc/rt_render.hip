@@ -1381,13 +1381,47 @@ __device__ __forceinline__ LbRange lbuf_range(const RtLightBuf& L, const Ray& r)
 }
 
 // Each range's entries -- the record inline, its key in the prim slot: one
-// contiguous load per test, no prim -> record indirection.  (Loading the next
-// entry's record ahead measured slower: its registers spill, shade 1.86 ->
-// 2.72 ms on C5, profiles/r03t_lbuf_inline/.)  Then the global list.
+// contiguous load per test, no prim -> record indirection, the next record's
+// load in flight (RT_LB_AHEAD).  Then the global list.
+// The next entry's record in flight while an entry is tested (round 5):
+// +12 VGPRs, so the shade kernel runs at 7 waves per SIMD (RT_SHADE_MIN_WAVES)
+// instead of 8 -- C5 shade 1.96 -> 1.85 ms (profiles/r07_shade/; at 8 waves
+// it spills: 1.92; at 6: 1.93).  Round 3 measured the lookahead at 8 waves
+// only (spills, 2.72 ms).
+#ifndef RT_LB_AHEAD
+#define RT_LB_AHEAD 1
+#endif
 template <bool COUNT>
 __device__ bool lbuf_scan(const KParams& p, const RtLightBuf& L, const Ray& r, const LbRange& g, LaneCount& lc) {
   for (int h = 0; h < 2; h++) {
     const float q = h == 0 ? g.lim : __builtin_inff();
+#if RT_LB_AHEAD
+    // the next entry's record in flight while this one is tested
+    uint32_t k = g.rs[h];
+    const uint32_t e = g.re[h];
+    float4 n0, n1, n2;
+    if (k < e) {
+      const float4* t = L.rec + 3 * (size_t)k;
+      n0 = t[0];
+      n1 = t[1];
+      n2 = t[2];
+    }
+    for (; k < e; k++) {
+      const float4 a0 = n0, a1 = n1, a2 = n2;
+      if (k + 1 < e) {
+        const float4* t = L.rec + 3 * (size_t)(k + 1);
+        n0 = t[0];
+        n1 = t[1];
+        n2 = t[2];
+      }
+      if (a2.y > q) break;
+      if (COUNT) {
+        lc.tris += lanes_distinct(k);
+        lc.ltris++;
+      }
+      if (any_hit_rec(r, a0, a1, a2, lc.risk)) return true;
+    }
+#else
     for (uint32_t k = g.rs[h]; k < g.re[h]; k++) {
       const float4* t = L.rec + 3 * (size_t)k;
       const float4 a0 = t[0], a1 = t[1], a2 = t[2];
@@ -1398,6 +1432,7 @@ __device__ bool lbuf_scan(const KParams& p, const RtLightBuf& L, const Ray& r, c
       }
       if (any_hit_rec(r, a0, a1, a2, lc.risk)) return true;
     }
+#endif
   }
   for (uint32_t k = 0; k < L.nglobal; k++) {
     const float4* t = p.tri_prim + 3 * (size_t)L.global[k];
@@ -1999,6 +2034,9 @@ __device__ __forceinline__ col shade_record(const KParams& p, bool valid, size_t
         // 2.16 ms on C5, profiles/r04b_shade_pre/)
         // (df by address, the block-0 condition a flag: a pointer chosen per
         // block kept df on the stack, a scratch store per query)
+        // (round 5, with the entries one ahead: the next light's cell ranges
+        // loaded while this light's entries are scanned, shade 1.85 -> 1.98
+        // ms at 7 waves per SIMD, profiles/r07_shade/)
         const bool sh = shadow_q<ACCEL, COUNT, POL>(p, P, shadow_dir(type, lv, P), type, li, valid, s, w, wc,
                                                     &df, nullptr, l0 == 0);
         if (COUNT) {
