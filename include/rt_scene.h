@@ -35,8 +35,10 @@ enum {
   RT_EZERONORMAL = -9, /* a closest hit had an exactly zero interpolated normal, or
                        * a shadow ray hit an object that can have one: cpu/hit.c:79,99
                        * skips such an object, which is not reproduced     */
-  RT_EHITBUF = -10,  /* the frame made more hits than the hit-record buffer held:
-                      * the image is incomplete; the buffer has been grown to the
+  RT_EHITBUF = -10,  /* the frame made more hits than the hit-record buffer held,
+                      * or more camera candidate-list entries than the
+                      * asynchronous list build had sized its buffers for: the
+                      * image is incomplete; the buffer has been grown to the
                       * frame's need, render the frame again              */
   RT_EINEXACT = -11  /* rendered with a tuning knob that gives up the cpu/rt parity
                       * guarantee (rt_hip_set_exact_camera(0), a camera bound scale

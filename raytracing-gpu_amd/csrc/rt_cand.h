@@ -64,7 +64,8 @@ struct CandParams {
   uint32_t* vals;         // entries: prim
   uint32_t* global;       // nprim: prims whose footprint is unbounded
   uint32_t* ctr;          // [1] global prims, [2] big footprints, [3] list length,
-                          // [5] 1 = more than item_cap items (big_kernel emits instead)
+                          // [5] 1 = more than item_cap items (big_kernel emits instead),
+                          // [6] the entry total, [7] 1 = an entry past key_cap
   uint32_t* big;          // nprim: list entries with big footprints (rt_cand.hip kSmallRows)
   float* skip;            // nprim: depth-skip bound of each listed prim
   uint32_t* big_lane;     // big_cap x 64: per big footprint, each lane's row-count subtotal
@@ -78,6 +79,11 @@ struct CandParams {
   // count: it sorts after every tile and bounds_kernel leaves it out)
   uint32_t refine;
   uint32_t drop_key;
+  // entries the key / value buffers hold (0: sized to the frame's exact total
+  // by a host read-back, no check).  Asynchronous builds size them from the
+  // previous frame's total: an entry past key_cap is not written and sets
+  // ctr[7] (rt_hip_stats then reports the frame and grows the buffers)
+  uint32_t key_cap;
 };
 
 // Host mirror for surveys (same classify/raster code): safe / footprint /
@@ -116,7 +122,7 @@ extern "C" hipError_t rt_cand_big(const CandParams* p, uint32_t nbig, hipStream_
 // (big footprint, chunk of its entries) item (used when ctr[5] == 0)
 extern "C" uint32_t rt_cand_big_waves(void);
 extern "C" hipError_t rt_cand_items(const CandParams* p, hipStream_t s);
-extern "C" hipError_t rt_cand_big_items(const CandParams* p, uint32_t nitems, hipStream_t s);
+extern "C" hipError_t rt_cand_big_items(const CandParams* p, uint32_t nitems, int check, hipStream_t s);
 extern "C" hipError_t rt_cand_scan(const uint32_t* in, uint32_t* out, uint32_t n, void* temp,
                                    size_t* temp_bytes, hipStream_t s);
 // exclusive scan of in[0 .. n], n = min(*n_dev, nmax) read on the device
@@ -129,6 +135,9 @@ extern "C" hipError_t rt_cand_sort(uint32_t* keys_in, uint32_t* keys_out, uint32
                                    uint32_t* vals_out, uint32_t n, int bits, void* temp,
                                    size_t* temp_bytes, hipStream_t s);
 // out[i] = skip[cand[i]]: the sorted lists' per-entry depth-skip bounds
+// keys[i] = key for i in [*total_dev, n) (an asynchronous build's unused tail)
+extern "C" hipError_t rt_cand_fill_tail(uint32_t* keys, const uint32_t* total_dev, uint32_t n, uint32_t key,
+                                        hipStream_t s);
 extern "C" hipError_t rt_cand_entry_skip(const uint32_t* cand, const float* skip, float* out,
                                          uint32_t n, const uint32_t* n_dev, hipStream_t s);
 extern "C" hipError_t rt_cand_bounds(const uint32_t* keys, uint32_t n, uint32_t* start,

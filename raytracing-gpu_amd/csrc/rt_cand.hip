@@ -1091,6 +1091,10 @@ __device__ __forceinline__ uint32_t emit_interval(const CandParams& p, int ty, i
     const int a = x0 > bx * tb ? x0 : bx * tb, b = x1 < bx * tb + tb - 1 ? x1 : bx * tb + tb - 1;
     const uint32_t base = blk * (uint32_t)(tb * tb) + row;
     for (int tx = a; tx <= b; tx++, k++) {
+      if (p.key_cap && o + k >= p.key_cap) {  // the buffers hold the previous frame's total
+        p.ctr[7] = 1u;
+        continue;
+      }
       const bool keep = !refine || tile_keep(p, (const float*)(p.tri + 3 * (size_t)prim), tx, ty);
       p.keys[o + k] = keep ? base + (uint32_t)(tx - bx * tb) : p.drop_key;
       p.vals[o + k] = prim;
@@ -1147,6 +1151,7 @@ __global__ __launch_bounds__(RT_LIST_BLOCK) void emit_kernel(CandParams p) {
 // Pass 2b: one wave per big footprint, its tile rows over the lanes; a wave
 // prefix sum of the lanes' row counts places each lane's entries.
 __global__ __launch_bounds__(64) void big_kernel(CandParams p) {
+  if (!p.ctr[5]) return;  // big_item_kernel emits (an asynchronous build launches both)
   const int lane = threadIdx.x;
   const uint32_t nbig = p.ctr[2];
   for (uint32_t b = blockIdx.x; b < nbig; b += gridDim.x) {
@@ -1189,16 +1194,36 @@ __device__ __forceinline__ int kth_rank_col(const CandParams& p, int x0, int x1,
 // their intervals and counts (row_ivs), a wave scan places them, and each
 // entry of the chunk finds its row by binary search over the 64 prefixes in
 // LDS.  Same (tile, prim) set as big_kernel; the sort orders it.
+// One workgroup per item.  CHECK (an asynchronous build: its grid is the
+// same frame's read-back build's) reads the item count and the over-cap flag
+// on the device: past item_cap (ctr[5]) big_kernel emits instead, and a count
+// the grid does not cover -- never expected -- sets ctr[7], so the frame is
+// reported rather than incomplete.  (The checks cost 16-18 VGPRs -- 4 waves
+// per SIMD instead of 5 -- so the read-back build's launch, whose grid is
+// the exact count, goes without them; a grid-stride loop over the items held
+// 118 VGPRs.)
+template <bool CHECK>
 __global__ __launch_bounds__(64) void big_item_kernel(CandParams p) {
   __shared__ uint32_t pre[65];
   __shared__ int rx[64][6], rf[64][3];
   __shared__ uint32_t rc[64][2];
   __shared__ int rty[64];
   const int lane = threadIdx.x;
+  if (CHECK) {
+    if (p.ctr[5]) return;
+    const uint32_t n_items = p.wave_base[kBigWaves];
+    if (blockIdx.x == 0 && lane == 0 && n_items > gridDim.x) p.ctr[7] = 1u;
+    if (blockIdx.x >= n_items) return;
+  }
   const uint2 it = p.items[blockIdx.x];
   const uint32_t j = p.big[it.x], prim = p.list[j];
   const uint32_t base = p.off[j], total = p.off[j + 1] - base;
-  const uint32_t c0 = it.y * kChunk, c1 = c0 + kChunk < total ? c0 + kChunk : total;
+  const uint32_t c0 = it.y * kChunk;
+  uint32_t c1 = c0 + kChunk < total ? c0 + kChunk : total;
+  if (CHECK && base + c1 > p.key_cap) {  // entries past the buffers: not written, the frame reported
+    if (lane == 0) p.ctr[7] = 1u;
+    c1 = p.key_cap > base ? p.key_cap - base : 0u;
+  }
   const Footprint fp = p.fp[j];
   int r0, r1;
   if (!raster_rows(p, fp, r0, r1)) return;  // no entries, no items
@@ -1258,9 +1283,17 @@ __global__ __launch_bounds__(64) void big_item_kernel(CandParams p) {
 // the frame's parts in LDS and re-read per entry, runs at 80 VGPRs and 6
 // waves per SIMD; inside big_item_kernel the same test held 137-175 VGPRs (2-3
 // waves) and the frame took 0.1 ms longer on C5 (profiles/r06e/ab.log).
+__device__ __forceinline__ void refine_item(const CandParams& p, uint32_t item);
+
+template <bool CHECK>
 __global__ __launch_bounds__(64) void refine_kernel(CandParams p) {
+  if (CHECK && (p.ctr[5] || blockIdx.x >= p.wave_base[kBigWaves])) return;
+  refine_item(p, blockIdx.x);
+}
+
+__device__ __forceinline__ void refine_item(const CandParams& p, uint32_t item) {
   const int lane = threadIdx.x;
-  const uint2 it = p.items[blockIdx.x];
+  const uint2 it = p.items[item];
   const uint32_t j = p.big[it.x], prim = p.list[j];
   const Footprint fp = p.fp[j];
   int r0, r1;
@@ -1280,6 +1313,7 @@ __global__ __launch_bounds__(64) void refine_kernel(CandParams p) {
     // re-read the LDS inputs per entry instead of holding them live across
     // the loop (a compiler memory barrier; 161 -> 80 VGPRs)
     __asm__ volatile("" ::: "memory");
+    if (p.key_cap && base + e >= p.key_cap) break;  // not written (ctr[7] is set)
     int tx, ty;
     rt_tile_xy(p.keys[base + e], (uint32_t)p.rank, (uint32_t)p.nranks, (uint32_t)p.blocks_x, (uint32_t)p.tb, &tx, &ty);
     if (!tile_keep(tf, tt, tx, ty)) p.keys[base + e] = p.drop_key;
@@ -1852,10 +1886,31 @@ extern "C" hipError_t rt_cand_items(const CandParams* p, hipStream_t s) {
   return hipGetLastError();
 }
 
-extern "C" hipError_t rt_cand_big_items(const CandParams* p, uint32_t nitems, hipStream_t s) {
+extern "C" hipError_t rt_cand_big_items(const CandParams* p, uint32_t nitems, int check, hipStream_t s) {
+  // nitems: the items read back (check = 0), or the same frame's read-back
+  // build's (check = 1: an asynchronous build; the kernels compare on the device)
   if (nitems == 0) return hipSuccess;
-  hipLaunchKernelGGL(rtc::big_item_kernel, dim3(nitems), dim3(64), 0, s, *p);
-  if (p->refine) hipLaunchKernelGGL(rtc::refine_kernel, dim3(nitems), dim3(64), 0, s, *p);
+  if (check) {
+    hipLaunchKernelGGL(rtc::big_item_kernel<true>, dim3(nitems), dim3(64), 0, s, *p);
+    if (p->refine) hipLaunchKernelGGL(rtc::refine_kernel<true>, dim3(nitems), dim3(64), 0, s, *p);
+  } else {
+    hipLaunchKernelGGL(rtc::big_item_kernel<false>, dim3(nitems), dim3(64), 0, s, *p);
+    if (p->refine) hipLaunchKernelGGL(rtc::refine_kernel<false>, dim3(nitems), dim3(64), 0, s, *p);
+  }
+  return hipGetLastError();
+}
+
+// entries [ctr[6], n) of keys (the buffers' unused tail in an asynchronous
+// build, sized from the previous frame) get `key`: they sort after every tile
+__global__ __launch_bounds__(256) void fill_tail_kernel(uint32_t* keys, const uint32_t* total, uint32_t n,
+                                                        uint32_t key) {
+  for (uint32_t i = *total + blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) keys[i] = key;
+}
+
+extern "C" hipError_t rt_cand_fill_tail(uint32_t* keys, const uint32_t* total_dev, uint32_t n, uint32_t key,
+                                        hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(fill_tail_kernel, dim3(1024), dim3(256), 0, s, keys, total_dev, n, key);
   return hipGetLastError();
 }
 

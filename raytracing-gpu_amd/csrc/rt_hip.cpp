@@ -103,6 +103,11 @@ struct rt_hip_ctx {
 // and the longest of them -- no longer hidden under other waves' camera
 // work -- sets the kernel's length.  RT_SEC_QUEUE=1 at context creation turns
 // it on (A/B).
+// per-rank candidate lists built without a host read-back (VERDICT r04
+// "render is async"): 1 = on (the first frame still reads its total back)
+#ifndef RT_ASYNC_LISTS_DEFAULT
+#define RT_ASYNC_LISTS_DEFAULT 1
+#endif
 #ifndef RT_SEC_QUEUE_DEFAULT
 #define RT_SEC_QUEUE_DEFAULT 0
 #endif
@@ -174,7 +179,21 @@ struct rt_hip_ctx {
   size_t cand_cap = 0, cand_tiles_cap = 0, order_cap = 0;
   void* d_scan_tmp = nullptr;
   size_t scan_tmp_bytes = 0;
-  uint32_t* h_cand = nullptr;  // pinned: total entries, risky, global, visits
+  uint32_t* h_cand = nullptr;  // pinned: total entries, risky, global, visits; [6..7] the last
+                               // asynchronous build's total and overflow flag (ctr[6..7])
+  // asynchronous per-rank builds (no host read-back in the render path): the
+  // entry buffers are sized from an earlier frame's total, read back without
+  // waiting when its build has finished
+  int async_lists = RT_ASYNC_LISTS_DEFAULT;
+  // the frame (camera frame, rank, nranks) whose per-rank lists were last
+  // built with a read-back, and their entry total: the same frame's lists
+  // are deterministic, so they are rebuilt without reading the total back
+  int known_valid = 0;
+  rt_frame known_frame{};
+  int known_rank = -1, known_nranks = 0;
+  uint32_t known_total = 0;
+  uint32_t known_nbig = 0, known_nitems = 0, known_over = 0;  // its big-emission launch shape
+  int last_async = 0;                 // the last render's lists came from an asynchronous build
   unsigned long long cand_prims = 0, cand_entries = 0, cand_global = 0;
   // triangle-parallel lists (rt_hip_cand_produce / rt_hip_cand_consume)
   uint32_t* d_send = nullptr;   // 3 words per routed entry, destination-rank order
@@ -618,6 +637,7 @@ extern "C" int rt_hip_create(int device, const rt_scene* scene, int accel, rt_hi
   rt_hip_ctx* c = new rt_hip_ctx();
   if (const char* e = std::getenv("RT_CAND_REFINE")) c->cand_refine = std::atoi(e) != 0;  // A/B knob
   if (const char* e = std::getenv("RT_SEC_QUEUE")) c->sec_queue = std::atoi(e) != 0;      // A/B knob
+  if (const char* e = std::getenv("RT_ASYNC_LISTS")) c->async_lists = std::atoi(e) != 0;  // A/B knob
   c->device = device;
   c->accel = dev_build ? (fs.ntri ? RT_ACCEL_OCTREE : RT_ACCEL_FLAT) : accel;
   c->nrec = (uint32_t)fs.nrec;
@@ -1337,7 +1357,7 @@ static int key_bits(size_t n_keys) {
 // glob_copies x globals (the triangle-parallel build routes each global to
 // every rank).  No contended atomics; deterministic.
 static int cand_build(rt_hip_ctx* c, CandParams& cp, hipStream_t s, uint32_t glob_copies, uint32_t* total_out,
-                      uint32_t* nglobal_out) {
+                      uint32_t* nglobal_out, bool async = false) {
   int rc = RT_OK;
   // every build overwrites the entry, offset and order buffers: lists that
   // rt_hip_cand_consume left for a render (ext) are gone from here on, so
@@ -1374,7 +1394,8 @@ static int cand_build(rt_hip_ctx* c, CandParams& cp, hipStream_t s, uint32_t glo
     HIP_TRY(hipMalloc((void**)&c->d_cand_off, (np + 1) * sizeof(uint32_t)));
     HIP_TRY(hipMalloc((void**)&c->d_cand_global, (np + 1) * sizeof(uint32_t)));
     HIP_TRY(hipMalloc((void**)&c->d_cand_big, (np + 1) * sizeof(uint32_t)));
-    HIP_TRY(hipMalloc((void**)&c->d_cand_ctr, 16 * sizeof(uint32_t)));  // [8]: a saved valid count
+    // [8]: a saved valid count; [16..23]: the last asynchronous build's ctr[0..7]
+    HIP_TRY(hipMalloc((void**)&c->d_cand_ctr, 32 * sizeof(uint32_t)));
     HIP_TRY(hipMalloc((void**)&c->d_cand_skip, (np + 1) * sizeof(float)));
     HIP_TRY(hipMalloc((void**)&c->d_cand_big_lane, (size_t)kBigLaneCap * 64 * sizeof(uint32_t)));
     HIP_TRY(hipMalloc((void**)&c->d_cand_items, ((size_t)kItemCap + 1) * sizeof(uint2)));
@@ -1438,6 +1459,32 @@ static int cand_build(rt_hip_ctx* c, CandParams& cp, hipStream_t s, uint32_t glo
   // over the list's length only (ctr[3], on the device); the entry total -> ctr[6]
   HIP_TRY(rt_cand_scan_dev(c->d_cand_visits, c->d_cand_off, (uint32_t)np, c->d_cand_ctr + 3, c->d_cand_ctr + 6,
                            c->d_scan_bsum, s));
+  if (async) {
+    // no read-back: the frame's lists were built before with a read-back of
+    // their total (known_total: deterministic for the same frame), so the
+    // buffers hold them; an entry past known_total would not be written and
+    // would set ctr[7] (rt_hip_stats then reports the frame: never silent).
+    // The emission kernels read the item count and the over-cap flag on the
+    // device and the render reads the global prims' count there
+    rc = cand_entry_buffers(c, c->known_total);
+    if (rc) return rc;
+    cp.keys = c->d_cand_keys;
+    cp.vals = c->d_cand_vals;
+    cp.key_cap = c->known_total;
+    HIP_TRY(rt_cand_emit(&cp, s));
+    // the same launch shape as the read-back build (the kernels read the
+    // counts on the device and loop over whatever they find)
+    if (c->known_over)
+      HIP_TRY(rt_cand_big(&cp, c->known_nbig, s));
+    else
+      HIP_TRY(rt_cand_big_items(&cp, c->known_nitems, 1, s));
+    HIP_TRY(rt_cand_fill_tail(c->d_cand_keys, c->d_cand_ctr + 6, c->known_total, cp.drop_key, s));
+    // this frame's counters for rt_hip_stats, in stream order, where no build writes
+    HIP_TRY(hipMemcpyAsync(c->d_cand_ctr + 16, c->d_cand_ctr, 8 * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    *total_out = c->known_total;  // the sort's length
+    *nglobal_out = 0;             // on the device (ctr[1])
+    return RT_OK;
+  }
   HIP_TRY(hipMemcpyAsync(c->h_cand, c->d_cand_ctr + 6, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
 #else
   tb = c->scan_tmp_bytes;
@@ -1452,13 +1499,17 @@ static int cand_build(rt_hip_ctx* c, CandParams& cp, hipStream_t s, uint32_t glo
   const uint32_t nitems = c->h_cand[4], items_over = c->h_cand[5];
   rc = cand_entry_buffers(c, (size_t)total + (size_t)glob_copies * nglobal);
   if (rc) return rc;
+  cp.key_cap = 0;
   cp.keys = c->d_cand_keys;
   cp.vals = c->d_cand_vals;
   HIP_TRY(rt_cand_emit(&cp, s));
   if (items_over)
     HIP_TRY(rt_cand_big(&cp, nbig, s));
   else
-    HIP_TRY(rt_cand_big_items(&cp, nitems, s));
+    HIP_TRY(rt_cand_big_items(&cp, nitems, 0, s));
+  c->known_nbig = nbig;
+  c->known_nitems = nitems;
+  c->known_over = items_over;
   *total_out = total;
   *nglobal_out = nglobal;
   return RT_OK;
@@ -1490,8 +1541,24 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
   cp.prim1 = c->nprim;
   const size_t nt = (size_t)kp->ntiles_local;
   uint32_t total = 0, nglobal = 0;
-  rc = cand_build(c, cp, s, 0, &total, &nglobal);
+  // asynchronous for a frame whose lists were built before (a new camera
+  // frame, rank split or the compatibility mode's lists read their total
+  // back once; so does cand_verify's rebuild, which keeps every footprint)
+  const bool async = RT_DEV_SCAN && c->async_lists && c->known_valid && !c->cand_store_fp && !compat &&
+                     c->known_rank == kp->rank && c->known_nranks == kp->nranks &&
+                     std::memcmp(&c->known_frame, f, sizeof *f) == 0;
+  rc = cand_build(c, cp, s, 0, &total, &nglobal, async);
   if (rc) return rc;
+  c->last_async = async ? 1 : 0;
+  if (!async && !compat) {  // the total just read back sizes this frame's later builds
+    c->known_valid = 1;
+    c->known_frame = *f;
+    c->known_rank = kp->rank;
+    c->known_nranks = kp->nranks;
+    c->known_total = total;
+  } else if (!async) {
+    c->known_valid = 0;
+  }
   rc = cand_tile_buffers(c, nt);
   if (rc) return rc;
   // keys are tiles < nt, or nt for an entry the refinement dropped: nt + 1 keys
@@ -1508,9 +1575,10 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
   kp->cand = c->d_cand;
   kp->cand_global = c->d_cand_global;
   kp->n_cand_global = nglobal;
+  kp->n_cand_global_dev = async ? c->d_cand_ctr + 1 : nullptr;
   kp->cand_skip = entry_skip;
   c->cand_entries = total;  // until rt_hip_stats reads start[nt]
-  c->d_cand_valid = c->cand_refine ? c->d_cand_start + nt : nullptr;
+  c->d_cand_valid = (c->cand_refine || async) ? c->d_cand_start + nt : nullptr;
   c->cand_global = nglobal;
   c->cand_prims = 0;  // not counted separately (entries and globals are)
   return RT_OK;
@@ -1732,6 +1800,7 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
     // gathers as padding.  Its stats read 0.
     c->cand_prims = c->cand_entries = c->cand_global = 0;
     c->d_cand_valid = nullptr;
+    c->last_async = 0;
     hipEvent_t* ev = c->ev[c->frames % RT_TIMED_FRAMES];
     if (c->timing) HIP_TRY(hipEventRecord(ev[0], s));
     HIP_TRY(hipMemsetAsync(c->d_counter, 0, kFrameCounterBytes, s));
@@ -1828,6 +1897,7 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
       if (rc) return rc;
     }
   }
+  if (!(c->accel == RT_ACCEL_OCTREE && c->d_node && c->exact_camera && !use_ext)) c->last_async = 0;
   // an empty octree scene has nothing to traverse: the FLAT kernels with 0
   // records are exact (their grids are the FLAT instantiation's own)
   const bool empty = c->accel == RT_ACCEL_OCTREE && !c->d_node;
@@ -2087,12 +2157,23 @@ extern "C" int rt_hip_stats(rt_hip_ctx* c, rt_stats* out) {
   hipStream_t s = c->last_stream ? c->last_stream : c->stream;
   HIP_TRY(hipMemcpyAsync(hs, c->d_stats, sizeof hs, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(hc, c->d_hit_count, sizeof hc, hipMemcpyDeviceToHost, s));
-  uint32_t valid = 0;
+  uint32_t valid = 0, actr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (c->d_cand_valid) HIP_TRY(hipMemcpyAsync(&valid, c->d_cand_valid, sizeof valid, hipMemcpyDeviceToHost, s));
+  const int was_async = c->last_async;
+  if (was_async) HIP_TRY(hipMemcpyAsync(actr, c->d_cand_ctr + 16, sizeof actr, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   if (c->d_cand_valid) {
     c->cand_entries = valid;
     c->d_cand_valid = nullptr;
+  }
+  if (was_async) {
+    c->last_async = 0;
+    c->cand_global = actr[1];
+    if (actr[7]) {  // never expected (the same frame's lists): reported, and the next build reads back
+      c->known_valid = 0;
+      return rt_set_error(RT_EHITBUF, "%u candidate-list entries, %u expected: render again", actr[6],
+                          c->known_total);
+    }
   }
   for (int k = 0; k < RT_NSTATS; k++) {  // the copies of each counter (RT_STAT_SETS)
     h[k] = 0;
@@ -2201,7 +2282,7 @@ extern "C" int rt_hip_render_image(rt_hip_ctx* c, const rt_frame* f, float* h_rg
   }
   rt_stats tmp;
   int rc = RT_OK;
-  for (int attempt = 0; attempt < 2; attempt++) {  // once more after the hit buffer grew
+  for (int attempt = 0; attempt < 3; attempt++) {  // again after the hit or list buffers grew
     rc = rt_hip_render(c, f, 0, 1, d_tiles, nullptr);
     if (!rc) rc = rt_hip_assemble(c, f, d_tiles, 1, d_rgb, nullptr);
     if (!rc && hipMemcpyAsync(h_rgb, d_rgb, npx * 3 * sizeof(float), hipMemcpyDeviceToHost,

@@ -153,6 +153,7 @@ struct KParams {
   const uint32_t* cand;         // prims
   const uint32_t* cand_global;  // prims every camera ray tests
   uint32_t n_cand_global;
+  const uint32_t* n_cand_global_dev;  // their count on the device (an asynchronous list build), or NULL
   const float4* tri_prim;       // prim-order triangle records
   const float* cand_skip;       // per cand entry: lower bound of new_dist - |pos - o| (depth skip)
   const uint32_t* tile_order;   // trace_kernel's work order: position -> rank-local tile (NULL: identity)

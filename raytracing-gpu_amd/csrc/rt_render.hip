@@ -1615,18 +1615,42 @@ __device__ col apply_light(const KParams& p, bool hit, const float* m, f3 P, f3 
 // parallel -- one memory round trip -- into the LDS stage, compacted, then
 // tested one after another as LDS broadcasts).  bmax: entries whose depth
 // skip bound exceeds it cannot win any lane.  Returns the entries tested.
+#ifndef RT_CAND_AHEAD
+#define RT_CAND_AHEAD 0
+#endif
 template <bool COUNT>
 __device__ __forceinline__ uint32_t cand_range(const KParams& p, const Ray& r, bool act, uint32_t s, uint32_t e,
                                                float bmax, Best& b, WaveCtx& w) {
   const int lane = w.lane;
   uint32_t tested = 0;
+#if RT_CAND_AHEAD
+  // the next round's entries (prim, skip bound) in flight while this round's
+  // records are gathered and tested
+  uint32_t nprim = 0;
+  float nskip = 0.0f;
+  if (lane < kOctRecs && s + lane < e) {
+    nprim = p.cand[s + lane];
+    nskip = p.cand_skip[s + lane];
+  }
+#endif
   for (uint32_t base = s; base < e; base += kOctRecs) {
     uint32_t prim = 0;
     bool keep = false;
+#if RT_CAND_AHEAD
+    if (lane < kOctRecs && base + lane < e) {
+      prim = nprim;
+      keep = !(nskip > bmax);
+    }
+    if (lane < kOctRecs && base + kOctRecs + lane < e) {
+      nprim = p.cand[base + kOctRecs + lane];
+      nskip = p.cand_skip[base + kOctRecs + lane];
+    }
+#else
     if (lane < kOctRecs && base + lane < e) {
       prim = p.cand[base + lane];
       keep = !(p.cand_skip[base + lane] > bmax);
     }
+#endif
     const uint64_t m = __ballot(keep);
     if (m == 0) continue;
     const uint32_t n = (uint32_t)__popcll(m);
@@ -1675,14 +1699,15 @@ __device__ __forceinline__ void cand_closest(const KParams& p, const Ray& r, boo
     const float bmax = __uint_as_float(uni(__float_as_uint(bl)));
   const uint32_t tested =
       cand_range<COUNT>(p, r, act, uni(p.cand_start[tile]), uni(p.cand_start[tile + 1]), bmax, b, w);
-  for (uint32_t k = 0; k < p.n_cand_global; k++) {
+  const uint32_t n_glob = p.n_cand_global_dev ? uni(*p.n_cand_global_dev) : p.n_cand_global;
+  for (uint32_t k = 0; k < n_glob; k++) {
     const float4* q = p.tri_prim + 3 * (size_t)uni(p.cand_global[k]);
     float4 q0 = ldu(q, 0), q1 = ldu(q, 1), q2 = ldu(q, 2);
     if (act) consider(r, q0, q1, q2, b);
   }
   if (COUNT) {
-    wc.tris += tested + p.n_cand_global;
-    wc.cl_tris += (tested + p.n_cand_global) * (uint32_t)__popcll(__ballot(act));
+    wc.tris += tested + n_glob;
+    wc.cl_tris += (tested + n_glob) * (uint32_t)__popcll(__ballot(act));
   }
 }
 
