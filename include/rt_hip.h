@@ -376,6 +376,12 @@ int rt_hip_cand_produce(rt_hip_ctx *ctx, const rt_frame *frame, int rank, int nr
 int rt_hip_cand_send_buffer(const rt_hip_ctx *ctx, const void **d_entries, size_t *n);
 int rt_hip_cand_consume(rt_hip_ctx *ctx, const rt_frame *frame, int rank, int nranks, const void *d_entries,
                         size_t n, unsigned nglobal, void *stream);
+/* Steps 1-4 for n contexts of this process at once (ctx[r] = rank r, any
+ * devices, e.g. all on one GPU): produce on every rank, the blocks moved by
+ * device memcpys, consume on every rank; synchronous.  rt_raytrace_multi
+ * makes the same exchange over RCCL (grouped ncclSend / ncclRecv) from 4
+ * GPUs up. */
+int rt_hip_cand_exchange_local(rt_hip_ctx **ctx, int n, const rt_frame *frame);
 
 /* d_gathered = nranks consecutive tile buffers (rank-major, as an RCCL gather
  * delivers them); writes the PPM-order image (W*H*3 floats) to d_rgb. */

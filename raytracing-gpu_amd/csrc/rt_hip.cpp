@@ -2478,6 +2478,104 @@ static int per_gpu(int ngpus, F fn) {
   return RT_OK;
 }
 
+// Triangle-parallel candidate lists of an n-rank frame over n contexts in
+// this process (rt_raytrace_multi, and tests on one GPU): every rank produces
+// the whole frame's entries of its 1/n of the triangles (rt_hip_cand_produce,
+// one thread per rank), the blocks are exchanged -- one grouped RCCL
+// send/recv all-to-all over the ranks' communicators (comms != NULL: one
+// device per rank, xGMI), or device memcpys (comms == NULL: any devices, e.g.
+// every context on GPU 0 in a test) -- and every rank consumes its own
+// (rt_hip_cand_consume); each context's next rt_hip_render(f, rank, n) uses
+// them.  The same three library calls bench.py makes around
+// torch.distributed's all_to_all_single.
+static int cand_exchange(rt_hip_ctx* const* ctx, int n, const rt_frame* f, ncclComm_t* comms) {
+  std::vector<std::vector<unsigned>> counts(n, std::vector<unsigned>(n, 0));
+  std::vector<unsigned> ng(n, 0);
+  int rc = per_gpu(n, [&](int r) {
+    return rt_hip_cand_produce(ctx[r], f, r, n, counts[r].data(), &ng[r], nullptr);
+  });
+  if (rc) return rc;
+  unsigned nglobal = 0;
+  for (unsigned x : ng) nglobal += x;
+  // rank d receives counts[r][d] entries from each r, in source order
+  std::vector<size_t> recv_n(n, 0);
+  for (int d = 0; d < n; d++)
+    for (int r = 0; r < n; r++) recv_n[d] += counts[r][d];
+  std::vector<uint32_t*> recv(n, nullptr);
+  bool in_group = false;
+  for (int d = 0; d < n && !rc; d++)
+    rc = rt_hip_malloc(ctx[d]->device, (recv_n[d] + 1) * 12, (void**)&recv[d]);
+  if (!rc && comms) {
+    NCCL_TRY(ncclGroupStart());
+    in_group = true;
+    for (int r = 0; r < n; r++) {
+      (void)hipSetDevice(ctx[r]->device);
+      size_t so = 0, ro = 0;
+      for (int d = 0; d < n; d++) {  // what r sends to d, and receives from d
+        if (counts[r][d]) NCCL_TRY(ncclSend(ctx[r]->d_send + 3 * so, 3 * (size_t)counts[r][d], ncclUint32, d,
+                                            comms[r], ctx[r]->stream));
+        if (counts[d][r]) NCCL_TRY(ncclRecv(recv[r] + 3 * ro, 3 * (size_t)counts[d][r], ncclUint32, d,
+                                            comms[r], ctx[r]->stream));
+        so += counts[r][d];
+        ro += counts[d][r];
+      }
+    }
+    in_group = false;
+    NCCL_TRY(ncclGroupEnd());
+  } else if (!rc) {
+    for (int r = 0; r < n && !rc; r++) {
+      if (hipSetDevice(ctx[r]->device) != hipSuccess || hipStreamSynchronize(ctx[r]->stream) != hipSuccess) {
+        rc = rt_set_error(RT_EHIP, "exchange: producer %d", r);
+        break;
+      }
+    }
+    for (int d = 0; d < n && !rc; d++) {
+      size_t ro = 0;
+      for (int r = 0; r < n && !rc; r++) {
+        size_t so = 0;
+        for (int k = 0; k < d; k++) so += counts[r][k];
+        if (counts[r][d] &&
+            hipMemcpyPeer(recv[d] + 3 * ro, ctx[d]->device, ctx[r]->d_send + 3 * so, ctx[r]->device,
+                          (size_t)counts[r][d] * 12) != hipSuccess)
+          rc = rt_set_error(RT_EHIP, "exchange: %d -> %d", r, d);
+        ro += counts[r][d];
+      }
+    }
+  }
+  if (!rc)
+    rc = per_gpu(n, [&](int d) {
+      return rt_hip_cand_consume(ctx[d], f, d, n, recv[d], recv_n[d], nglobal, nullptr);
+    });
+  // the consumes read the received blocks on their streams: wait, then free
+  for (int d = 0; d < n; d++) {
+    if (recv[d]) {
+      (void)hipSetDevice(ctx[d]->device);
+      (void)hipStreamSynchronize(ctx[d]->stream);
+      rt_hip_free(recv[d]);
+    }
+  }
+  return rc;
+out:
+  if (in_group) (void)ncclGroupEnd();
+  for (int d = 0; d < n; d++)
+    if (recv[d]) rt_hip_free(recv[d]);
+  return rc;
+}
+
+extern "C" int rt_hip_cand_exchange_local(rt_hip_ctx** ctx, int n, const rt_frame* f) {
+  if (!ctx || !f || n < 1 || n > 256) return rt_set_error(RT_EINVAL, "bad argument");
+  for (int r = 0; r < n; r++)
+    if (!ctx[r]) return rt_set_error(RT_EINVAL, "null context %d", r);
+  return cand_exchange(ctx, n, f, nullptr);
+}
+
+// rt_raytrace_multi's candidate lists: triangle-parallel from this many GPUs
+// up (as bench.py: below it the second sort and the exchange cost more than
+// the per-rank build's shared part)
+#ifndef RT_MULTI_PARTITION_MIN
+#define RT_MULTI_PARTITION_MIN 4
+#endif
+
 extern "C" int rt_raytrace_multi(const char* input, const char* output, int ngpus, int accel,
                                  rt_stats* stats, double* render_ms) {
   if (!input || !output || ngpus < 1 || ngpus > 64) return rt_set_error(RT_EINVAL, "bad argument");
@@ -2535,6 +2633,11 @@ extern "C" int rt_raytrace_multi(const char* input, const char* output, int ngpu
     (void)hipDeviceSynchronize();
   }
   t0 = std::chrono::steady_clock::now();
+  if (ngpus >= RT_MULTI_PARTITION_MIN && ctx[0]->accel == RT_ACCEL_OCTREE && ctx[0]->d_node &&
+      ctx[0]->exact_camera) {
+    rc = cand_exchange(ctx.data(), ngpus, &f, comms.data());  // each rank 1/N of the triangles, one all-to-all
+    if (rc) goto out;
+  }
   rc = per_gpu(ngpus, [&](int g) {
     int r = rt_hip_render(ctx[g], &f, g, ngpus, d_tiles[g], nullptr);
     rt_stats st;

@@ -188,6 +188,7 @@ _PROTOS = [
                                   C.c_void_p]),
     ("rt_hip_cand_produce", C.c_int, [C.c_void_p, C.POINTER(Frame), C.c_int, C.c_int, C.POINTER(C.c_uint),
                                       C.POINTER(C.c_uint), C.c_void_p]),
+    ("rt_hip_cand_exchange_local", C.c_int, [C.POINTER(C.c_void_p), C.c_int, C.POINTER(Frame)]),
     ("rt_hip_cand_send_buffer", C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
     ("rt_hip_cand_consume", C.c_int, [C.c_void_p, C.POINTER(Frame), C.c_int, C.c_int, C.c_void_p, C.c_size_t,
                                       C.c_uint, C.c_void_p]),
@@ -655,6 +656,16 @@ class Context:
             self.close()
         except Exception:
             pass
+
+
+def cand_exchange_local(contexts, frame):
+    """Triangle-parallel lists of an len(contexts)-rank frame in this process
+    (rt_hip_cand_exchange_local): contexts[r] produces rank r's slice, the
+    blocks move by device memcpy, every rank consumes its own; each context's
+    next render(frame, r, n) uses them.  The exchange rt_raytrace_multi makes
+    over RCCL from 4 GPUs up, drivable with every context on one GPU."""
+    arr = (C.c_void_p * len(contexts))(*[c.h for c in contexts])
+    _check(lib().rt_hip_cand_exchange_local(arr, len(contexts), C.byref(frame)), "rt_hip_cand_exchange_local")
 
 
 def exchange_cand_entries(dist, send, counts, nglobal):

@@ -559,6 +559,27 @@ def test_triangle_parallel_lists_match_per_rank(gpu, nranks, accel):
     assert_bitexact(t2, t_ref, "per-rank build after a consumed frame")
 
 
+@pytest.mark.parametrize("nranks", [4, 8])
+def test_cand_exchange_local_matches_per_rank(gpu, nranks):
+    """the exchange rt_raytrace_multi makes over RCCL (from 4
+    GPUs up), driven with N contexts on one GPU and the device-memcpy
+    transport: every rank's render from the exchanged lists equals its render
+    from its own per-rank lists, bit for bit, with the same entry count."""
+    s = gpu.Scene.synthetic(6, 6, 9776, seed=0x5EED, width=960, height=540)
+    f = s.frame()
+    ctxs = [gpu.Context(s, "octree_gpu") for _ in range(nranks)]
+    ref = gpu.Context(s, "octree_gpu")
+    gpu.cand_exchange_local(ctxs, f)
+    for d in range(nranks):
+        t_ext, st_ext = _tiles_of_rank(ctxs[d], f, d, nranks)
+        t_ref, st_ref = _tiles_of_rank(ref, f, d, nranks)
+        assert st_ext["cand_entries"] == st_ref["cand_entries"] > 0, d
+        assert_bitexact(t_ext, t_ref, f"rank {d}/{nranks}: exchanged vs per-rank lists")
+        assert (st_ext["closest"], st_ext["shadow"]) == (st_ref["closest"], st_ref["shadow"])
+    with pytest.raises(gpu.RtError):
+        gpu.cand_exchange_local([], f)
+
+
 def test_consumed_lists_invalidated_by_a_later_build(gpu):
     """lists rt_hip_cand_consume leaves for a render live in the
     context's shared list buffers.  A produce (e.g. the next frame's) between
