@@ -16,13 +16,19 @@ namespace rtc {
 struct Footprint;
 }
 
+// prims per block of a producer's interleaved slice (CandParams::sl_stride)
+#define RT_SLICE_BLOCK 1024u
+
 struct CandParams {
   const float4* tri;      // prim-order triangle records (3 float4 each)
   const float4* node;     // octree nodes (2 float4 each: box + words), may be NULL
   const uint32_t* prim_leaf;  // nprim: a leaf holding a record of the prim (NULL: none)
   uint32_t nprim;
-  uint32_t prim0, prim1;  // the prims this build lists: [prim0, prim1) (a slice of a
-                          // triangle-parallel multi-GPU build; else [0, nprim))
+  uint32_t prim0, prim1;  // the prims this build lists: [prim0, prim1) (else [0, nprim)), or
+  uint32_t sl_stride, sl_rank;  // with sl_stride > 1, the i-th of prim1 - prim0 prims of
+                          // the blocks of RT_SLICE_BLOCK prims b = sl_rank mod sl_stride
+                          // (a producer's slice of a triangle-parallel multi-GPU build:
+                          // interleaved blocks spread a scene region's cost over the producers)
   double pos[3];          // eye (camera position)
   double u[3], v[3];      // image-plane axes (normalised camera u, v)
   double C[3];            // image-plane origin
@@ -64,6 +70,7 @@ struct CandParams {
   uint32_t* vals;         // entries: prim
   uint32_t* global;       // nprim: prims whose footprint is unbounded
   uint32_t* ctr;          // [1] global prims, [2] big footprints, [3] list length,
+                          // [4] big emission items (item_kernel),
                           // [5] 1 = more than item_cap items (big_kernel emits instead),
                           // [6] the entry total, [7] 1 = an entry past key_cap
   uint32_t* big;          // nprim: list entries with big footprints (rt_cand.hip kSmallRows)
@@ -72,6 +79,7 @@ struct CandParams {
   uint32_t big_cap;       // (big_count_kernel -> big_kernel; beyond it big_kernel recounts)
   uint2* items;           // item_cap: (big footprint, chunk of its entries), big_item_kernel's waves
   uint32_t item_cap;
+  uint32_t chunk_shift;   // entries per item = 1 << chunk_shift
   uint32_t* wave_items;   // rt_cand_big_waves() + 1: items of each big_count wave ([last] = 0)
   const uint32_t* wave_base;  // its exclusive scan ([last] = all items)
   // 1: the big footprints' entries are refined per tile (rt_cand.hip
@@ -132,7 +140,7 @@ extern "C" uint32_t rt_cand_scan_dev_tiles(uint32_t nmax);
 extern "C" hipError_t rt_cand_scan_dev(const uint32_t* in, uint32_t* out, uint32_t nmax, const uint32_t* n_dev,
                                        uint32_t* total, uint32_t* bsum, hipStream_t s);
 extern "C" hipError_t rt_cand_sort(uint32_t* keys_in, uint32_t* keys_out, uint32_t* vals_in,
-                                   uint32_t* vals_out, uint32_t n, int bits, void* temp,
+                                   uint32_t* vals_out, uint32_t n, int begin_bit, int end_bit, void* temp,
                                    size_t* temp_bytes, hipStream_t s);
 // out[i] = skip[cand[i]]: the sorted lists' per-entry depth-skip bounds
 // keys[i] = key for i in [*total_dev, n) (an asynchronous build's unused tail)
@@ -145,28 +153,38 @@ extern "C" hipError_t rt_cand_bounds(const uint32_t* keys, uint32_t n, uint32_t*
 // Triangle-parallel multi-GPU lists (rt_hip_cand_produce / rt_hip_cand_consume):
 // a whole-frame build (one rank, scanline tiles) of a slice of the prims, its
 // entries routed to the N-rank tile map.  route: key = scanline tile ->
-// dest_rank * (tpr + 1) + rank-local tile (tpr = tiles per rank), and
-// drop_key (an entry the refinement dropped) -> nranks * (tpr + 1); globals:
-// one entry per rank with the local slot tpr.  rank_bounds: start[d] = first
-// entry of rank d in the routed, sorted keys (start[n] = the routed entries,
-// the dropped ones sort after them).  pack: 3
-// words per entry (local tile or tpr, prim, skip bits).  unpack (consumer):
+// dest_rank << tbits | rank-local tile (tpr = tiles per rank < 2^tbits), and
+// drop_key (an entry the refinement dropped) -> nranks << tbits; globals:
+// one entry per rank with the local slot tpr.  Then partitioned by rank
+// (part_*, below) into 3 words per entry (local tile or tpr, prim, skip
+// bits).  unpack (consumer):
 // keys = local tile (tpr -> ntiles: the globals sort last), idx = i.
 // gather: the sorted entries' prims and skip bounds.
 extern "C" hipError_t rt_cand_route(uint32_t* keys, uint32_t n, int tiles_x, int nranks, int blocks_x, int tb,
-                                    uint32_t tpr, uint32_t drop_key, hipStream_t s);
+                                    uint32_t tbits, uint32_t drop_key, const uint32_t* total_dev, hipStream_t s);
 extern "C" hipError_t rt_cand_route_globals(const uint32_t* global, uint32_t nglobal, int nranks, uint32_t tpr,
-                                            uint32_t* keys, uint32_t* vals, hipStream_t s);
-extern "C" hipError_t rt_cand_rank_bounds(const uint32_t* keys, uint32_t n, uint32_t tpr, int nranks,
-                                          uint32_t* start, hipStream_t s);
-extern "C" hipError_t rt_cand_pack(const uint32_t* keys, const uint32_t* prims, const float* skip, uint32_t n,
-                                   uint32_t tpr, uint32_t* out, hipStream_t s);
+                                            uint32_t tbits, uint32_t* keys, uint32_t* vals, hipStream_t s);
+// Stable partition of n routed keys by rank (rank nranks: dropped), packed
+// 3 words per entry in out (the dropped ones not written), start[d] = first
+// entry of rank d (start[nranks] = the routed entries): part_count ->
+// hist[(nranks + 1) x rt_cand_part_waves(n)] -> exclusive scan (off) ->
+// part_scatter.  nranks <= 256.
+extern "C" uint32_t rt_cand_part_waves(uint32_t n);
+extern "C" hipError_t rt_cand_part_count(const uint32_t* keys, uint32_t n, uint32_t tbits, int nranks,
+                                         uint32_t* hist, hipStream_t s);
+extern "C" hipError_t rt_cand_part_scatter(const uint32_t* keys, const uint32_t* prims, const float* skip,
+                                           uint32_t n, uint32_t tbits, int nranks, const uint32_t* off,
+                                           uint32_t* start, uint32_t* out, hipStream_t s);
 extern "C" hipError_t rt_cand_unpack(const uint32_t* in, uint32_t n, uint32_t ntiles, uint32_t tpr, uint32_t* keys,
                                      uint32_t* idx, hipStream_t s);
 extern "C" hipError_t rt_cand_gather(const uint32_t* in, const uint32_t* idx, uint32_t n, uint32_t* cand,
                                      float* skip, hipStream_t s);
 // longest-first work order of the tiles (heavy candidate lists first):
 // perm[position] = tile.  tmp == NULL: *tmp_bytes = the scan's need.
+// item_cost / cost_sum / waves (optional): the per-item clocks, their sum
+// and the grid of an earlier trace of the same frame: tiles with an item
+// longer than a quarter of a wave's balanced share also go first.
 extern "C" hipError_t rt_cand_order(const uint32_t* start, uint32_t ntiles, uint32_t total,
-                                    uint32_t* flags, uint32_t* pos, uint32_t* perm, void* tmp,
+                                    uint32_t* flags, uint32_t* pos, uint32_t* perm, const uint32_t* item_cost,
+                                    const unsigned long long* cost_sum, uint32_t waves, void* tmp,
                                     size_t* tmp_bytes, hipStream_t s);

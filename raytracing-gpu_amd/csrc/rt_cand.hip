@@ -883,10 +883,14 @@ constexpr uint32_t kSmallEntries = 32;
 // persistent waves of the big-footprint passes (they loop over the big list,
 // whose length only the device knows before the scan)
 constexpr int kBigWaves = 4096;
-// entries per big_item_kernel wave.  One wave per footprint (big_kernel) left
-// the chip idle behind a few long ones: C5's largest footprint has 53,789
-// entries in rows of ~200 tiles, each lane writing its row alone, and the
-// kernel ran at 0.42 resident waves per SIMD (profiles/r03w_c5/pmc_sq.json).
+// Entries per big_item_kernel / refine_kernel wave: 1 << CandParams::
+// chunk_shift.  One wave per footprint (big_kernel) left the chip idle behind
+// a few long ones: C5's largest footprint has 53,789 entries in rows of ~200
+// tiles, each lane writing its row alone, and the kernel ran at 0.42 resident
+// waves per SIMD (profiles/r03w_c5/pmc_sq.json).  1024 for a whole frame; a
+// build of 1/N of the work (a rank's share, a producer's slice) has 1/N of
+// the items, too few to cover the latency of one, and takes smaller chunks
+// (rt_hip.cpp cand_chunk_shift).
 // threads per workgroup of the per-prim list passes (fast path,
 // classification, small emission)
 #ifndef RT_LIST_BLOCK
@@ -898,22 +902,25 @@ constexpr int kBigWaves = 4096;
 #ifndef RT_SORT_BITS
 #define RT_SORT_BITS 9
 #endif
-#ifndef RT_CAND_CHUNK
-#define RT_CAND_CHUNK 1024
-#endif
-constexpr uint32_t kChunk = RT_CAND_CHUNK;
 
 // Pass 0: the float fast path over every prim; flags the prims it cannot
 // prove safe (visits[prim] = 1), which an exclusive scan and scatter_kernel
 // turn into a compact list, so the f64 classification of pass 1 runs on full
 // waves instead of on the scattered third of the lanes of every wave.
+// the i-th prim of the build's slice (CandParams::prim0, sl_stride)
+__device__ __forceinline__ uint32_t slice_prim(const CandParams& p, uint32_t i) {
+  if (p.sl_stride <= 1u) return p.prim0 + i;
+  const uint32_t b = i / RT_SLICE_BLOCK;
+  return (b * p.sl_stride + p.sl_rank) * RT_SLICE_BLOCK + i % RT_SLICE_BLOCK;
+}
+
 __global__ __launch_bounds__(RT_LIST_BLOCK) void quick_kernel(CandParams p) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;  // index in the slice [prim0, prim1)
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;  // index in the slice
   const uint32_t len = p.prim1 - p.prim0;
   if (i < 8u) p.ctr[i] = 0u;          // the frame's counters (count / big passes, later launches)
   if (i == 0u) p.visits[len] = 0u;    // the scan's last input
   if (i >= len) return;
-  p.visits[i] = quick_class(p, (const float*)(p.tri + 3 * (size_t)(p.prim0 + i))) == Q_LIST ? 1u : 0u;
+  p.visits[i] = quick_class(p, (const float*)(p.tri + 3 * (size_t)slice_prim(p, i))) == Q_LIST ? 1u : 0u;
 }
 
 __global__ __launch_bounds__(256) void scatter_kernel(CandParams p) {
@@ -924,7 +931,7 @@ __global__ __launch_bounds__(256) void scatter_kernel(CandParams p) {
     p.ctr[3] = p.off[len];  // list length
     return;
   }
-  if (p.visits[i]) p.list[p.off[i]] = p.prim0 + i;
+  if (p.visits[i]) p.list[p.off[i]] = slice_prim(p, i);
 }
 
 // The footprints whose entries are refined per tile (CandParams::refine):
@@ -1044,9 +1051,9 @@ __global__ __launch_bounds__(64) void big_count_kernel(CandParams p) {
     if (b < p.big_cap) p.big_lane[(size_t)b * 64 + lane] = cnt;  // big_kernel's offsets
     cnt = wave_sum(cnt);
     if (lane == 0) p.visits[j] = cnt;
-    witems += (cnt + kChunk - 1) / kChunk;
+    witems += (cnt + (1u << p.chunk_shift) - 1) >> p.chunk_shift;
   }
-  // this wave's big_item_kernel items (one per kChunk entries of each of its
+  // this wave's big_item_kernel items (one per chunk of entries of each of its
   // footprints), placed by a scan over the waves: one atomic per footprint
   // on a shared counter serialised at L2 (big_count 0.16 -> 1.5 ms on C5)
   if (lane == 0) p.wave_items[blockIdx.x] = witems;
@@ -1059,8 +1066,9 @@ __global__ __launch_bounds__(64) void item_kernel(CandParams p) {
   const int lane = threadIdx.x;
   const uint32_t nbig = p.ctr[2];
   uint32_t at = p.wave_base[blockIdx.x];
+  if (blockIdx.x == 0 && lane == 0) p.ctr[4] = p.wave_base[kBigWaves];  // all items (read back with ctr[])
   for (uint32_t b = blockIdx.x; b < nbig; b += gridDim.x) {
-    const uint32_t ni = (p.visits[p.big[b]] + kChunk - 1) / kChunk;
+    const uint32_t ni = (p.visits[p.big[b]] + (1u << p.chunk_shift) - 1) >> p.chunk_shift;
     if (at + ni <= p.item_cap) {
       for (uint32_t c = (uint32_t)lane; c < ni; c += 64) p.items[at + c] = make_uint2(b, c);
     } else if (lane == 0) {
@@ -1188,7 +1196,7 @@ __device__ __forceinline__ int kth_rank_col(const CandParams& p, int x0, int x1,
 }
 
 // Pass 2b, entry-parallel (big_count_kernel's items): the wave writes entries
-// [c kChunk, (c + 1) kChunk) of big footprint b, lane-consecutive (coalesced
+// [c chunk, (c + 1) chunk) of big footprint b, lane-consecutive (coalesced
 // stores).  Row by row in row-major order, each row's intervals in
 // raster_row's order; the rows are taken 64 at a time -- the lanes compute
 // their intervals and counts (row_ivs), a wave scan places them, and each
@@ -1218,8 +1226,8 @@ __global__ __launch_bounds__(64) void big_item_kernel(CandParams p) {
   const uint2 it = p.items[blockIdx.x];
   const uint32_t j = p.big[it.x], prim = p.list[j];
   const uint32_t base = p.off[j], total = p.off[j + 1] - base;
-  const uint32_t c0 = it.y * kChunk;
-  uint32_t c1 = c0 + kChunk < total ? c0 + kChunk : total;
+  const uint32_t c0 = it.y << p.chunk_shift;
+  uint32_t c1 = c0 + (1u << p.chunk_shift) < total ? c0 + (1u << p.chunk_shift) : total;
   if (CHECK && base + c1 > p.key_cap) {  // entries past the buffers: not written, the frame reported
     if (lane == 0) p.ctr[7] = 1u;
     c1 = p.key_cap > base ? p.key_cap - base : 0u;
@@ -1299,7 +1307,8 @@ __device__ __forceinline__ void refine_item(const CandParams& p, uint32_t item) 
   int r0, r1;
   if (!raster_rows(p, fp, r0, r1) || !refined_rows(r0, r1)) return;
   const uint32_t base = p.off[j], total = p.off[j + 1] - base;
-  const uint32_t c0 = it.y * kChunk, c1 = c0 + kChunk < total ? c0 + kChunk : total;
+  const uint32_t c0 = it.y << p.chunk_shift;
+  const uint32_t c1 = c0 + (1u << p.chunk_shift) < total ? c0 + (1u << p.chunk_shift) : total;
   __shared__ TileTri tt;
   __shared__ TileFrame tf;
   __shared__ int tt_ok;
@@ -1363,58 +1372,118 @@ __global__ __launch_bounds__(256) void entry_skip_kernel(const uint32_t* cand, c
 
 // --- triangle-parallel multi-GPU lists (rt_cand.h "route") ---------------
 // A whole-frame entry (scanline tile of the one-rank map) -> its rank d and
-// rank-local tile l under the N-rank block map: key d (tpr + 1) + l.
+// rank-local tile l under the N-rank block map: key d << tbits | l (l <= tpr
+// < 2^tbits), partitioned by d below.
 __global__ __launch_bounds__(256) void route_kernel(uint32_t* keys, uint32_t n, int tiles_x, int nranks,
-                                                    int blocks_x, int tb, uint32_t tpr, uint32_t drop_key) {
+                                                    int blocks_x, int tb, uint32_t tbits, uint32_t drop_key,
+                                                    const uint32_t* total_dev) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint32_t t = keys[i];
+  // an asynchronous build's buffers hold the known total: entries past the
+  // build's own (total_dev) are unused (never expected; checked by the host)
+  const uint32_t t = total_dev && i >= *total_dev ? drop_key : keys[i];
   if (t == drop_key) {  // dropped by the refinement: after every rank's entries
-    keys[i] = (uint32_t)nranks * (tpr + 1u);
+    keys[i] = (uint32_t)nranks << tbits;
     return;
   }
   uint32_t d;
   const uint32_t l = rt_tile_local((int)(t % (uint32_t)tiles_x), (int)(t / (uint32_t)tiles_x), (uint32_t)nranks,
                                    (uint32_t)blocks_x, (uint32_t)tb, &d);
-  keys[i] = d * (tpr + 1u) + l;
+  keys[i] = d << tbits | l;
 }
 
 // the slice's globals: one entry per rank, local slot tpr
 __global__ __launch_bounds__(256) void route_globals_kernel(const uint32_t* global, uint32_t nglobal, int nranks,
-                                                            uint32_t tpr, uint32_t* keys, uint32_t* vals) {
+                                                            uint32_t tpr, uint32_t tbits, uint32_t* keys,
+                                                            uint32_t* vals) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nglobal * (uint32_t)nranks) return;
   const uint32_t d = i / nglobal, g = i % nglobal;
-  keys[i] = d * (tpr + 1u) + tpr;
+  keys[i] = d << tbits | tpr;
   vals[i] = global[g];
 }
 
-// start[d] = first entry of rank d (keys sorted), start[nranks] = the routed
-// entries (the dropped ones, key nranks (tpr + 1), sort after them)
-__global__ __launch_bounds__(64) void rank_bounds_kernel(const uint32_t* keys, uint32_t n, uint32_t tpr,
-                                                         int nranks, uint32_t* start) {
-  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
-  if (d > (uint32_t)nranks) return;
-  const uint32_t key = d * (tpr + 1u);
-  uint32_t lo = 0, hi = n;
-  while (lo < hi) {
-    const uint32_t mid = lo + (hi - lo) / 2;
-    if (keys[mid] < key)
-      lo = mid + 1;
-    else
-      hi = mid;
+// Stable partition of the routed entries by destination rank, packed for
+// the exchange (replaces a radix sort on the rank bits + rank_bounds + pack:
+// 3 launches and a scan instead of 9; the produce step is latency-bound at
+// 1/N of a frame).  Wave w owns entries [w kPartChunk, (w + 1) kPartChunk);
+// part_count_kernel -> hist[d nw + w] = its entries of rank d (d <= nranks,
+// nranks = dropped) -> exclusive scan (rank-major: every rank's entries in
+// wave order) -> part_scatter_kernel writes each entry at its rank's running
+// offset, in entry order (a per-step ballot per distinct rank), 3 words
+// (local tile or tpr, prim, skip bits); start[d] = hist offset of (d, 0).
+constexpr uint32_t kPartSteps = 16, kPartChunk = 64 * kPartSteps;
+
+__global__ __launch_bounds__(64) void part_count_kernel(const uint32_t* keys, uint32_t n, uint32_t tbits,
+                                                        int nranks, uint32_t* hist) {
+  __shared__ uint32_t cnt[257];
+  const int lane = threadIdx.x;
+  const uint32_t nw = gridDim.x, w = blockIdx.x;
+  for (int d = lane; d <= nranks; d += 64) cnt[d] = 0u;
+  __syncthreads();
+  const uint32_t e0 = w * kPartChunk, e1 = e0 + kPartChunk < n ? e0 + kPartChunk : n;
+  uint32_t k[kPartSteps];  // every load in flight at once (the pass is latency-bound)
+#pragma unroll
+  for (uint32_t t = 0; t < kPartSteps; t++) {
+    const uint32_t i = e0 + t * 64u + (uint32_t)lane;
+    k[t] = i < e1 ? keys[i] >> tbits : 0xffffffffu;
   }
-  start[d] = lo;
+#pragma unroll
+  for (uint32_t t = 0; t < kPartSteps; t++)
+    if (k[t] != 0xffffffffu) atomicAdd(&cnt[k[t]], 1u);
+  __syncthreads();
+  for (int d = lane; d <= nranks; d += 64) hist[(size_t)d * nw + w] = cnt[d];
 }
 
-__global__ __launch_bounds__(256) void pack_kernel(const uint32_t* keys, const uint32_t* prims, const float* skip,
-                                                   uint32_t n, uint32_t tpr, uint32_t* out) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t prim = prims[i];
-  out[3 * (size_t)i] = keys[i] % (tpr + 1u);
-  out[3 * (size_t)i + 1] = prim;
-  out[3 * (size_t)i + 2] = __float_as_uint(skip[prim]);
+__global__ __launch_bounds__(64) void part_scatter_kernel(const uint32_t* keys, const uint32_t* prims,
+                                                          const float* skip, uint32_t n, uint32_t tbits, int nranks,
+                                                          const uint32_t* off, uint32_t* start, uint32_t* out) {
+  __shared__ uint32_t base[257];
+  const int lane = threadIdx.x;
+  const uint32_t nw = gridDim.x, w = blockIdx.x;
+  for (int d = lane; d <= nranks; d += 64) {
+    base[d] = off[(size_t)d * nw + w];
+    if (w == 0) start[d] = base[d];
+  }
+  __syncthreads();
+  const uint32_t e0 = w * kPartChunk, e1 = e0 + kPartChunk < n ? e0 + kPartChunk : n;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  uint32_t kk[kPartSteps], pr[kPartSteps];
+  float sk[kPartSteps];
+  // the chunk's keys, prims and skip bounds in flight at once (latency-bound)
+#pragma unroll
+  for (uint32_t t = 0; t < kPartSteps; t++) {
+    const uint32_t i = e0 + t * 64u + (uint32_t)lane;
+    kk[t] = i < e1 ? keys[i] : 0xffffffffu;
+    pr[t] = i < e1 ? prims[i] : 0u;
+  }
+#pragma unroll
+  for (uint32_t t = 0; t < kPartSteps; t++) sk[t] = kk[t] != 0xffffffffu ? skip[pr[t]] : 0.0f;
+#pragma unroll
+  for (uint32_t t = 0; t < kPartSteps; t++) {
+    const uint32_t i = e0 + t * 64u + (uint32_t)lane;
+    if (e0 + t * 64u >= e1) break;
+    const bool valid = i < e1;
+    const uint32_t key = kk[t];
+    const uint32_t d = key >> tbits;
+    uint64_t left = __ballot(valid);
+    uint32_t pos = 0;
+    while (left) {  // one round per distinct rank of this step's entries
+      const int first = __ffsll((long long)left) - 1;
+      const uint32_t dd = (uint32_t)__shfl((int)d, first, 64);
+      const uint64_t m = __ballot(valid && d == dd) & left;
+      // (one wave: its LDS read of base[dd] completes before its write)
+      const uint32_t b = base[dd];
+      if (valid && d == dd) pos = b + (uint32_t)__popcll(m & lt);
+      if (lane == first) base[dd] = b + (uint32_t)__popcll(m);
+      left &= ~m;
+    }
+    if (valid && d < (uint32_t)nranks) {
+      out[3 * (size_t)pos] = key & ((1u << tbits) - 1u);
+      out[3 * (size_t)pos + 1] = pr[t];
+      out[3 * (size_t)pos + 2] = __float_as_uint(sk[t]);
+    }
+  }
 }
 
 __global__ __launch_bounds__(256) void unpack_kernel(const uint32_t* in, uint32_t n, uint32_t ntiles, uint32_t tpr,
@@ -1442,16 +1511,28 @@ __global__ __launch_bounds__(256) void gather_kernel(const uint32_t* in, const u
 // perm: heavy tiles first, then the rest, each in their own order.
 // a tile is heavy when its list is longer than 8x the mean; the mean over
 // the entries with a tile (start[ntiles], read here: the host's total also
-// counts the entries the refinement dropped)
+// counts the entries the refinement dropped).
+// Also heavy (item_cost != NULL: the same frame rendered before on this
+// context): a tile one of whose items took more than a quarter of a
+// balanced wave's share of that trace (cost_sum / waves).  Long reflection
+// chains cost little camera-candidate work -- C5's worst items at N = 8 are
+// mirror paths through tiles of 30-60 entries -- and one of them started
+// late ran past every other wave: rank 0 of 8 traced in 1.23 ms against
+// 0.88-0.97 for the others with the same total clocks (tools/tile_cost.py).
 __global__ __launch_bounds__(256) void heavy_flag_kernel(const uint32_t* start, uint32_t ntiles,
-                                                         uint32_t* flags) {
+                                                         uint32_t* flags, const uint32_t* item_cost,
+                                                         const unsigned long long* cost_sum, uint32_t waves) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t > ntiles) return;
   const uint32_t total = start[ntiles] - start[0];
-  flags[t] = t < ntiles && (unsigned long long)(start[t + 1] - start[t]) * ntiles >
-                               8ull * (unsigned long long)total
-                 ? 1u
-                 : 0u;
+  bool heavy = t < ntiles && (unsigned long long)(start[t + 1] - start[t]) * ntiles > 8ull * (unsigned long long)total;
+  if (item_cost && t < ntiles && !heavy) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) m = item_cost[4 * (size_t)t + k] > m ? item_cost[4 * (size_t)t + k] : m;
+    heavy = 4.0 * (double)m * (double)waves > (double)*cost_sum;
+  }
+  flags[t] = heavy ? 1u : 0u;
 }
 
 __global__ __launch_bounds__(256) void heavy_perm_kernel(const uint32_t* flags, const uint32_t* pos,
@@ -1854,9 +1935,10 @@ extern "C" hipError_t rt_cand_scatter(const CandParams* p, hipStream_t s) {
 }
 
 extern "C" hipError_t rt_cand_count(const CandParams* p, hipStream_t s) {
-  if (p->nprim == 0) return hipSuccess;
+  const uint32_t len = p->prim1 - p->prim0;  // the list holds prims of the slice only
+  if (len == 0) return hipSuccess;
   // sized for the worst case; threads beyond the list's length exit at once
-  hipLaunchKernelGGL(rtc::count_kernel, dim3((p->nprim + RT_LIST_BLOCK - 1) / RT_LIST_BLOCK), dim3(RT_LIST_BLOCK), 0, s, *p);
+  hipLaunchKernelGGL(rtc::count_kernel, dim3((len + RT_LIST_BLOCK - 1) / RT_LIST_BLOCK), dim3(RT_LIST_BLOCK), 0, s, *p);
   return hipGetLastError();
 }
 
@@ -1867,8 +1949,9 @@ extern "C" hipError_t rt_cand_big_count(const CandParams* p, hipStream_t s) {
 }
 
 extern "C" hipError_t rt_cand_emit(const CandParams* p, hipStream_t s) {
-  if (p->nprim == 0) return hipSuccess;
-  hipLaunchKernelGGL(rtc::emit_kernel, dim3((p->nprim + RT_LIST_BLOCK - 1) / RT_LIST_BLOCK), dim3(RT_LIST_BLOCK), 0, s, *p);
+  const uint32_t len = p->prim1 - p->prim0;
+  if (len == 0) return hipSuccess;
+  hipLaunchKernelGGL(rtc::emit_kernel, dim3((len + RT_LIST_BLOCK - 1) / RT_LIST_BLOCK), dim3(RT_LIST_BLOCK), 0, s, *p);
   return hipGetLastError();
 }
 
@@ -1935,7 +2018,7 @@ extern "C" hipError_t rt_cand_scan(const uint32_t* in, uint32_t* out, uint32_t n
 }
 
 extern "C" hipError_t rt_cand_sort(uint32_t* keys_in, uint32_t* keys_out, uint32_t* vals_in,
-                                   uint32_t* vals_out, uint32_t n, int bits, void* temp,
+                                   uint32_t* vals_out, uint32_t n, int begin_bit, int end_bit, void* temp,
                                    size_t* temp_bytes, hipStream_t s) {
 #if RT_SORT_BITS
   // digits of RT_SORT_BITS bits per onesweep place (rocPRIM's gfx950 u32/u32
@@ -1944,11 +2027,11 @@ extern "C" hipError_t rt_cand_sort(uint32_t* keys_in, uint32_t* keys_out, uint32
       rocprim::default_config, rocprim::default_config,
       rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 16>, rocprim::kernel_config<1024, 16>,
                                           RT_SORT_BITS, rocprim::block_radix_rank_algorithm::match>>;
-  return rocprim::radix_sort_pairs<cfg>(temp, *temp_bytes, keys_in, keys_out, vals_in, vals_out, (size_t)n, 0,
-                                        bits, s);
+  return rocprim::radix_sort_pairs<cfg>(temp, *temp_bytes, keys_in, keys_out, vals_in, vals_out, (size_t)n,
+                                        begin_bit, end_bit, s);
 #else
   return rocprim::radix_sort_pairs(temp, *temp_bytes, keys_in, keys_out, vals_in, vals_out,
-                                   (size_t)n, 0, bits, s);
+                                   (size_t)n, begin_bit, end_bit, s);
 #endif
 }
 
@@ -1969,33 +2052,41 @@ extern "C" hipError_t rt_cand_bounds(const uint32_t* keys, uint32_t n, uint32_t*
 
 
 extern "C" hipError_t rt_cand_route(uint32_t* keys, uint32_t n, int tiles_x, int nranks, int blocks_x, int tb,
-                                    uint32_t tpr, uint32_t drop_key, hipStream_t s) {
+                                    uint32_t tbits, uint32_t drop_key, const uint32_t* total_dev, hipStream_t s) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(rtc::route_kernel, dim3((n + 255) / 256), dim3(256), 0, s, keys, n, tiles_x, nranks, blocks_x,
-                     tb, tpr, drop_key);
+                     tb, tbits, drop_key, total_dev);
   return hipGetLastError();
 }
 
 extern "C" hipError_t rt_cand_route_globals(const uint32_t* global, uint32_t nglobal, int nranks, uint32_t tpr,
-                                            uint32_t* keys, uint32_t* vals, hipStream_t s) {
+                                            uint32_t tbits, uint32_t* keys, uint32_t* vals, hipStream_t s) {
   const uint32_t n = nglobal * (uint32_t)nranks;
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(rtc::route_globals_kernel, dim3((n + 255) / 256), dim3(256), 0, s, global, nglobal, nranks,
-                     tpr, keys, vals);
+                     tpr, tbits, keys, vals);
   return hipGetLastError();
 }
 
-extern "C" hipError_t rt_cand_rank_bounds(const uint32_t* keys, uint32_t n, uint32_t tpr, int nranks,
-                                          uint32_t* start, hipStream_t s) {
-  hipLaunchKernelGGL(rtc::rank_bounds_kernel, dim3((nranks + 1 + 63) / 64), dim3(64), 0, s, keys, n, tpr, nranks,
-                     start);
+extern "C" uint32_t rt_cand_part_waves(uint32_t n) {
+  return (n + rtc::kPartChunk - 1) / rtc::kPartChunk;
+}
+
+extern "C" hipError_t rt_cand_part_count(const uint32_t* keys, uint32_t n, uint32_t tbits, int nranks,
+                                         uint32_t* hist, hipStream_t s) {
+  const uint32_t nw = rt_cand_part_waves(n);
+  if (nw == 0) return hipSuccess;
+  hipLaunchKernelGGL(rtc::part_count_kernel, dim3(nw), dim3(64), 0, s, keys, n, tbits, nranks, hist);
   return hipGetLastError();
 }
 
-extern "C" hipError_t rt_cand_pack(const uint32_t* keys, const uint32_t* prims, const float* skip, uint32_t n,
-                                   uint32_t tpr, uint32_t* out, hipStream_t s) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(rtc::pack_kernel, dim3((n + 255) / 256), dim3(256), 0, s, keys, prims, skip, n, tpr, out);
+extern "C" hipError_t rt_cand_part_scatter(const uint32_t* keys, const uint32_t* prims, const float* skip,
+                                           uint32_t n, uint32_t tbits, int nranks, const uint32_t* off,
+                                           uint32_t* start, uint32_t* out, hipStream_t s) {
+  const uint32_t nw = rt_cand_part_waves(n);
+  if (nw == 0) return hipMemsetAsync(start, 0, ((size_t)nranks + 1) * sizeof(uint32_t), s);
+  hipLaunchKernelGGL(rtc::part_scatter_kernel, dim3(nw), dim3(64), 0, s, keys, prims, skip, n, tbits, nranks, off,
+                     start, out);
   return hipGetLastError();
 }
 
@@ -2014,12 +2105,13 @@ extern "C" hipError_t rt_cand_gather(const uint32_t* in, const uint32_t* idx, ui
 }
 
 extern "C" hipError_t rt_cand_order(const uint32_t* start, uint32_t ntiles, uint32_t total,
-                                    uint32_t* flags, uint32_t* pos, uint32_t* perm, void* tmp,
+                                    uint32_t* flags, uint32_t* pos, uint32_t* perm, const uint32_t* item_cost,
+                                    const unsigned long long* cost_sum, uint32_t waves, void* tmp,
                                     size_t* tmp_bytes, hipStream_t s) {
   if (!tmp) return rt_cand_scan(flags, pos, ntiles, nullptr, tmp_bytes, s);
   const dim3 b(256), g((ntiles + 1 + 255) / 256);
   (void)total;
-  hipLaunchKernelGGL(rtc::heavy_flag_kernel, g, b, 0, s, start, ntiles, flags);
+  hipLaunchKernelGGL(rtc::heavy_flag_kernel, g, b, 0, s, start, ntiles, flags, item_cost, cost_sum, waves);
   hipError_t e = rt_cand_scan(flags, pos, ntiles, tmp, tmp_bytes, s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(rtc::heavy_perm_kernel, g, b, 0, s, flags, pos, ntiles, perm);

@@ -52,6 +52,12 @@ extern "C" {
 
 #define RT_TIMED_FRAMES 1024
 
+// the trace's work order puts the long items of the same frame's previous
+// trace first (rt_cand.hip heavy_flag_kernel); 0: entries only (A/B knob)
+#ifndef RT_COST_ORDER
+#define RT_COST_ORDER 1
+#endif
+
 // per-frame counters (one allocation, rt_hip_ctx::d_counter): 8 item-stream
 // counters 128 B apart, the stats, RT_HIT_REGIONS hit-record and as many
 // shade-chunk counters 32 words apart
@@ -60,7 +66,29 @@ static_assert(RT_NSTATS <= RT_STAT_STRIDE, "stat copies overlap");
 static constexpr size_t kStatBytes = RT_STAT_SETS * RT_STAT_STRIDE * sizeof(unsigned long long);
 static constexpr size_t kHitCounterBytes = 2 * RT_HIT_REGIONS * 32 * sizeof(uint32_t);
 static constexpr size_t kSecCounterBytes = 2 * 32 * sizeof(uint32_t);  // secondary queue: append, chunk
-static constexpr size_t kFrameCounterBytes = kItemCounterBytes + kStatBytes + kHitCounterBytes + kSecCounterBytes;
+static constexpr size_t kCostBytes = 64;  // the trace's item-clock sum (KParams::cost_sum)
+static constexpr size_t kFrameCounterBytes =
+    kItemCounterBytes + kStatBytes + kHitCounterBytes + kSecCounterBytes + kCostBytes;
+
+// The sizes of one list build, which are deterministic for its (camera
+// frame, rank, nranks): a later build of the same frame sizes its buffers and
+// launches from them instead of reading its own back (async_lists).
+struct ListShape {
+  int valid = 0;
+  rt_frame frame{};
+  int rank = -1, nranks = 0;
+  uint32_t total = 0, nglobal = 0;           // entries, global prims
+  uint32_t nbig = 0, nitems = 0, over = 0;   // the big-emission launch shape
+  bool same(const rt_frame* f, int r, int n) const {
+    return valid && rank == r && nranks == n && std::memcmp(&frame, f, sizeof *f) == 0;
+  }
+  void set(const rt_frame* f, int r, int n) {
+    valid = 1;
+    frame = *f;
+    rank = r;
+    nranks = n;
+  }
+};
 
 struct rt_hip_ctx {
   int device = 0;
@@ -179,26 +207,31 @@ struct rt_hip_ctx {
   size_t cand_cap = 0, cand_tiles_cap = 0, order_cap = 0;
   void* d_scan_tmp = nullptr;
   size_t scan_tmp_bytes = 0;
-  uint32_t* h_cand = nullptr;  // pinned: total entries, risky, global, visits; [6..7] the last
-                               // asynchronous build's total and overflow flag (ctr[6..7])
+  uint32_t* h_cand = nullptr;  // pinned: a read-back build's ctr[0..7] (rt_cand.h CandParams::ctr)
   // asynchronous per-rank builds (no host read-back in the render path): the
   // entry buffers are sized from an earlier frame's total, read back without
   // waiting when its build has finished
   int async_lists = RT_ASYNC_LISTS_DEFAULT;
   // the frame (camera frame, rank, nranks) whose per-rank lists were last
-  // built with a read-back, and their entry total: the same frame's lists
-  // are deterministic, so they are rebuilt without reading the total back
-  int known_valid = 0;
-  rt_frame known_frame{};
-  int known_rank = -1, known_nranks = 0;
-  uint32_t known_total = 0;
-  uint32_t known_nbig = 0, known_nitems = 0, known_over = 0;  // its big-emission launch shape
+  // built with a read-back, and their sizes: the same frame's lists are
+  // deterministic, so they are rebuilt without reading the total back
+  ListShape known;
+  ListShape pknown;  // the same for the last read-back produce (rt_hip_cand_produce)
+  // the frame (camera frame, rank, nranks) whose trace last recorded its
+  // per-item clocks (d_item_cost, their sum in the frame counters) and its
+  // grid: the same frame's next work order puts its long items first
+  ListShape cost_hist;
+  uint32_t cost_waves = 0;
+  uint32_t* d_item_cost = nullptr;  // 4 x ntiles_local
+  size_t item_cost_cap = 0;
   int last_async = 0;                 // the last render's lists came from an asynchronous build
   unsigned long long cand_prims = 0, cand_entries = 0, cand_global = 0;
   // triangle-parallel lists (rt_hip_cand_produce / rt_hip_cand_consume)
   uint32_t* d_send = nullptr;   // 3 words per routed entry, destination-rank order
   size_t send_cap = 0;          // words
   uint32_t send_n = 0;          // entries of the last produce
+  uint32_t* d_part = nullptr;    // the partition's per-wave rank counts and their scan
+  size_t part_cap = 0;          // words
   uint32_t* d_rstart = nullptr;  // nranks + 1 first entries per destination
   uint32_t* h_rstart = nullptr;  // pinned copy
   size_t rstart_cap = 0;
@@ -365,6 +398,8 @@ extern "C" void rt_hip_destroy(rt_hip_ctx* c) {
   if (c->h_cand) (void)hipHostFree(c->h_cand);
   (void)hipFree(c->d_send);
   (void)hipFree(c->d_rstart);
+  (void)hipFree(c->d_part);
+  (void)hipFree(c->d_item_cost);
   if (c->h_rstart) (void)hipHostFree(c->h_rstart);
   for (auto& f : c->ev)
     for (hipEvent_t e : f)
@@ -806,12 +841,14 @@ extern "C" int rt_hip_set_cull_slack(rt_hip_ctx* c, float ulps) {
   if (!c || !(ulps >= 0.0f)) return rt_set_error(RT_EINVAL, "bad slack");
   c->eps_ulps = ulps;
   c->cam_eps_ulps = ulps;
+  c->known.valid = c->pknown.valid = 0;  // the lists change
   return RT_OK;
 }
 
 extern "C" int rt_hip_set_camera_slack(rt_hip_ctx* c, float ulps) {
   if (!c || !(ulps >= 0.0f)) return rt_set_error(RT_EINVAL, "bad slack");
   c->cam_eps_ulps = ulps;
+  c->known.valid = c->pknown.valid = 0;  // the lists change
   return RT_OK;
 }
 
@@ -844,12 +881,14 @@ extern "C" int rt_hip_set_policy(rt_hip_ctx* c, int policy) {
 extern "C" int rt_hip_set_camera_refine(rt_hip_ctx* c, int enable) {
   if (!c) return rt_set_error(RT_EINVAL, "null context");
   c->cand_refine = enable ? 1 : 0;
+  c->known.valid = c->pknown.valid = 0;  // the lists change
   return RT_OK;
 }
 
 extern "C" int rt_hip_set_camera_bound_scale(rt_hip_ctx* c, double scale) {
   if (!c || !(scale > 0.0)) return rt_set_error(RT_EINVAL, "bad bound scale");
   c->bound_scale = scale;
+  c->known.valid = c->pknown.valid = 0;  // the lists change
   return RT_OK;
 }
 
@@ -1139,7 +1178,14 @@ static constexpr uint32_t kItemCap = RT_CAND_ITEM_CAP;
 extern "C" int rt_hip_set_cand_item_cap(rt_hip_ctx* c, unsigned cap) {
   if (!c) return rt_set_error(RT_EINVAL, "null context");
   c->cand_item_cap = cap;
+  c->known.valid = c->pknown.valid = 0;  // the lists change
   return RT_OK;
+}
+
+// the trace's item-clock sum in the frame counters (KParams::cost_sum)
+static unsigned long long* cost_sum_of(rt_hip_ctx* c) {
+  return (unsigned long long*)((char*)c->d_counter + kItemCounterBytes + kStatBytes + kHitCounterBytes +
+                               kSecCounterBytes);
 }
 
 // Frame constants of the candidate lists for rank/nranks (no device work).
@@ -1327,16 +1373,23 @@ static int cand_tile_buffers(rt_hip_ctx* c, size_t nt) {
 
 // The longest-first work order of the nt tiles from their offsets, and the
 // lists' kernel parameters common to both builds.
-static int cand_order(rt_hip_ctx* c, KParams* kp, size_t nt, uint32_t total, hipStream_t s) {
+static int cand_order(rt_hip_ctx* c, KParams* kp, size_t nt, uint32_t total, hipStream_t s, const rt_frame* f,
+                      int rank, int nranks) {
   size_t tb = 0;
+  // the item clocks of this frame's last trace on this context (its counters
+  // are zeroed only by the render that follows this order)
+  const bool hist = c->cost_hist.same(f, rank, nranks) && c->d_item_cost && c->item_cost_cap >= 4 * nt;
+  const uint32_t* ic = hist ? c->d_item_cost : nullptr;
+  const unsigned long long* cs = hist ? cost_sum_of(c) : nullptr;
   HIP_TRY(rt_cand_order(c->d_cand_start, (uint32_t)nt, total, c->d_order, c->d_order + nt + 1,
-                        c->d_order + 2 * (nt + 1), nullptr, &tb, s));
+                        c->d_order + 2 * (nt + 1), ic, cs, c->cost_waves, nullptr, &tb, s));
   int rc = ensure_tmp(c, tb);
   if (rc) return rc;
   tb = c->scan_tmp_bytes;
   HIP_TRY(rt_cand_order(c->d_cand_start, (uint32_t)nt, total, c->d_order, c->d_order + nt + 1,
-                        c->d_order + 2 * (nt + 1), c->d_scan_tmp, &tb, s));
+                        c->d_order + 2 * (nt + 1), ic, cs, c->cost_waves, c->d_scan_tmp, &tb, s));
   kp->tile_order = c->d_order + 2 * (nt + 1);
+  kp->n_heavy = c->d_order + (nt + 1) + nt;  // the scan of the heavy flags: its total
   kp->cand_start = c->d_cand_start;
   kp->tri_prim = c->d_tri_prim;
   return RT_OK;
@@ -1356,8 +1409,22 @@ static int key_bits(size_t n_keys) {
 // only host sync) -> emit.  The entry buffers are sized for total +
 // glob_copies x globals (the triangle-parallel build routes each global to
 // every rank).  No contended atomics; deterministic.
+// Entries per big emission item for a build of 1/split of a frame's work (a
+// rank's lists of an N-rank frame, a producer's slice of N): 1024 for a whole
+// frame, halved per doubling of split down to 128, so the items stay many
+// enough to overlap (rt_cand.hip).  RT_CAND_CHUNK_SHIFT: A/B knob.
+static uint32_t cand_chunk_shift(uint32_t split) {
+  if (const char* e = std::getenv("RT_CAND_CHUNK_SHIFT")) {
+    const int v = std::atoi(e);
+    if (v >= 6 && v <= 14) return (uint32_t)v;
+  }
+  uint32_t sh = 10;
+  for (uint32_t q = split; q > 1 && sh > 7; q >>= 1) sh--;
+  return sh;
+}
+
 static int cand_build(rt_hip_ctx* c, CandParams& cp, hipStream_t s, uint32_t glob_copies, uint32_t* total_out,
-                      uint32_t* nglobal_out, bool async = false) {
+                      uint32_t* nglobal_out, const ListShape* known = nullptr, ListShape* shape = nullptr) {
   int rc = RT_OK;
   // every build overwrites the entry, offset and order buffers: lists that
   // rt_hip_cand_consume left for a render (ext) are gone from here on, so
@@ -1421,6 +1488,7 @@ static int cand_build(rt_hip_ctx* c, CandParams& cp, hipStream_t s, uint32_t glo
   cp.big_cap = kBigLaneCap;
   cp.items = c->d_cand_items;
   cp.item_cap = c->cand_item_cap < kItemCap ? c->cand_item_cap : kItemCap;
+  cp.chunk_shift = cand_chunk_shift(glob_copies ? glob_copies : (uint32_t)cp.nranks);
   cp.wave_items = c->d_cand_wave_items;
   cp.wave_base = c->d_cand_wave_base;
   cp.refine = c->cand_refine ? 1u : 0u;
@@ -1459,43 +1527,46 @@ static int cand_build(rt_hip_ctx* c, CandParams& cp, hipStream_t s, uint32_t glo
   // over the list's length only (ctr[3], on the device); the entry total -> ctr[6]
   HIP_TRY(rt_cand_scan_dev(c->d_cand_visits, c->d_cand_off, (uint32_t)np, c->d_cand_ctr + 3, c->d_cand_ctr + 6,
                            c->d_scan_bsum, s));
-  if (async) {
+  if (known) {
     // no read-back: the frame's lists were built before with a read-back of
-    // their total (known_total: deterministic for the same frame), so the
-    // buffers hold them; an entry past known_total would not be written and
-    // would set ctr[7] (rt_hip_stats then reports the frame: never silent).
-    // The emission kernels read the item count and the over-cap flag on the
-    // device and the render reads the global prims' count there
-    rc = cand_entry_buffers(c, c->known_total);
+    // their sizes (deterministic for the same frame), so the buffers hold
+    // them; an entry past known->total would not be written and would set
+    // ctr[7] (rt_hip_stats then reports the frame, rt_hip_cand_produce
+    // builds again: never silent).  The emission kernels read the item
+    // count and the over-cap flag on the device and the render reads the
+    // global prims' count there
+    rc = cand_entry_buffers(c, (size_t)known->total + (size_t)glob_copies * known->nglobal);
     if (rc) return rc;
     cp.keys = c->d_cand_keys;
     cp.vals = c->d_cand_vals;
-    cp.key_cap = c->known_total;
+    cp.key_cap = known->total;
     HIP_TRY(rt_cand_emit(&cp, s));
     // the same launch shape as the read-back build (the kernels read the
     // counts on the device and loop over whatever they find)
-    if (c->known_over)
-      HIP_TRY(rt_cand_big(&cp, c->known_nbig, s));
+    if (known->over)
+      HIP_TRY(rt_cand_big(&cp, known->nbig, s));
     else
-      HIP_TRY(rt_cand_big_items(&cp, c->known_nitems, 1, s));
-    HIP_TRY(rt_cand_fill_tail(c->d_cand_keys, c->d_cand_ctr + 6, c->known_total, cp.drop_key, s));
+      HIP_TRY(rt_cand_big_items(&cp, known->nitems, 1, s));
+    // (a produce's route_kernel drops the unused tail itself)
+    if (!glob_copies) HIP_TRY(rt_cand_fill_tail(c->d_cand_keys, c->d_cand_ctr + 6, known->total, cp.drop_key, s));
     // this frame's counters for rt_hip_stats, in stream order, where no build writes
-    HIP_TRY(hipMemcpyAsync(c->d_cand_ctr + 16, c->d_cand_ctr, 8 * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
-    *total_out = c->known_total;  // the sort's length
-    *nglobal_out = 0;             // on the device (ctr[1])
+    if (!glob_copies) HIP_TRY(hipMemcpyAsync(c->d_cand_ctr + 16, c->d_cand_ctr, 8 * sizeof(uint32_t),
+                                             hipMemcpyDeviceToDevice, s));
+    *total_out = known->total;  // the sort's length
+    *nglobal_out = known->nglobal;  // (the render reads the count on the device, ctr[1])
     return RT_OK;
   }
-  HIP_TRY(hipMemcpyAsync(c->h_cand, c->d_cand_ctr + 6, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  // one read-back of the build's sizes: ctr[1..6] (the total in [6], the
+  // items in [4])
+  HIP_TRY(hipMemcpyAsync(c->h_cand, c->d_cand_ctr, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
 #else
   tb = c->scan_tmp_bytes;
   HIP_TRY(rt_cand_scan(c->d_cand_visits, c->d_cand_off, (uint32_t)np, c->d_scan_tmp, &tb, s));
-  HIP_TRY(hipMemcpyAsync(c->h_cand, c->d_cand_off + np, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(c->h_cand, c->d_cand_ctr, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(c->h_cand + 6, c->d_cand_off + np, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
 #endif
-  HIP_TRY(hipMemcpyAsync(c->h_cand + 1, c->d_cand_ctr + 1, 5 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(c->h_cand + 4, c->d_cand_wave_base + rt_cand_big_waves(), sizeof(uint32_t),
-                         hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
-  const uint32_t total = c->h_cand[0], nglobal = c->h_cand[1], nbig = c->h_cand[2];
+  const uint32_t total = c->h_cand[6], nglobal = c->h_cand[1], nbig = c->h_cand[2];
   const uint32_t nitems = c->h_cand[4], items_over = c->h_cand[5];
   rc = cand_entry_buffers(c, (size_t)total + (size_t)glob_copies * nglobal);
   if (rc) return rc;
@@ -1507,25 +1578,30 @@ static int cand_build(rt_hip_ctx* c, CandParams& cp, hipStream_t s, uint32_t glo
     HIP_TRY(rt_cand_big(&cp, nbig, s));
   else
     HIP_TRY(rt_cand_big_items(&cp, nitems, 0, s));
-  c->known_nbig = nbig;
-  c->known_nitems = nitems;
-  c->known_over = items_over;
+  if (shape) {
+    shape->total = total;
+    shape->nglobal = nglobal;
+    shape->nbig = nbig;
+    shape->nitems = nitems;
+    shape->over = items_over;
+  }
   *total_out = total;
   *nglobal_out = nglobal;
   return RT_OK;
 }
 
-// Sorts n (key < n_keys, value) pairs keys/vals -> keys2/vals2 (rocPRIM radix
-// sort, temporary storage in d_scan_tmp).
+// Sorts n (key < n_keys, value) pairs keys/vals -> keys2/vals2 on the key
+// bits from begin_bit up (rocPRIM radix sort, stable, temporary storage in
+// d_scan_tmp).
 static int cand_sort(rt_hip_ctx* c, uint32_t* keys, uint32_t* keys2, uint32_t* vals, uint32_t* vals2, uint32_t n,
-                     size_t n_keys, hipStream_t s) {
+                     size_t n_keys, hipStream_t s, int begin_bit = 0) {
   const int bits = key_bits(n_keys);
   size_t tb = 0;
-  HIP_TRY(rt_cand_sort(keys, keys2, vals, vals2, n, bits, nullptr, &tb, s));
+  HIP_TRY(rt_cand_sort(keys, keys2, vals, vals2, n, begin_bit, bits, nullptr, &tb, s));
   int rc = ensure_tmp(c, tb);
   if (rc) return rc;
   tb = c->scan_tmp_bytes;
-  if (n) HIP_TRY(rt_cand_sort(keys, keys2, vals, vals2, n, bits, c->d_scan_tmp, &tb, s));
+  if (n) HIP_TRY(rt_cand_sort(keys, keys2, vals, vals2, n, begin_bit, bits, c->d_scan_tmp, &tb, s));
   return RT_OK;
 }
 
@@ -1544,20 +1620,16 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
   // asynchronous for a frame whose lists were built before (a new camera
   // frame, rank split or the compatibility mode's lists read their total
   // back once; so does cand_verify's rebuild, which keeps every footprint)
-  const bool async = RT_DEV_SCAN && c->async_lists && c->known_valid && !c->cand_store_fp && !compat &&
-                     c->known_rank == kp->rank && c->known_nranks == kp->nranks &&
-                     std::memcmp(&c->known_frame, f, sizeof *f) == 0;
-  rc = cand_build(c, cp, s, 0, &total, &nglobal, async);
+  const bool async = RT_DEV_SCAN && c->async_lists && !c->cand_store_fp && !compat &&
+                     c->known.same(f, kp->rank, kp->nranks);
+  rc = cand_build(c, cp, s, 0, &total, &nglobal, async ? &c->known : nullptr, async ? nullptr : &c->known);
   if (rc) return rc;
   c->last_async = async ? 1 : 0;
-  if (!async && !compat) {  // the total just read back sizes this frame's later builds
-    c->known_valid = 1;
-    c->known_frame = *f;
-    c->known_rank = kp->rank;
-    c->known_nranks = kp->nranks;
-    c->known_total = total;
+  if (async) nglobal = 0;  // on the device (ctr[1])
+  if (!async && !compat) {  // the sizes just read back size this frame's later builds
+    c->known.set(f, kp->rank, kp->nranks);
   } else if (!async) {
-    c->known_valid = 0;
+    c->known.valid = 0;
   }
   rc = cand_tile_buffers(c, nt);
   if (rc) return rc;
@@ -1570,7 +1642,7 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
   float* entry_skip = (float*)c->d_cand_keys2;
   HIP_TRY(rt_cand_entry_skip(c->d_cand, c->d_cand_skip, entry_skip, total, c->d_cand_start + nt, s));
   // longest-first work order of the rank's tiles (heavy lists first)
-  rc = cand_order(c, kp, nt, total, s);
+  rc = cand_order(c, kp, nt, total, s, f, kp->rank, kp->nranks);
   if (rc) return rc;
   kp->cand = c->d_cand;
   kp->cand_global = c->d_cand_global;
@@ -1602,22 +1674,42 @@ extern "C" int rt_hip_cand_produce(rt_hip_ctx* c, const rt_frame* f, int rank, i
   int rc = cand_params(f, c->scene_c, c->scene_r, c->cam_eps_ulps, c->bound_scale, 0, 1, &cp, 0);
   if (rc) return rc;
   const uint64_t np = c->nprim;
-  cp.prim0 = (uint32_t)(np * (uint64_t)rank / (uint64_t)nranks);
-  cp.prim1 = (uint32_t)(np * (uint64_t)(rank + 1) / (uint64_t)nranks);
+  // this producer's slice: the blocks of RT_SLICE_BLOCK prims b = rank mod
+  // nranks (prims near each other in the scene -- one sphere, one region --
+  // are near each other in prim order: contiguous slices loaded the producer
+  // of the nearest objects ~20 % above the mean on C5, blocks spread it)
+  const uint64_t nb = (np + RT_SLICE_BLOCK - 1) / RT_SLICE_BLOCK;
+  uint64_t len = 0;
+  for (uint64_t b = (uint64_t)rank; b < nb; b += (uint64_t)nranks)
+    len += std::min<uint64_t>(RT_SLICE_BLOCK, np - b * RT_SLICE_BLOCK);
+  cp.prim0 = 0;
+  cp.prim1 = (uint32_t)len;
+  cp.sl_stride = (uint32_t)nranks;
+  cp.sl_rank = (uint32_t)rank;
+  // a slice produced before for this frame is built without the mid-build
+  // read-back (its sizes are deterministic); the read-back of the counts at
+  // the end checks them, and a mismatch -- never expected -- builds again
+  const bool async = RT_DEV_SCAN && c->async_lists && !c->cand_store_fp && c->pknown.same(f, rank, nranks);
   uint32_t total = 0, nglobal = 0;
-  rc = cand_build(c, cp, s, (uint32_t)nranks, &total, &nglobal);
+  rc = cand_build(c, cp, s, (uint32_t)nranks, &total, &nglobal, async ? &c->pknown : nullptr,
+                  async ? nullptr : &c->pknown);
   if (rc) return rc;
+  if (!async) c->pknown.set(f, rank, nranks);
   const uint32_t tpr = (uint32_t)rt_hip_tiles_per_rank(f->width, f->height, nranks);
   const int tb = rt_block_side(nranks);
-  HIP_TRY(rt_cand_route(c->d_cand_keys, total, cp.tiles_x, nranks, rt_blocks_x(cp.tiles_x, tb), tb, tpr, cp.drop_key,
-                        s));
-  HIP_TRY(rt_cand_route_globals(c->d_cand_global, nglobal, nranks, tpr, c->d_cand_keys + total,
+  // key = rank << tbits | local tile (tpr: a global), rank nranks for an
+  // entry the refinement dropped (or, in an asynchronous build, past the
+  // build's own total); then a stable partition by rank: each rank's entries
+  // keep their emission order, which the consumer's stable sort by tile
+  // turns into the per-tile order of the rank's own build
+  const int tbits = key_bits((size_t)tpr + 1);
+  if (nranks > 256 || tbits + key_bits((size_t)nranks + 1) > 32)
+    return rt_set_error(RT_EINVAL, "%d ranks x %u tiles per rank: routed keys exceed 32 bits", nranks, tpr);
+  HIP_TRY(rt_cand_route(c->d_cand_keys, total, cp.tiles_x, nranks, rt_blocks_x(cp.tiles_x, tb), tb, (uint32_t)tbits,
+                        cp.drop_key, async ? c->d_cand_ctr + 6 : nullptr, s));
+  HIP_TRY(rt_cand_route_globals(c->d_cand_global, nglobal, nranks, tpr, (uint32_t)tbits, c->d_cand_keys + total,
                                 c->d_cand_vals + total, s));
   const uint32_t n = total + nglobal * (uint32_t)nranks;
-  // keys < nranks (tpr + 1), or that for an entry the refinement dropped
-  rc = cand_sort(c, c->d_cand_keys, c->d_cand_keys2, c->d_cand_vals, c->d_cand, n,
-                 (size_t)nranks * (tpr + 1) + 1, s);
-  if (rc) return rc;
   if ((size_t)nranks + 1 > c->rstart_cap) {
     (void)hipFree(c->d_rstart);
     (void)hipHostFree(c->h_rstart);
@@ -1636,11 +1728,39 @@ extern "C" int rt_hip_cand_produce(rt_hip_ctx* c, const rt_frame* f, int rank, i
     HIP_TRY(hipMalloc((void**)&c->d_send, cap * sizeof(uint32_t)));
     c->send_cap = cap;
   }
-  HIP_TRY(rt_cand_rank_bounds(c->d_cand_keys2, n, tpr, nranks, c->d_rstart, s));
-  HIP_TRY(rt_cand_pack(c->d_cand_keys2, c->d_cand, c->d_cand_skip, n, tpr, c->d_send, s));
+  // per-wave rank counts (rank-major) -> exclusive scan -> stable scatter
+  const size_t nh = ((size_t)nranks + 1) * rt_cand_part_waves(n);
+  if (2 * nh + 2 > c->part_cap) {
+    (void)hipFree(c->d_part);
+    c->d_part = nullptr;
+    c->part_cap = 0;
+    const size_t cap = 2 * (nh + nh / 4) + 1024;
+    HIP_TRY(hipMalloc((void**)&c->d_part, cap * sizeof(uint32_t)));
+    c->part_cap = cap;
+  }
+  uint32_t* hist = c->d_part;
+  uint32_t* hoff = c->d_part + nh + 1;
+  if (nh) {
+    size_t tmpb = 0;
+    HIP_TRY(rt_cand_scan(hist, hoff, (uint32_t)(nh - 1), nullptr, &tmpb, s));
+    rc = ensure_tmp(c, tmpb);
+    if (rc) return rc;
+    tmpb = c->scan_tmp_bytes;
+    HIP_TRY(rt_cand_part_count(c->d_cand_keys, n, (uint32_t)tbits, nranks, hist, s));
+    HIP_TRY(rt_cand_scan(hist, hoff, (uint32_t)(nh - 1), c->d_scan_tmp, &tmpb, s));
+  }
+  HIP_TRY(rt_cand_part_scatter(c->d_cand_keys, c->d_cand_vals, c->d_cand_skip, n, (uint32_t)tbits, nranks, hoff,
+                               c->d_rstart, c->d_send, s));
   HIP_TRY(hipMemcpyAsync(c->h_rstart, c->d_rstart, ((size_t)nranks + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost,
                          s));
+  if (async) HIP_TRY(hipMemcpyAsync(c->h_cand, c->d_cand_ctr, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  if (async && (c->h_cand[7] || c->h_cand[6] != c->pknown.total || c->h_cand[1] != c->pknown.nglobal ||
+                c->h_cand[2] != c->pknown.nbig || c->h_cand[4] != c->pknown.nitems ||
+                c->h_cand[5] != c->pknown.over)) {
+    c->pknown.valid = 0;  // not this slice's sizes after all: build it with the read-back
+    return rt_hip_cand_produce(c, f, rank, nranks, counts, nglobal_out, stream);
+  }
   for (int d = 0; d < nranks; d++) counts[d] = c->h_rstart[d + 1] - c->h_rstart[d];
   *nglobal_out = nglobal;
   c->send_n = c->h_rstart[nranks];  // the routed entries (the refinement's dropped ones sort after them)
@@ -1685,7 +1805,7 @@ extern "C" int rt_hip_cand_consume(rt_hip_ctx* c, const rt_frame* f, int rank, i
   HIP_TRY(rt_cand_gather(in, c->d_cand, (uint32_t)n, c->d_cand_vals, (float*)c->d_cand_keys, s));
   KParams kp;
   std::memset(&kp, 0, sizeof kp);
-  rc = cand_order(c, &kp, nt, total, s);
+  rc = cand_order(c, &kp, nt, total, s, f, rank, nranks);
   if (rc) return rc;
   c->ext = kp;
   c->ext.cand = c->d_cand_vals;
@@ -1804,6 +1924,7 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
     hipEvent_t* ev = c->ev[c->frames % RT_TIMED_FRAMES];
     if (c->timing) HIP_TRY(hipEventRecord(ev[0], s));
     HIP_TRY(hipMemsetAsync(c->d_counter, 0, kFrameCounterBytes, s));
+    c->cost_hist.valid = 0;  // (the counters hold no trace's clocks now)
     if (c->timing) {
       for (int k = 1; k < 5; k++) HIP_TRY(hipEventRecord(ev[k], s));
       c->frames++;
@@ -1887,6 +2008,7 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
       p.n_cand_global = c->ext.n_cand_global;
       p.cand_skip = c->ext.cand_skip;
       p.tile_order = c->ext.tile_order;
+      p.n_heavy = c->ext.n_heavy;
       p.tri_prim = c->ext.tri_prim;
       c->cand_entries = c->ext_total;
       c->d_cand_valid = nullptr;
@@ -1930,9 +2052,30 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
     return rt_set_error(RT_EHIP, "render: prim-order records missing");
   if (!p.hit || !p.last || !p.out || (p.nrec && (!p.tri || !p.nrm)))
     return rt_set_error(RT_EHIP, "render: device buffers missing");
+  // item clocks for the same frame's next work order (only the candidate
+  // lists' order uses them)
+  if (p.tile_order && RT_COST_ORDER) {
+    const size_t items = 4 * (size_t)p.ntiles_local;
+    if (items > c->item_cost_cap) {
+      (void)hipFree(c->d_item_cost);
+      c->d_item_cost = nullptr;
+      c->item_cost_cap = 0;
+      c->cost_hist.valid = 0;
+      HIP_TRY(hipMalloc((void**)&c->d_item_cost, items * sizeof(uint32_t)));
+      c->item_cost_cap = items;
+    }
+    p.item_cost = c->d_item_cost;
+    p.cost_sum = cost_sum_of(c);
+  }
   HIP_TRY(hipMemsetAsync(c->d_counter, 0, kFrameCounterBytes, s));  // item streams, stats, record counters
   if (c->timing) HIP_TRY(hipEventRecord(ev[1], s));
   HIP_TRY(rt_launch_trace(&p, dacc, c->count_work, pol, gt, s));
+  if (p.item_cost) {
+    c->cost_hist.set(f, rank, nranks);
+    c->cost_waves = (uint32_t)gt;
+  } else {
+    c->cost_hist.valid = 0;
+  }
   if (c->timing) HIP_TRY(hipEventRecord(ev[2], s));
   HIP_TRY(rt_launch_shade(&p, dacc, c->count_work, spol, gs, s));
   HIP_TRY(rt_launch_shade_fixup(&p, c->nprim, s));
@@ -2170,9 +2313,9 @@ extern "C" int rt_hip_stats(rt_hip_ctx* c, rt_stats* out) {
     c->last_async = 0;
     c->cand_global = actr[1];
     if (actr[7]) {  // never expected (the same frame's lists): reported, and the next build reads back
-      c->known_valid = 0;
+      c->known.valid = 0;
       return rt_set_error(RT_EHITBUF, "%u candidate-list entries, %u expected: render again", actr[6],
-                          c->known_total);
+                          c->known.total);
     }
   }
   for (int k = 0; k < RT_NSTATS; k++) {  // the copies of each counter (RT_STAT_SETS)
@@ -2378,6 +2521,7 @@ extern "C" int rt_hip_render_compat(rt_hip_ctx* c, const rt_camera* cam, unsigne
       return rc;
     }
   }
+  c->cost_hist.valid = 0;  // the counters are the compat render's
   if (hipMemsetAsync(c->d_counter, 0, kFrameCounterBytes, s) != hipSuccess ||
       rt_launch_compat(&p, accel, c->grid, s) != hipSuccess ||
       rt_launch_downscale(d_hi, d_lo, cam->width, cam->height, s) != hipSuccess ||

@@ -157,6 +157,14 @@ struct KParams {
   const float4* tri_prim;       // prim-order triangle records
   const float* cand_skip;       // per cand entry: lower bound of new_dist - |pos - o| (depth skip)
   const uint32_t* tile_order;   // trace_kernel's work order: position -> rank-local tile (NULL: identity)
+  // the trace's per-item cost (shader clocks of each (tile, sample) item,
+  // saturated to 32 bits) and their sum (zeroed before launch), for the next
+  // frame's work order (rt_cand_order); NULL: not recorded
+  uint32_t* item_cost;
+  unsigned long long* cost_sum;
+  // the heavy tiles at the front of tile_order (rt_cand_order's count, on
+  // the device; NULL: none): their items run at raised wave priority
+  const uint32_t* n_heavy;
   // secondary-ray queue (NULL: camera waves follow their paths to the end):
   // trace_kernel appends each camera path that goes on as {o.xyz, coef},
   // {d.xyz, deepest record} plus its (item, lane) slot of last[];

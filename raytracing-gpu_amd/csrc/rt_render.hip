@@ -1255,6 +1255,9 @@ static constexpr int kPacketMin = 8;
 // longest items of an 8-way split (reflection-heavy tiles, tools/tile_cost.py)
 // finish sooner -- slowest of 8 ranks 3.13 -> 2.95 ms, C5 at N = 1 10.07 ->
 // 10.04 ms (profiles/r05s_packet_depth/; round 2 measured 0 and 1 equal at N = 1)
+#ifndef RT_HEAVY_PRIO
+#define RT_HEAVY_PRIO 1
+#endif
 #ifndef RT_PACKET_MAX_DEPTH
 #define RT_PACKET_MAX_DEPTH 0
 #endif
@@ -1926,6 +1929,11 @@ __global__ __launch_bounds__(64, RT_TRACE_MIN_WAVES) void trace_kernel(KParams p
   const uint32_t home = (uint32_t)blockIdx.x & 7u;
   uint32_t probe = 0;
   bool first = true;
+  unsigned long long wave_cost = 0;  // lane 0: this wave's item clocks (p.item_cost)
+  // Items of the heavy tiles (the front of the work order) run at raised
+  // wave priority: with 5 waves per SIMD a long mirror path otherwise shares
+  // its SIMD's issue slots to the end and becomes the rank's critical path.
+  const uint32_t n_heavy = p.n_heavy ? uni(*p.n_heavy) : 0u;
   for (;;) {
     const uint32_t x = (home + probe) & 7u;
     const uint32_t nx = nt > x ? (nt - x + 7u) / 8u : 0u;  // tiles of stream x
@@ -1946,7 +1954,9 @@ __global__ __launch_bounds__(64, RT_TRACE_MIN_WAVES) void trace_kernel(KParams p
     }
     const uint32_t pos = 8u * (q >> 2) + x;  // the tile's place in the work order
     const uint32_t u = 4u * (p.tile_order ? p.tile_order[pos] : pos) + (q & 3u);  // item 4t + s
-    const unsigned long long c0 = COUNT ? __builtin_readcyclecounter() : 0ull;
+    const bool prio = RT_HEAVY_PRIO && pos < n_heavy;
+    if (prio) __builtin_amdgcn_s_setprio(3);
+    const unsigned long long c0 = (COUNT || p.item_cost) ? __builtin_readcyclecounter() : 0ull;
     const uint32_t ph0[3] = {wc.cy_cam, wc.cy_cand, wc.cy_sec};
     wc.sec_lane_nodes = wc.sec_lane_tris = 0;
     const uint32_t t = u >> 2;
@@ -1957,6 +1967,12 @@ __global__ __launch_bounds__(64, RT_TRACE_MIN_WAVES) void trace_kernel(KParams p
     p.last[(size_t)u * 64 + lane] =
         trace_path<ACCEL, COUNT, POL>(p, valid, point, dir, x, stk, w, wc, t, 0, 1.0f, RT_NO_REC,
                                       u * 64u + (uint32_t)lane);
+    if (prio) __builtin_amdgcn_s_setprio(0);
+    if (p.item_cost && lane == 0) {  // the next frame's work order (rt_cand_order)
+      const unsigned long long cy = __builtin_readcyclecounter() - c0;
+      p.item_cost[u] = cy < 0xffffffffull ? (uint32_t)cy : 0xffffffffu;
+      wave_cost += cy;
+    }
     if (COUNT && p.tile_cycles && lane == 0) {
       // [0] the item's clocks, [1..3] its phase clocks (camera walk, camera
       // candidates, secondary walks), planes of 4 * ntiles_local items
@@ -1969,6 +1985,7 @@ __global__ __launch_bounds__(64, RT_TRACE_MIN_WAVES) void trace_kernel(KParams p
       p.tile_cycles[u + 5 * items] = wc.sec_lane_tris;
     }
   }
+  if (p.cost_sum && lane == 0 && wave_cost) atomicAdd(p.cost_sum, wave_cost);
   flush_counts(p, wc, lane);
 }
 

@@ -580,6 +580,37 @@ def test_cand_exchange_local_matches_per_rank(gpu, nranks):
         gpu.cand_exchange_local([], f)
 
 
+def test_produce_repeated_slice_is_identical(gpu):
+    """A slice produced before for the same frame (the last produce of the
+    context: each GPU produces its own rank's slice every frame) is rebuilt
+    without the mid-build read-back (its sizes are known): the routed entries
+    and the per-rank counts equal the read-back build's bit for bit."""
+    import ctypes as C
+    L = gpu_lib()
+    s = gpu.Scene.synthetic(6, 6, 9776, seed=0x5EED, width=960, height=540)
+    f = s.frame()
+    ctx = gpu.Context(s, "octree_gpu")
+    nranks = 4
+
+    def produce(r):
+        counts, ng = ctx.cand_produce(f, r, nranks)
+        ptr, n = ctx.cand_send_buffer()
+        host = np.empty((max(n, 1), 3), np.uint32)
+        if n:
+            assert L.rt_hip_memcpy_d2h(host.ctypes.data_as(C.c_void_p), C.c_void_p(ptr), n * 12) == 0
+        return host[:n].copy(), counts, ng
+
+    for r in range(nranks):
+        h0, c0, g0 = produce(r)  # read-back build
+        for _ in range(2):       # known sizes
+            h1, c1, g1 = produce(r)
+            assert (c0, g0) == (c1, g1), r
+            assert np.array_equal(h0, h1), r
+    total = sum(produce(0)[1])
+    ctx.set_camera_bound_scale(1.5)  # other lists: read back again
+    assert sum(produce(0)[1]) >= total
+
+
 def test_consumed_lists_invalidated_by_a_later_build(gpu):
     """lists rt_hip_cand_consume leaves for a render live in the
     context's shared list buffers.  A produce (e.g. the next frame's) between

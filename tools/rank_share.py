@@ -75,6 +75,7 @@ def main():
     ap.add_argument("--nranks", type=int, nargs="+", default=[1, 2, 4, 8])
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--all-ranks", action="store_true", help="every rank, not just the first and last")
+    ap.add_argument("--reverse", action="store_true", help="measure the ranks in reverse order")
     ap.add_argument("--out", default=os.path.join(REPO, "gpurun_out", "rank_share.json"))
     ap.add_argument("--partition", action="store_true",
                     help="also the triangle-parallel lists (rt_hip_cand_produce / consume): each "
@@ -89,7 +90,8 @@ def main():
         per = rtgpu.tile_buffer_floats(f.width, f.height, n)
         d = C.c_void_p()
         assert L.rt_hip_malloc(0, per * 4, C.byref(d)) == 0
-        for rank in (range(n) if a.all_ranks else sorted({0, n - 1})):
+        ranks = list(range(n)) if a.all_ranks else sorted({0, n - 1})
+        for rank in (ranks[::-1] if a.reverse else ranks):
             for _ in range(2):  # warm-up (the first may size the hit buffer: RT_EHITBUF)
                 ctx.render(f, rank, n, d.value)
                 try:
