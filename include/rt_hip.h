@@ -304,10 +304,15 @@ int rt_hip_set_camera_refine(rt_hip_ctx *ctx, int enable);
  * (grown by its distance error) reaches beyond the triangle, in units of the
  * walk's slack, and 16 of their entries; out[68] the entries with the per-tile
  * refinement (rt_hip_set_camera_refine), [69] / [70] the refined footprints'
- * entries before / after it; use_leaves: also accept triangles whose error
- * region fits a leaf box of the host-built octree. */
+ * entries before / after it; [71..77] the float fast path's verdicts: listed,
+ * of those f64-safe through a leaf box, f64-safe otherwise, footprints with
+ * no tile, global; proven safe, away (off the frame); [78] / [79] the listed
+ * ones f64-safe because their error region stays within the slack / no line
+ * is steep enough to be accepted; [80] fast-path verdicts "safe" the f64
+ * classification does not confirm (must be 0); use_leaves: also accept
+ * triangles whose error region fits a leaf box of the host-built octree. */
 int rt_cand_survey(const rt_scene *scene, float eps_ulps, double bound_scale, int threads,
-                   int use_leaves, unsigned long long out[72]);
+                   int use_leaves, unsigned long long out[88]);
 
 /* Host-only sample of the per-tile refinement (rt_hip_set_camera_refine) of
  * a scene's frame: every stride-th entry of the refined footprints as (prim,

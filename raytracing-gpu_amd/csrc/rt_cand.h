@@ -100,7 +100,7 @@ struct CandParams {
 // the device count pass disagrees with the tiles the raster emits.
 extern "C" int rt_cand_survey_host(const CandParams* p, const float* tri, const float* node,
                                    const uint32_t* prim_leaf, int threads,
-                                   unsigned long long out[72]);
+                                   unsigned long long out[88]);
 // Host sample of the per-tile refinement's decisions (tests; see rt_cand.hip)
 extern "C" size_t rt_cand_refine_sample_host(const CandParams* p, const float* tri, uint32_t stride,
                                              uint32_t* out, size_t cap, size_t* total);

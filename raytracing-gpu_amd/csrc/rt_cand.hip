@@ -111,7 +111,7 @@ RTC_FN double pt_tri_dist(const double* x, const double* a, const double* b, con
 // and the distance error derr; td[6] = -1 when T_D has no bound for every
 // candidate line (c_ok > 0).
 RTC_FN int classify(const CandParams& p, const float* r, const float* leafbox, Footprint& fp,
-                    double* td = nullptr) {
+                    double* td = nullptr, int* why = nullptr) {
   const double v0[3] = {r[0], r[1], r[2]}, e1[3] = {r[3], r[4], r[5]}, e2[3] = {r[6], r[7], r[8]};
   const double v1[3] = {v0[0] + e1[0], v0[1] + e1[1], v0[2] + e1[2]};
   const double v2[3] = {v0[0] + e2[0], v0[1] + e2[1], v0[2] + e2[2]};
@@ -120,7 +120,10 @@ RTC_FN int classify(const CandParams& p, const float* r, const float* leafbox, F
                        e1[0] * e2[1] - e1[1] * e2[0]};
   const double nl = norm3(n);
   double e_a = p.c_a * kEps * l1 * l2 * kDMax;
-  if (nl * kDMax + e_a < kAMin) return SAFE;  // |a| < 1e-7 for every ray: never accepted
+  if (nl * kDMax + e_a < kAMin) {  // |a| < 1e-7 for every ray: never accepted
+    if (why) *why = 0;
+    return SAFE;
+  }
   const double inl = 1.0 / nl;  // (the unit normal to an ulp or two: inside every margin below)
   const double nh[3] = {n[0] * inl, n[1] * inl, n[2] * inl};
   const double pv[3] = {p.pos[0] - v0[0], p.pos[1] - v0[1], p.pos[2] - v0[2]};
@@ -222,14 +225,20 @@ RTC_FN int classify(const CandParams& p, const float* r, const float* leafbox, F
   // holding the triangle (so the walk visits that leaf and tests it), and
   // the float distance error cannot push it past the walk's pruning
   if (c_ok == 0.0 && derr <= 2.0 * p.eps_avail) {
-    if (hreach <= p.eps_avail) return SAFE;
+    if (hreach <= p.eps_avail) {
+      if (why) *why = 1;
+      return SAFE;
+    }
     if (leafbox) {
       const double e = p.eps_avail;
       bool in = true;
       for (int k = 0; k < 3 && in; k++)
         for (int a = 0; a < 3 && in; a++)
           in = P[k][a] >= (double)leafbox[a] - e && P[k][a] <= (double)leafbox[4 + a] + e;
-      if (in) return SAFE;
+      if (in) {
+        if (why) *why = 2;
+        return SAFE;
+      }
     }
   }
   // band: a candidate line at cosine c crosses the plane |h'| / c from a
@@ -246,7 +255,10 @@ RTC_FN int classify(const CandParams& p, const float* r, const float* leafbox, F
   // line with c < c_min is accepted.  Every candidate line has c <= c_band,
   // so c_min > c_band leaves none (with c_ok > 0 the lines below c_ok are
   // unbounded and c_min < c_ok: no exit there)
-  if (c_ok == 0.0 && (kAMin - e_a) > c_band * (kDMax * nl) * (1.0 + 1e-6)) return SAFE;
+  if (c_ok == 0.0 && (kAMin - e_a) > c_band * (kDMax * nl) * (1.0 + 1e-6)) {
+    if (why) *why = 3;
+    return SAFE;
+  }
 #endif
 #if defined(RT_SURVEY_DUMP) && !defined(__HIP_DEVICE_COMPILE__)
   if (td) {
@@ -398,13 +410,17 @@ RTC_FN bool rank_may_touch(const CandParams& p, const double q[3], double rb) {
 
 enum { Q_SAFE = 0, Q_LIST = 1, Q_AWAY = 2 };
 
+#ifndef RT_QUICK_TIGHT
+#define RT_QUICK_TIGHT 1
+#endif
+
 // Fast, conservative float version of classify()'s SAFE test (no leaf box):
 // every quantity is a positive magnitude computed in a few float operations,
 // bounded with explicit margins, so a true result is a proof on its own.
 // Most triangles of a frame take this exit.  A triangle it cannot prove safe
 // whose error region provably stays off this rank's tiles (rank_may_touch)
 // is Q_AWAY: its footprint would be empty here, so it is not classified.
-RTC_FN int quick_class(const CandParams& p, const float* r) {
+RTC_FN int quick_class(const CandParams& p, const float* r, float* dbg = nullptr) {
   const float fe = 5.9604645e-8f;
   const float e1x = r[3], e1y = r[4], e1z = r[5], e2x = r[6], e2y = r[7], e2z = r[8];
   const float l1 = sqrtf(e1x * e1x + e1y * e1y + e1z * e1z) * 1.00001f;
@@ -442,6 +458,28 @@ RTC_FN int quick_class(const CandParams& p, const float* r) {
     rho_o = rho;
     return (du + dv + dw) * (l1 + l2) * 1.0001f;
   };
+  // H with the corners' own displacements (classify's expand: |du e1 + dv
+  // e2|, |(dw + dv) e1 - dv e2|, |-du e1 + (dw + du) e2|) instead of their
+  // common bound (du + dv + dw)(l1 + l2), which is up to ~2x larger: the
+  // crossing region's reach, whose test below decides most triangles.  The
+  // vectors' rounding is absolute (cancellation), so it is bounded by 8 eps
+  // of the terms' magnitudes on top of the relative margin.
+  auto Ht = [&](float c, float& a_o, float& rho_o) {
+    const float a = fmaxf(amin, (dmin * nlo * c - e_a) * 0.99999f);
+    const float ra = 1.0f / a;
+    const float rho = e_a * ra;
+    const float rom = 1.0f / (1.0f - rho);
+    const float du = e_sh * ra * rom, dv = e_dq * ra * rom;
+    const float dw = (4.0f * fe + (e_sh + e_dq) * ra + rho) * rom;
+    a_o = a;
+    rho_o = rho;
+    const float p1 = dw + dv, p2 = dw + du;
+    const float x0 = du * e1x + dv * e2x, y0 = du * e1y + dv * e2y, z0 = du * e1z + dv * e2z;
+    const float x1 = p1 * e1x - dv * e2x, y1 = p1 * e1y - dv * e2y, z1 = p1 * e1z - dv * e2z;
+    const float x2 = p2 * e2x - du * e1x, y2 = p2 * e2y - du * e1y, z2 = p2 * e2z - du * e1z;
+    const float m = fmaxf(x0 * x0 + y0 * y0 + z0 * z0, fmaxf(x1 * x1 + y1 * y1 + z1 * z1, x2 * x2 + y2 * y2 + z2 * z2));
+    return sqrtf(m) * 1.0002f + 8.0f * fe * (p1 + p2) * (l1 + l2);
+  };
   float a, rho;
   const float ck = fminf(1.0f, (amin + e_a) / (dmin * nlo) * 1.0001f);
   const float kmax_ch = fmaxf(ck * H(ck, a, rho), H(1.0f, a, rho)) * 1.0001f;
@@ -458,7 +496,10 @@ RTC_FN int quick_class(const CandParams& p, const float* r) {
   float cl = num / (vmax + (float)p.dline) * 0.9999f;
   float h = H(cl, a, rho);
   // componentwise second round (see classify): the candidate lines cross
-  // T_D, inside the ball (centroid, max vertex distance + h)
+  // T_D, inside the ball (centroid, max vertex distance + h) -- with the
+  // common bound h, so that the cone, and the componentwise error terms from
+  // it, stay above classify()'s own (its ball is around T_D's corners):
+  // every verdict here is one classify() also reaches (rt_cand_survey [80])
   const float cx = (e1x + e2x) / 3.0f, cy = (e1y + e2y) / 3.0f, cz = (e1z + e2z) / 3.0f;  // - v0
   float rv = sqrtf(cx * cx + cy * cy + cz * cz);  // max vertex distance from the centroid
   rv = fmaxf(rv, sqrtf((e1x - cx) * (e1x - cx) + (e1y - cy) * (e1y - cy) + (e1z - cz) * (e1z - cz)));
@@ -494,9 +535,16 @@ RTC_FN int quick_class(const CandParams& p, const float* r) {
       h = H(cl, a, rho);
     }
   }
+  if (RT_QUICK_TIGHT) h = Ht(cl, a, rho);
   const float rmax = vmax + h;
   const float derr = (e_eq / (a * (1.0f - rho)) + (rmax + (float)p.lmax) * (rho + 4.0f * fe) / (1.0f - rho) +
                       4.0f * fe * ((float)p.omax + rmax + (float)p.lmax)) * 1.0001f;
+  if (dbg) {
+    dbg[0] = h;
+    dbg[1] = derr;
+    dbg[2] = cl;
+    dbg[3] = a;
+  }
   if (h <= (float)p.eps_avail * 0.9999f && derr <= 2.0f * (float)p.eps_avail * 0.9999f) return Q_SAFE;
   // T_D lies in the ball (centroid, rv + h): every corner of T_D is within
   // H(cl) of its vertex.  The centroid in double from the record's floats.
@@ -1657,15 +1705,20 @@ extern "C" hipError_t rt_cand_prim_leaf(const float4* node, uint32_t nnode, cons
 
 extern "C" int rt_cand_survey_host(const CandParams* p, const float* tri, const float* node,
                                    const uint32_t* prim_leaf, int threads,
-                                   unsigned long long out[72]) {
+                                   unsigned long long out[88]) {
   // out: [0] safe, [1] footprint, [2] global, [3] entries, [4 + k] prims
   // with 2^k <= entries < 2^(k+1), [20 + k] their entries (k < 16);
   // [36 + k] footprint prims whose T_D box (grown by the distance error
   // beyond the pruning margin) reaches beyond the triangle's own box by
   // g with 2^(k-8) <= g / eps_avail < 2^(k-7) (k = 0: below 2^-7; k = 15:
   // 2^7 and more, or unbounded), [52 + k] their entries
+  // [71..77]: quick_class's verdicts (listed; of those classify() SAFE
+  // through the leaf box, SAFE otherwise, FOOTPRINT without a tile, GLOBAL;
+  // Q_SAFE; Q_AWAY); [78] / [79] listed and SAFE by the reach / steepness
+  // exits; [80] Q_SAFE that classify() does not confirm
+  for (int k = 0; k < 88; k++) out[k] = 0;
   if (threads < 1) threads = 1;
-  std::vector<unsigned long long> part(72 * (size_t)threads, 0);
+  std::vector<unsigned long long> part(88 * (size_t)threads, 0);
   std::vector<unsigned long long> bad((size_t)threads, 0);
   std::vector<std::thread> th;
 #ifdef RT_SURVEY_DUMP
@@ -1673,7 +1726,7 @@ extern "C" int rt_cand_survey_host(const CandParams* p, const float* tri, const 
 #endif
   for (int t = 0; t < threads; t++)
     th.emplace_back([&, t]() {
-      unsigned long long* o = &part[72 * (size_t)t];
+      unsigned long long* o = &part[88 * (size_t)t];
       for (uint32_t i = (uint32_t)t; i < p->nprim; i += (uint32_t)threads) {
         rtc::Footprint fp;
         const float* lb = prim_leaf ? node + 8 * (size_t)prim_leaf[i] : nullptr;
@@ -1681,6 +1734,34 @@ extern "C" int rt_cand_survey_host(const CandParams* p, const float* tri, const 
         const float* rec = tri + 12 * (size_t)i;
         const int c = rtc::classify(*p, rec, lb, fp, td);
         o[c]++;
+        const int qc = rtc::quick_class(*p, rec);
+        if (qc == rtc::Q_LIST) {
+          o[71]++;
+          if (c == rtc::SAFE) {
+            rtc::Footprint f2;
+            int why = -1;
+            o[rtc::classify(*p, rec, nullptr, f2, nullptr, &why) == rtc::SAFE ? 73 : 72]++;
+            if (why == 1) o[78]++;  // the error region within the slack
+            if (why == 3) o[79]++;  // no candidate line steep enough to be accepted
+          } else if (c == rtc::GLOBAL) {
+            o[75]++;
+          }
+        } else {
+          o[qc == rtc::Q_SAFE ? 76 : 77]++;
+          if (qc == rtc::Q_SAFE && c != rtc::SAFE) {
+            o[80]++;  // the fast path's proof must hold
+            if (getenv("RT_SURVEY_VIOL") && o[80] <= 8) {
+              float dq[4];
+              rtc::quick_class(*p, rec, dq);
+              rtc::Footprint f3;
+              double t3[18];
+              for (double& x : t3) x = -9.0;
+              rtc::classify(*p, rec, nullptr, f3, t3);
+              fprintf(stderr, "viol prim %u c %d: f32 h %.6g derr %.6g cl %.6g a %.6g | f64 hreach %.6g cl %.6g kmax %.6g e_a %.6g derr %.6g eps %.6g\n",
+                      i, c, dq[0], dq[1], dq[2], dq[3], t3[13], t3[12], t3[14], t3[15], t3[6], p->eps_avail);
+            }
+          }
+        }
         if (c == rtc::FOOTPRINT) {
           unsigned long long v = 0, kept = 0;
           rtc::raster(*p, fp, [&](uint32_t tl) {
@@ -1723,6 +1804,7 @@ extern "C" int rt_cand_survey_host(const CandParams* p, const float* tri, const 
 #endif
           }
           o[3] += v;
+          if (!v && qc == rtc::Q_LIST) o[74]++;
           int k = 0;
           while (k < 15 && (2ull << k) <= v) k++;
           if (v) {
@@ -1758,9 +1840,9 @@ extern "C" int rt_cand_survey_host(const CandParams* p, const float* tri, const 
     fclose(fo);
   }
 #endif
-  for (int k = 0; k < 72; k++) {
+  for (int k = 0; k < 88; k++) {
     out[k] = 0;
-    for (int t = 0; t < threads; t++) out[k] += part[72 * (size_t)t + k];
+    for (int t = 0; t < threads; t++) out[k] += part[88 * (size_t)t + k];
   }
   unsigned long long nbad = 0;
   for (int t = 0; t < threads; t++) nbad += bad[t];

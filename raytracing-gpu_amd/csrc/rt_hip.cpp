@@ -923,7 +923,7 @@ extern "C" int rt_cand_refine_sample(const rt_scene* scene, float eps_ulps, doub
 }
 
 extern "C" int rt_cand_survey(const rt_scene* scene, float eps_ulps, double bound_scale, int threads,
-                              int use_leaves, unsigned long long out[72]) {
+                              int use_leaves, unsigned long long out[88]) {
   if (!scene || !out) return rt_set_error(RT_EINVAL, "null argument");
   rt_frame f;
   int rc = rt_frame_from_camera(&scene->camera, &f);

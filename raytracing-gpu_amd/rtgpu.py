@@ -381,7 +381,7 @@ def accel_probe(scene, accel="octree", stride=97, check=True):
 def cand_survey(scene, eps_ulps=64.0, bound_scale=1.0, threads=8, leaves=False):
     """Host-only: {safe, footprint, global, entries} of the camera candidate
     lists of the scene's frame (csrc/rt_cand.hip classify + raster)."""
-    out = (C.c_ulonglong * 72)()
+    out = (C.c_ulonglong * 88)()
     _check(lib().rt_cand_survey(scene.ptr, eps_ulps, bound_scale, threads, 1 if leaves else 0, out),
            "cand_survey")
     r = dict(zip(("safe", "footprint", "global", "entries"), (int(x) for x in out[:4])))
@@ -390,6 +390,11 @@ def cand_survey(scene, eps_ulps=64.0, bound_scale=1.0, threads=8, leaves=False):
     # entries before and after it
     r["refined"] = int(out[68])
     r["big_entries"], r["big_kept"] = int(out[69]), int(out[70])
+    # the float fast path (quick_class) and what the f64 classification makes
+    # of the prims it lists
+    r["quick"] = dict(zip(("listed", "listed_safe_leaf", "listed_safe_other", "listed_no_tiles",
+                           "listed_global", "safe", "away", "listed_safe_reach", "listed_safe_steep",
+                           "safe_violations"), (int(x) for x in out[71:81])))
     r["hist"] = [(1 << k, int(out[4 + k]), int(out[20 + k])) for k in range(16) if out[4 + k]]
     # footprint prims by how far their T_D box reaches beyond the triangle, in
     # units of the walk's slack: (lower edge 2^(k-8), prims, entries)
