@@ -175,6 +175,13 @@ extern "C" hipError_t rt_cand_part_count(const uint32_t* keys, uint32_t n, uint3
 extern "C" hipError_t rt_cand_part_scatter(const uint32_t* keys, const uint32_t* prims, const float* skip,
                                            uint32_t n, uint32_t tbits, int nranks, const uint32_t* off,
                                            uint32_t* start, uint32_t* out, hipStream_t s);
+// Stable compaction of the entries whose key is not drop_key into
+// keys_out / vals_out (at most cap; beyond it *ctr7 = 1): per-wave counts
+// (cnt, rt_cand_part_waves(n) + 1 words) -> exclusive scan (off, off[nw] =
+// the kept total) -> scatter.  tmp == NULL: *tmp_bytes = the scan's need.
+extern "C" hipError_t rt_cand_compact(const uint32_t* keys, const uint32_t* vals, uint32_t n, uint32_t drop_key,
+                                      uint32_t cap, uint32_t* cnt, uint32_t* off, void* tmp, size_t* tmp_bytes,
+                                      uint32_t* keys_out, uint32_t* vals_out, uint32_t* ctr7, hipStream_t s);
 extern "C" hipError_t rt_cand_unpack(const uint32_t* in, uint32_t n, uint32_t ntiles, uint32_t tpr, uint32_t* keys,
                                      uint32_t* idx, hipStream_t s);
 extern "C" hipError_t rt_cand_gather(const uint32_t* in, const uint32_t* idx, uint32_t n, uint32_t* cand,

@@ -54,6 +54,11 @@ extern "C" {
 
 // the trace's work order puts the long items of the same frame's previous
 // trace first (rt_cand.hip heavy_flag_kernel); 0: entries only (A/B knob)
+// asynchronous list builds compact the refinement's kept entries before the
+// sort (rt_cand_compact); 0: sort them all (A/B knob)
+#ifndef RT_COMPACT_LISTS
+#define RT_COMPACT_LISTS 1
+#endif
 #ifndef RT_COST_ORDER
 #define RT_COST_ORDER 1
 #endif
@@ -220,6 +225,15 @@ struct rt_hip_ctx {
   // the frame (camera frame, rank, nranks) whose trace last recorded its
   // per-item clocks (d_item_cost, their sum in the frame counters) and its
   // grid: the same frame's next work order puts its long items first
+  // the entries the refinement kept (start[ntiles]) in the last build of
+  // kept_for's frame, read back without waiting (h_kept, ev_kept): the same
+  // frame's asynchronous builds compact the entries to that many before the
+  // sort instead of sorting the dropped ones too
+  ListShape kept_for;
+  uint32_t* h_kept = nullptr;   // pinned
+  hipEvent_t ev_kept = nullptr;
+  int kept_ready = 0;           // h_kept holds kept_for's count
+  uint32_t kept = 0;
   ListShape cost_hist;
   uint32_t cost_waves = 0;
   uint32_t* d_item_cost = nullptr;  // 4 x ntiles_local
@@ -400,6 +414,8 @@ extern "C" void rt_hip_destroy(rt_hip_ctx* c) {
   (void)hipFree(c->d_rstart);
   (void)hipFree(c->d_part);
   (void)hipFree(c->d_item_cost);
+  if (c->h_kept) (void)hipHostFree(c->h_kept);
+  if (c->ev_kept) (void)hipEventDestroy(c->ev_kept);
   if (c->h_rstart) (void)hipHostFree(c->h_rstart);
   for (auto& f : c->ev)
     for (hipEvent_t e : f)
@@ -841,14 +857,14 @@ extern "C" int rt_hip_set_cull_slack(rt_hip_ctx* c, float ulps) {
   if (!c || !(ulps >= 0.0f)) return rt_set_error(RT_EINVAL, "bad slack");
   c->eps_ulps = ulps;
   c->cam_eps_ulps = ulps;
-  c->known.valid = c->pknown.valid = 0;  // the lists change
+  c->known.valid = c->pknown.valid = c->kept_for.valid = 0;  // the lists change
   return RT_OK;
 }
 
 extern "C" int rt_hip_set_camera_slack(rt_hip_ctx* c, float ulps) {
   if (!c || !(ulps >= 0.0f)) return rt_set_error(RT_EINVAL, "bad slack");
   c->cam_eps_ulps = ulps;
-  c->known.valid = c->pknown.valid = 0;  // the lists change
+  c->known.valid = c->pknown.valid = c->kept_for.valid = 0;  // the lists change
   return RT_OK;
 }
 
@@ -881,14 +897,14 @@ extern "C" int rt_hip_set_policy(rt_hip_ctx* c, int policy) {
 extern "C" int rt_hip_set_camera_refine(rt_hip_ctx* c, int enable) {
   if (!c) return rt_set_error(RT_EINVAL, "null context");
   c->cand_refine = enable ? 1 : 0;
-  c->known.valid = c->pknown.valid = 0;  // the lists change
+  c->known.valid = c->pknown.valid = c->kept_for.valid = 0;  // the lists change
   return RT_OK;
 }
 
 extern "C" int rt_hip_set_camera_bound_scale(rt_hip_ctx* c, double scale) {
   if (!c || !(scale > 0.0)) return rt_set_error(RT_EINVAL, "bad bound scale");
   c->bound_scale = scale;
-  c->known.valid = c->pknown.valid = 0;  // the lists change
+  c->known.valid = c->pknown.valid = c->kept_for.valid = 0;  // the lists change
   return RT_OK;
 }
 
@@ -1178,7 +1194,7 @@ static constexpr uint32_t kItemCap = RT_CAND_ITEM_CAP;
 extern "C" int rt_hip_set_cand_item_cap(rt_hip_ctx* c, unsigned cap) {
   if (!c) return rt_set_error(RT_EINVAL, "null context");
   c->cand_item_cap = cap;
-  c->known.valid = c->pknown.valid = 0;  // the lists change
+  c->known.valid = c->pknown.valid = c->kept_for.valid = 0;  // the lists change
   return RT_OK;
 }
 
@@ -1633,11 +1649,61 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
   }
   rc = cand_tile_buffers(c, nt);
   if (rc) return rc;
-  // keys are tiles < nt, or nt for an entry the refinement dropped: nt + 1 keys
-  rc = cand_sort(c, c->d_cand_keys, c->d_cand_keys2, c->d_cand_vals, c->d_cand, total, nt + 1, s);
-  if (rc) return rc;
+  // the kept count of this frame's earlier build, once its read-back is done
+  if (!c->kept_ready && c->kept_for.valid && c->ev_kept && hipEventQuery(c->ev_kept) == hipSuccess) {
+    c->kept = *c->h_kept;
+    c->kept_ready = 1;
+  }
+  const bool compact = RT_COMPACT_LISTS && async && c->cand_refine && c->kept_ready &&
+                       c->kept_for.same(f, kp->rank, kp->nranks) && c->kept <= total;
+  if (compact) {
+    // the kept entries (stable) -> keys2 / d_cand, sorted back into keys /
+    // vals, and the buffer pairs swapped so that the sorted ones are where
+    // the uncompacted path leaves them
+    const uint32_t nw = rt_cand_part_waves(total);
+    if ((size_t)2 * nw + 4 > c->part_cap) {
+      (void)hipFree(c->d_part);
+      c->d_part = nullptr;
+      c->part_cap = 0;
+      const size_t cap = 2 * ((size_t)nw + nw / 4) + 1024;
+      HIP_TRY(hipMalloc((void**)&c->d_part, cap * sizeof(uint32_t)));
+      c->part_cap = cap;
+    }
+    uint32_t* cnt = c->d_part;
+    uint32_t* off = c->d_part + nw + 1;
+    size_t tmpb = 0;
+    HIP_TRY(rt_cand_compact(c->d_cand_keys, c->d_cand_vals, total, (uint32_t)nt, c->kept, cnt, off, nullptr, &tmpb,
+                            c->d_cand_keys2, c->d_cand, c->d_cand_ctr + 7, s));
+    rc = ensure_tmp(c, tmpb);
+    if (rc) return rc;
+    tmpb = c->scan_tmp_bytes;
+    HIP_TRY(rt_cand_compact(c->d_cand_keys, c->d_cand_vals, total, (uint32_t)nt, c->kept, cnt, off, c->d_scan_tmp,
+                            &tmpb, c->d_cand_keys2, c->d_cand, c->d_cand_ctr + 7, s));
+    // (fewer kept than last time -- never expected -- leaves a tail: dropped)
+    HIP_TRY(rt_cand_fill_tail(c->d_cand_keys2, off + nw, c->kept, (uint32_t)nt, s));
+    // the per-frame counters rt_hip_stats reads (the overflow flag was set after the snapshot)
+    HIP_TRY(hipMemcpyAsync(c->d_cand_ctr + 23, c->d_cand_ctr + 7, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    rc = cand_sort(c, c->d_cand_keys2, c->d_cand_keys, c->d_cand, c->d_cand_vals, c->kept, nt + 1, s);
+    if (rc) return rc;
+    std::swap(c->d_cand_keys, c->d_cand_keys2);
+    std::swap(c->d_cand_vals, c->d_cand);
+    total = c->kept;
+  } else {
+    // keys are tiles < nt, or nt for an entry the refinement dropped: nt + 1 keys
+    rc = cand_sort(c, c->d_cand_keys, c->d_cand_keys2, c->d_cand_vals, c->d_cand, total, nt + 1, s);
+    if (rc) return rc;
+  }
   // start[nt] = the entries with a tile (the dropped ones sort after them)
   HIP_TRY(rt_cand_bounds(c->d_cand_keys2, total, c->d_cand_start, (uint32_t)nt, s));
+  if (RT_COMPACT_LISTS && c->cand_refine && !compat && !c->kept_for.same(f, kp->rank, kp->nranks)) {
+    // this frame's kept count, for its later builds (read back without waiting)
+    if (!c->h_kept) HIP_TRY(hipHostMalloc((void**)&c->h_kept, sizeof(uint32_t), hipHostMallocDefault));
+    if (!c->ev_kept) HIP_TRY(hipEventCreateWithFlags(&c->ev_kept, hipEventDisableTiming));
+    HIP_TRY(hipMemcpyAsync(c->h_kept, c->d_cand_start + nt, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipEventRecord(c->ev_kept, s));
+    c->kept_for.set(f, kp->rank, kp->nranks);
+    c->kept_ready = 0;
+  }
   // the sorted keys are spent: their buffer takes the per-entry skip bounds
   float* entry_skip = (float*)c->d_cand_keys2;
   HIP_TRY(rt_cand_entry_skip(c->d_cand, c->d_cand_skip, entry_skip, total, c->d_cand_start + nt, s));
@@ -2313,7 +2379,7 @@ extern "C" int rt_hip_stats(rt_hip_ctx* c, rt_stats* out) {
     c->last_async = 0;
     c->cand_global = actr[1];
     if (actr[7]) {  // never expected (the same frame's lists): reported, and the next build reads back
-      c->known.valid = 0;
+      c->known.valid = c->kept_for.valid = 0;
       return rt_set_error(RT_EHITBUF, "%u candidate-list entries, %u expected: render again", actr[6],
                           c->known.total);
     }

@@ -659,8 +659,10 @@ def test_async_lists_repeated_frame(gpu):
     ref, st_ref = gpu.Context(s, "octree_gpu").render_image(f)  # one frame: read-back build
     ctx = gpu.Context(s, "octree_gpu")
     small = gpu.Scene.synthetic(6, 6, 9776, seed=0x5EED, width=240, height=136)
-    for frame_no in range(4):
-        img, st = ctx.render_image(f)  # frames 1-3: asynchronous lists
+    for frame_no in range(6):
+        # frames 1-5: asynchronous lists; from the second build after the
+        # frame's first, the refinement's kept entries compacted before the sort
+        img, st = ctx.render_image(f)
         assert_bitexact(img, ref, f"frame {frame_no}: asynchronous candidate lists")
         assert (st["closest"], st["shadow"], st["cand_entries"]) == \
             (st_ref["closest"], st_ref["shadow"], st_ref["cand_entries"])
@@ -668,9 +670,10 @@ def test_async_lists_repeated_frame(gpu):
             ctx.render_image(small.frame())  # another frame in between
     # rank splits on the same context: each (frame, rank) once with a read-back
     t0, st0 = _tiles_of_rank(ctx, f, 1, 4)
-    t1, st1 = _tiles_of_rank(ctx, f, 1, 4)  # asynchronous
-    assert_bitexact(t1, t0, "rank 1 of 4, asynchronous lists")
-    assert st1["cand_entries"] == st0["cand_entries"] > 0
+    for _ in range(3):
+        t1, st1 = _tiles_of_rank(ctx, f, 1, 4)  # asynchronous (then also compacted)
+        assert_bitexact(t1, t0, "rank 1 of 4, asynchronous lists")
+        assert st1["cand_entries"] == st0["cand_entries"] > 0
 
 
 def test_triangle_parallel_lists_two_processes(gpu):
