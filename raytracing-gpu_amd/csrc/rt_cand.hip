@@ -962,7 +962,11 @@ __device__ __forceinline__ uint32_t slice_prim(const CandParams& p, uint32_t i) 
   return (b * p.sl_stride + p.sl_rank) * RT_SLICE_BLOCK + i % RT_SLICE_BLOCK;
 }
 
-__global__ __launch_bounds__(RT_LIST_BLOCK) void quick_kernel(CandParams p) {
+// waves per SIMD the fast path is compiled for (VGPR budget; A/B knob)
+#ifndef RT_QUICK_WAVES
+#define RT_QUICK_WAVES 1
+#endif
+__global__ __launch_bounds__(RT_LIST_BLOCK, RT_QUICK_WAVES) void quick_kernel(CandParams p) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;  // index in the slice
   const uint32_t len = p.prim1 - p.prim0;
   if (i < 8u) p.ctr[i] = 0u;          // the frame's counters (count / big passes, later launches)
@@ -1341,8 +1345,11 @@ __global__ __launch_bounds__(64) void big_item_kernel(CandParams p) {
 // waves) and the frame took 0.1 ms longer on C5 (profiles/r06e/ab.log).
 __device__ __forceinline__ void refine_item(const CandParams& p, uint32_t item);
 
+#ifndef RT_REFINE_WAVES
+#define RT_REFINE_WAVES 1
+#endif
 template <bool CHECK>
-__global__ __launch_bounds__(64) void refine_kernel(CandParams p) {
+__global__ __launch_bounds__(64, RT_REFINE_WAVES) void refine_kernel(CandParams p) {
   if (CHECK && (p.ctr[5] || blockIdx.x >= p.wave_base[kBigWaves])) return;
   refine_item(p, blockIdx.x);
 }
