@@ -139,6 +139,9 @@ extern "C" hipError_t rt_cand_scan(const uint32_t* in, uint32_t* out, uint32_t n
 extern "C" uint32_t rt_cand_scan_dev_tiles(uint32_t nmax);
 extern "C" hipError_t rt_cand_scan_dev(const uint32_t* in, uint32_t* out, uint32_t nmax, const uint32_t* n_dev,
                                        uint32_t* total, uint32_t* bsum, hipStream_t s);
+// the fast path's flags (p->visits over the slice) scanned straight into the
+// compact list (p->list) and its length (p->ctr[3]): scan_dev + scatter fused
+extern "C" hipError_t rt_cand_scan_scatter(const CandParams* p, uint32_t* bsum, hipStream_t s);
 extern "C" hipError_t rt_cand_sort(uint32_t* keys_in, uint32_t* keys_out, uint32_t* vals_in,
                                    uint32_t* vals_out, uint32_t n, int begin_bit, int end_bit, void* temp,
                                    size_t* temp_bytes, hipStream_t s);
@@ -160,21 +163,24 @@ extern "C" hipError_t rt_cand_bounds(const uint32_t* keys, uint32_t n, uint32_t*
 // bits).  unpack (consumer):
 // keys = local tile (tpr -> ntiles: the globals sort last), idx = i.
 // gather: the sorted entries' prims and skip bounds.
-extern "C" hipError_t rt_cand_route(uint32_t* keys, uint32_t n, int tiles_x, int nranks, int blocks_x, int tb,
-                                    uint32_t tbits, uint32_t drop_key, const uint32_t* total_dev, hipStream_t s);
 extern "C" hipError_t rt_cand_route_globals(const uint32_t* global, uint32_t nglobal, int nranks, uint32_t tpr,
                                             uint32_t tbits, uint32_t* keys, uint32_t* vals, hipStream_t s);
 // Stable partition of n routed keys by rank (rank nranks: dropped), packed
 // 3 words per entry in out (the dropped ones not written), start[d] = first
-// entry of rank d (start[nranks] = the routed entries): part_count ->
+// entry of rank d (start[nranks] = the routed entries; start[nranks + 1 ..
+// nranks + 8] = ctr[0 .. 7], for one read-back): part_count ->
 // hist[(nranks + 1) x rt_cand_part_waves(n)] -> exclusive scan (off) ->
 // part_scatter.  nranks <= 256.
 extern "C" uint32_t rt_cand_part_waves(uint32_t n);
-extern "C" hipError_t rt_cand_part_count(const uint32_t* keys, uint32_t n, uint32_t tbits, int nranks,
-                                         uint32_t* hist, hipStream_t s);
+// part_count routes the first nroute keys itself (route_kernel's mapping;
+// total_dev: an asynchronous build's own entry count, the rest dropped) and
+// writes them back; the keys past nroute come routed (the globals)
+extern "C" hipError_t rt_cand_part_count(uint32_t* keys, uint32_t n, uint32_t tbits, int nranks, uint32_t* hist,
+                                         uint32_t nroute, int tiles_x, int blocks_x, int tb, uint32_t drop_key,
+                                         const uint32_t* total_dev, hipStream_t s);
 extern "C" hipError_t rt_cand_part_scatter(const uint32_t* keys, const uint32_t* prims, const float* skip,
                                            uint32_t n, uint32_t tbits, int nranks, const uint32_t* off,
-                                           uint32_t* start, uint32_t* out, hipStream_t s);
+                                           uint32_t* start, uint32_t* out, const uint32_t* ctr, hipStream_t s);
 // Stable compaction of the entries whose key is not drop_key into
 // keys_out / vals_out (at most cap; beyond it *ctr7 = 1): per-wave counts
 // (cnt, rt_cand_part_waves(n) + 1 words) -> exclusive scan (off, off[nw] =

@@ -1068,7 +1068,10 @@ __device__ __forceinline__ void count_one(const CandParams& p, uint32_t j) {
   p.visits[j] = visits;
 }
 
-__global__ __launch_bounds__(RT_LIST_BLOCK) void count_kernel(CandParams p) {
+#ifndef RT_COUNT_WAVES
+#define RT_COUNT_WAVES 1
+#endif
+__global__ __launch_bounds__(RT_LIST_BLOCK, RT_COUNT_WAVES) void count_kernel(CandParams p) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j < p.ctr[3]) count_one(p, j);
 }
@@ -1429,22 +1432,13 @@ __global__ __launch_bounds__(256) void entry_skip_kernel(const uint32_t* cand, c
 // A whole-frame entry (scanline tile of the one-rank map) -> its rank d and
 // rank-local tile l under the N-rank block map: key d << tbits | l (l <= tpr
 // < 2^tbits), partitioned by d below.
-__global__ __launch_bounds__(256) void route_kernel(uint32_t* keys, uint32_t n, int tiles_x, int nranks,
-                                                    int blocks_x, int tb, uint32_t tbits, uint32_t drop_key,
-                                                    const uint32_t* total_dev) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  // an asynchronous build's buffers hold the known total: entries past the
-  // build's own (total_dev) are unused (never expected; checked by the host)
-  const uint32_t t = total_dev && i >= *total_dev ? drop_key : keys[i];
-  if (t == drop_key) {  // dropped by the refinement: after every rank's entries
-    keys[i] = (uint32_t)nranks << tbits;
-    return;
-  }
+__device__ __forceinline__ uint32_t route_key(uint32_t t, int tiles_x, int nranks, int blocks_x, int tb,
+                                              uint32_t tbits, uint32_t drop_key) {
+  if (t == drop_key) return (uint32_t)nranks << tbits;  // dropped by the refinement: after every rank's entries
   uint32_t d;
   const uint32_t l = rt_tile_local((int)(t % (uint32_t)tiles_x), (int)(t / (uint32_t)tiles_x), (uint32_t)nranks,
                                    (uint32_t)blocks_x, (uint32_t)tb, &d);
-  keys[i] = d << tbits | l;
+  return d << tbits | l;
 }
 
 // the slice's globals: one entry per rank, local slot tpr
@@ -1469,19 +1463,33 @@ __global__ __launch_bounds__(256) void route_globals_kernel(const uint32_t* glob
 // (local tile or tpr, prim, skip bits); start[d] = hist offset of (d, 0).
 constexpr uint32_t kPartSteps = 16, kPartChunk = 64 * kPartSteps;
 
-__global__ __launch_bounds__(64) void part_count_kernel(const uint32_t* keys, uint32_t n, uint32_t tbits,
-                                                        int nranks, uint32_t* hist) {
+// (with the routing of the entries [0, nroute) fused in: route_kernel's
+// key, written back for part_scatter; the globals past them come routed)
+__global__ __launch_bounds__(64) void part_count_kernel(uint32_t* keys, uint32_t n, uint32_t tbits, int nranks,
+                                                        uint32_t* hist, uint32_t nroute, int tiles_x, int blocks_x,
+                                                        int tb, uint32_t drop_key, const uint32_t* total_dev) {
   __shared__ uint32_t cnt[257];
   const int lane = threadIdx.x;
   const uint32_t nw = gridDim.x, w = blockIdx.x;
   for (int d = lane; d <= nranks; d += 64) cnt[d] = 0u;
   __syncthreads();
   const uint32_t e0 = w * kPartChunk, e1 = e0 + kPartChunk < n ? e0 + kPartChunk : n;
+  const uint32_t own = total_dev ? *total_dev : nroute;  // entries the build wrote (async: <= nroute)
   uint32_t k[kPartSteps];  // every load in flight at once (the pass is latency-bound)
 #pragma unroll
   for (uint32_t t = 0; t < kPartSteps; t++) {
     const uint32_t i = e0 + t * 64u + (uint32_t)lane;
-    k[t] = i < e1 ? keys[i] >> tbits : 0xffffffffu;
+    k[t] = i < e1 ? keys[i] : 0u;
+  }
+#pragma unroll
+  for (uint32_t t = 0; t < kPartSteps; t++) {
+    const uint32_t i = e0 + t * 64u + (uint32_t)lane;
+    if (i < e1 && i < nroute) {
+      const uint32_t key = route_key(i < own ? k[t] : drop_key, tiles_x, nranks, blocks_x, tb, tbits, drop_key);
+      keys[i] = key;
+      k[t] = key;
+    }
+    k[t] = i < e1 ? k[t] >> tbits : 0xffffffffu;
   }
 #pragma unroll
   for (uint32_t t = 0; t < kPartSteps; t++)
@@ -1492,14 +1500,17 @@ __global__ __launch_bounds__(64) void part_count_kernel(const uint32_t* keys, ui
 
 __global__ __launch_bounds__(64) void part_scatter_kernel(const uint32_t* keys, const uint32_t* prims,
                                                           const float* skip, uint32_t n, uint32_t tbits, int nranks,
-                                                          const uint32_t* off, uint32_t* start, uint32_t* out) {
+                                                          const uint32_t* off, uint32_t* start, uint32_t* out,
+                                                          const uint32_t* ctr) {
   __shared__ uint32_t base[257];
   const int lane = threadIdx.x;
-  const uint32_t nw = gridDim.x, w = blockIdx.x;
+  const uint32_t nw = (n + kPartChunk - 1) / kPartChunk, w = blockIdx.x;  // (one workgroup when n = 0)
   for (int d = lane; d <= nranks; d += 64) {
-    base[d] = off[(size_t)d * nw + w];
+    base[d] = nw ? off[(size_t)d * nw + w] : 0u;
     if (w == 0) start[d] = base[d];
   }
+  // the build's counters beside the starts: the host reads both in one copy
+  if (w == 0 && lane < 8) start[nranks + 1 + lane] = ctr[lane];
   __syncthreads();
   const uint32_t e0 = w * kPartChunk, e1 = e0 + kPartChunk < n ? e0 + kPartChunk : n;
   const uint64_t lt = (1ull << lane) - 1ull;
@@ -1701,28 +1712,27 @@ __global__ __launch_bounds__(kScanThreads) void scan_sums_kernel(const uint32_t*
   if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
 }
 
-// one workgroup: exclusive scan of the nb tile sums in place
-__global__ __launch_bounds__(kScanThreads) void scan_tops_kernel(uint32_t* bsum, uint32_t nb) {
-  __shared__ uint32_t sh[kScanThreads / 64];
-  uint32_t carry = 0;
-  for (uint32_t b0 = 0; b0 < nb; b0 += kScanThreads) {
-    const uint32_t i = b0 + threadIdx.x;
-    const uint32_t x = i < nb ? bsum[i] : 0u;
-    uint32_t tot;
-    const uint32_t ex = block_excl_scan(x, sh, &tot);
-    if (i < nb) bsum[i] = carry + ex;
-    carry += tot;
-  }
-}
-
+// The tiles' prefix: each apply workgroup sums the tile sums before its own
+// (a few thousand tiles at most: ~10 loads per thread from L2) instead of a
+// one-workgroup pass over them between the two launches.
+// SCATTER (the fast path's flags over the build's slice, CandParams p): the
+// exclusive prefix of a flagged prim is its place in the compact list, which
+// this pass writes directly (list[o] = prim), and the scan's last value is
+// the list length (ctr[3]) -- no offsets array, no scatter launch.
+template <bool SCATTER>
 __global__ __launch_bounds__(kScanThreads) void scan_apply_kernel(const uint32_t* __restrict__ in, uint32_t* out,
                                                                   uint32_t nmax, const uint32_t* n_dev,
-                                                                  const uint32_t* bsum, uint32_t* total) {
+                                                                  const uint32_t* bsum, uint32_t* total,
+                                                                  CandParams p) {
   __shared__ uint32_t v[kScanTile + kScanThreads];  // thread t's 16 values at t * 17 (no bank conflicts)
   __shared__ uint32_t sh[kScanThreads / 64];
   const uint32_t n1 = scan_len(nmax, n_dev), base = blockIdx.x * (uint32_t)kScanTile;
   if (base >= n1) return;  // uniform per block
   const int t = threadIdx.x;
+  uint32_t before = 0;
+  for (uint32_t b = (uint32_t)t; b < blockIdx.x; b += kScanThreads) before += bsum[b];
+  uint32_t tot0;
+  block_excl_scan(before, sh, &tot0);  // tot0 = the tiles before this one
   for (int k = 0; k < kScanPer; k++) {
     const uint32_t e = (uint32_t)(k * kScanThreads + t), i = base + e;
     v[e + e / kScanPer] = i < n1 ? in[i] : 0u;
@@ -1731,11 +1741,28 @@ __global__ __launch_bounds__(kScanThreads) void scan_apply_kernel(const uint32_t
   uint32_t run = 0;
   for (int k = 0; k < kScanPer; k++) run += v[t * (kScanPer + 1) + k];
   uint32_t tot;
-  uint32_t pre = bsum[blockIdx.x] + block_excl_scan(run, sh, &tot);
+  uint32_t pre = tot0 + block_excl_scan(run, sh, &tot);
+  uint32_t flags = 0;  // SCATTER: which of this thread's values were set
   for (int k = 0; k < kScanPer; k++) {
     const uint32_t x = v[t * (kScanPer + 1) + k];
+    if (SCATTER && x) flags |= 1u << k;
     v[t * (kScanPer + 1) + k] = pre;
     pre += x;
+  }
+  if (SCATTER) {
+    // thread t's values are elements t * 16 + k of the tile: write the list
+    // entries of its flagged ones (in[] holds 0 / 1)
+    for (int k = 0; k < kScanPer; k++) {
+      const uint32_t e = (uint32_t)(t * kScanPer + k), i = base + e;
+      if (i >= n1) break;
+      const uint32_t o = v[t * (kScanPer + 1) + k];
+      if (i == n1 - 1u) {
+        p.ctr[3] = o;  // list length (the scan's last input is 0)
+      } else if ((flags >> k) & 1u) {
+        p.list[o] = slice_prim(p, i);
+      }
+    }
+    return;
   }
   __syncthreads();
   for (int k = 0; k < kScanPer; k++) {
@@ -1745,6 +1772,41 @@ __global__ __launch_bounds__(kScanThreads) void scan_apply_kernel(const uint32_t
       out[i] = o;
       if (i == n1 - 1u && total) *total = o;
     }
+  }
+}
+
+// Exclusive scan of in[0 .. n] (n + 1 values, out[n] = their sum) in one
+// workgroup, for the short scans between list passes (the big footprints'
+// items, a partition's per-wave counts): one launch instead of rocPRIM's two.
+constexpr uint32_t kSmallScanThreads = 1024, kSmallScanPer = 16;
+constexpr uint32_t kSmallScanMax = kSmallScanThreads * kSmallScanPer;
+
+__global__ __launch_bounds__(kSmallScanThreads) void scan_small_kernel(const uint32_t* __restrict__ in,
+                                                                       uint32_t* __restrict__ out, uint32_t n) {
+  __shared__ uint32_t wsum[kSmallScanThreads / 64];
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  const uint32_t m = n + 1u, per = (m + kSmallScanThreads - 1u) / kSmallScanThreads;
+  const uint32_t i0 = t * per;
+  uint32_t v[kSmallScanPer], run = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kSmallScanPer; k++) {
+    v[k] = (k < per && i0 + k < m) ? in[i0 + k] : 0u;
+    run += v[k];
+  }
+  uint32_t inc = run;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, 64);
+    if ((int)lane >= o) inc += y;
+  }
+  if (lane == 63u) wsum[wv] = inc;
+  __syncthreads();
+  uint32_t before = 0;
+  for (uint32_t k = 0; k < wv; k++) before += wsum[k];
+  uint32_t pre = before + inc - run;
+#pragma unroll
+  for (uint32_t k = 0; k < kSmallScanPer; k++) {
+    if (k < per && i0 + k < m) out[i0 + k] = pre;
+    pre += v[k];
   }
 }
 
@@ -2147,14 +2209,34 @@ extern "C" hipError_t rt_cand_scan_dev(const uint32_t* in, uint32_t* out, uint32
                                        uint32_t* total, uint32_t* bsum, hipStream_t s) {
   const uint32_t nb = rt_cand_scan_dev_tiles(nmax);
   hipLaunchKernelGGL(rtc::scan_sums_kernel, dim3(nb), dim3(rtc::kScanThreads), 0, s, in, nmax, n_dev, bsum);
-  hipLaunchKernelGGL(rtc::scan_tops_kernel, dim3(1), dim3(rtc::kScanThreads), 0, s, bsum, nb);
-  hipLaunchKernelGGL(rtc::scan_apply_kernel, dim3(nb), dim3(rtc::kScanThreads), 0, s, in, out, nmax, n_dev,
-                     (const uint32_t*)bsum, total);
+  CandParams none;
+  memset(&none, 0, sizeof none);
+  hipLaunchKernelGGL(rtc::scan_apply_kernel<false>, dim3(nb), dim3(rtc::kScanThreads), 0, s, in, out, nmax, n_dev,
+                     (const uint32_t*)bsum, total, none);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t rt_cand_scan_scatter(const CandParams* p, uint32_t* bsum, hipStream_t s) {
+  const uint32_t len = p->prim1 - p->prim0;
+  const uint32_t nb = rt_cand_scan_dev_tiles(len);
+  hipLaunchKernelGGL(rtc::scan_sums_kernel, dim3(nb), dim3(rtc::kScanThreads), 0, s, p->visits, len,
+                     (const uint32_t*)nullptr, bsum);
+  hipLaunchKernelGGL(rtc::scan_apply_kernel<true>, dim3(nb), dim3(rtc::kScanThreads), 0, s,
+                     (const uint32_t*)p->visits, (uint32_t*)nullptr, len, (const uint32_t*)nullptr,
+                     (const uint32_t*)bsum, (uint32_t*)nullptr, *p);
   return hipGetLastError();
 }
 
 extern "C" hipError_t rt_cand_scan(const uint32_t* in, uint32_t* out, uint32_t n, void* temp,
                                    size_t* temp_bytes, hipStream_t s) {
+  if ((size_t)n + 1 <= rtc::kSmallScanMax) {  // one workgroup, no temporary storage
+    if (!temp) {
+      *temp_bytes = 0;
+      return hipSuccess;
+    }
+    hipLaunchKernelGGL(rtc::scan_small_kernel, dim3(1), dim3(rtc::kSmallScanThreads), 0, s, in, out, n);
+    return hipGetLastError();
+  }
   return rocprim::exclusive_scan(temp, *temp_bytes, in, out, 0u, (size_t)n + 1,
                                  rocprim::plus<uint32_t>(), s);
 }
@@ -2193,14 +2275,6 @@ extern "C" hipError_t rt_cand_bounds(const uint32_t* keys, uint32_t n, uint32_t*
 }
 
 
-extern "C" hipError_t rt_cand_route(uint32_t* keys, uint32_t n, int tiles_x, int nranks, int blocks_x, int tb,
-                                    uint32_t tbits, uint32_t drop_key, const uint32_t* total_dev, hipStream_t s) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(rtc::route_kernel, dim3((n + 255) / 256), dim3(256), 0, s, keys, n, tiles_x, nranks, blocks_x,
-                     tb, tbits, drop_key, total_dev);
-  return hipGetLastError();
-}
-
 extern "C" hipError_t rt_cand_route_globals(const uint32_t* global, uint32_t nglobal, int nranks, uint32_t tpr,
                                             uint32_t tbits, uint32_t* keys, uint32_t* vals, hipStream_t s) {
   const uint32_t n = nglobal * (uint32_t)nranks;
@@ -2228,21 +2302,22 @@ extern "C" uint32_t rt_cand_part_waves(uint32_t n) {
   return (n + rtc::kPartChunk - 1) / rtc::kPartChunk;
 }
 
-extern "C" hipError_t rt_cand_part_count(const uint32_t* keys, uint32_t n, uint32_t tbits, int nranks,
-                                         uint32_t* hist, hipStream_t s) {
+extern "C" hipError_t rt_cand_part_count(uint32_t* keys, uint32_t n, uint32_t tbits, int nranks, uint32_t* hist,
+                                         uint32_t nroute, int tiles_x, int blocks_x, int tb, uint32_t drop_key,
+                                         const uint32_t* total_dev, hipStream_t s) {
   const uint32_t nw = rt_cand_part_waves(n);
   if (nw == 0) return hipSuccess;
-  hipLaunchKernelGGL(rtc::part_count_kernel, dim3(nw), dim3(64), 0, s, keys, n, tbits, nranks, hist);
+  hipLaunchKernelGGL(rtc::part_count_kernel, dim3(nw), dim3(64), 0, s, keys, n, tbits, nranks, hist, nroute,
+                     tiles_x, blocks_x, tb, drop_key, total_dev);
   return hipGetLastError();
 }
 
 extern "C" hipError_t rt_cand_part_scatter(const uint32_t* keys, const uint32_t* prims, const float* skip,
                                            uint32_t n, uint32_t tbits, int nranks, const uint32_t* off,
-                                           uint32_t* start, uint32_t* out, hipStream_t s) {
+                                           uint32_t* start, uint32_t* out, const uint32_t* ctr, hipStream_t s) {
   const uint32_t nw = rt_cand_part_waves(n);
-  if (nw == 0) return hipMemsetAsync(start, 0, ((size_t)nranks + 1) * sizeof(uint32_t), s);
-  hipLaunchKernelGGL(rtc::part_scatter_kernel, dim3(nw), dim3(64), 0, s, keys, prims, skip, n, tbits, nranks, off,
-                     start, out);
+  hipLaunchKernelGGL(rtc::part_scatter_kernel, dim3(nw ? nw : 1u), dim3(64), 0, s, keys, prims, skip, n, tbits,
+                     nranks, off, start, out, ctr);
   return hipGetLastError();
 }
 

@@ -1329,6 +1329,9 @@ static int cand_params(const rt_frame* f, const float scene_c[3], float scene_r,
 }
 
 static int ensure_tmp(rt_hip_ctx* c, size_t bytes) {
+  // never null once ensured: rt_cand_scan takes a null temp for a size query,
+  // also on its one-workgroup path, which needs none
+  if (bytes < 256) bytes = 256;
   if (bytes <= c->scan_tmp_bytes && c->d_scan_tmp) return RT_OK;
   (void)hipFree(c->d_scan_tmp);
   c->d_scan_tmp = nullptr;
@@ -1524,8 +1527,8 @@ static int cand_build(rt_hip_ctx* c, CandParams& cp, hipStream_t s, uint32_t glo
   const uint32_t slice = cp.prim1 - cp.prim0;
   HIP_TRY(rt_cand_quick(&cp, s));
 #if RT_DEV_SCAN
-  HIP_TRY(rt_cand_scan_dev(c->d_cand_visits, c->d_cand_off, slice, nullptr, nullptr, c->d_scan_bsum, s));
-  HIP_TRY(rt_cand_scatter(&cp, s));
+  (void)slice;
+  HIP_TRY(rt_cand_scan_scatter(&cp, c->d_scan_bsum, s));
 #else
   tb = c->scan_tmp_bytes;
   HIP_TRY(rt_cand_scan(c->d_cand_visits, c->d_cand_off, slice, c->d_scan_tmp, &tb, s));
@@ -1771,20 +1774,19 @@ extern "C" int rt_hip_cand_produce(rt_hip_ctx* c, const rt_frame* f, int rank, i
   const int tbits = key_bits((size_t)tpr + 1);
   if (nranks > 256 || tbits + key_bits((size_t)nranks + 1) > 32)
     return rt_set_error(RT_EINVAL, "%d ranks x %u tiles per rank: routed keys exceed 32 bits", nranks, tpr);
-  HIP_TRY(rt_cand_route(c->d_cand_keys, total, cp.tiles_x, nranks, rt_blocks_x(cp.tiles_x, tb), tb, (uint32_t)tbits,
-                        cp.drop_key, async ? c->d_cand_ctr + 6 : nullptr, s));
+  // (the entries' routing is fused into the partition's count pass)
   HIP_TRY(rt_cand_route_globals(c->d_cand_global, nglobal, nranks, tpr, (uint32_t)tbits, c->d_cand_keys + total,
                                 c->d_cand_vals + total, s));
   const uint32_t n = total + nglobal * (uint32_t)nranks;
-  if ((size_t)nranks + 1 > c->rstart_cap) {
+  if ((size_t)nranks + 9 > c->rstart_cap) {  // the starts, then the build's counters
     (void)hipFree(c->d_rstart);
     (void)hipHostFree(c->h_rstart);
     c->d_rstart = nullptr;
     c->h_rstart = nullptr;
     c->rstart_cap = 0;
-    HIP_TRY(hipMalloc((void**)&c->d_rstart, ((size_t)nranks + 1) * sizeof(uint32_t)));
-    HIP_TRY(hipHostMalloc((void**)&c->h_rstart, ((size_t)nranks + 1) * sizeof(uint32_t), hipHostMallocDefault));
-    c->rstart_cap = (size_t)nranks + 1;
+    HIP_TRY(hipMalloc((void**)&c->d_rstart, ((size_t)nranks + 9) * sizeof(uint32_t)));
+    HIP_TRY(hipHostMalloc((void**)&c->h_rstart, ((size_t)nranks + 9) * sizeof(uint32_t), hipHostMallocDefault));
+    c->rstart_cap = (size_t)nranks + 9;
   }
   if (3 * (size_t)n + 1 > c->send_cap) {
     (void)hipFree(c->d_send);
@@ -1812,18 +1814,19 @@ extern "C" int rt_hip_cand_produce(rt_hip_ctx* c, const rt_frame* f, int rank, i
     rc = ensure_tmp(c, tmpb);
     if (rc) return rc;
     tmpb = c->scan_tmp_bytes;
-    HIP_TRY(rt_cand_part_count(c->d_cand_keys, n, (uint32_t)tbits, nranks, hist, s));
+    HIP_TRY(rt_cand_part_count(c->d_cand_keys, n, (uint32_t)tbits, nranks, hist, total, cp.tiles_x,
+                               rt_blocks_x(cp.tiles_x, tb), tb, cp.drop_key, async ? c->d_cand_ctr + 6 : nullptr, s));
     HIP_TRY(rt_cand_scan(hist, hoff, (uint32_t)(nh - 1), c->d_scan_tmp, &tmpb, s));
   }
   HIP_TRY(rt_cand_part_scatter(c->d_cand_keys, c->d_cand_vals, c->d_cand_skip, n, (uint32_t)tbits, nranks, hoff,
-                               c->d_rstart, c->d_send, s));
-  HIP_TRY(hipMemcpyAsync(c->h_rstart, c->d_rstart, ((size_t)nranks + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                               c->d_rstart, c->d_send, c->d_cand_ctr, s));
+  // the per-rank starts and the build's counters in one read-back
+  HIP_TRY(hipMemcpyAsync(c->h_rstart, c->d_rstart, ((size_t)nranks + 9) * sizeof(uint32_t), hipMemcpyDeviceToHost,
                          s));
-  if (async) HIP_TRY(hipMemcpyAsync(c->h_cand, c->d_cand_ctr, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
-  if (async && (c->h_cand[7] || c->h_cand[6] != c->pknown.total || c->h_cand[1] != c->pknown.nglobal ||
-                c->h_cand[2] != c->pknown.nbig || c->h_cand[4] != c->pknown.nitems ||
-                c->h_cand[5] != c->pknown.over)) {
+  const uint32_t* hc = c->h_rstart + nranks + 1;  // ctr[0 .. 7]
+  if (async && (hc[7] || hc[6] != c->pknown.total || hc[1] != c->pknown.nglobal || hc[2] != c->pknown.nbig ||
+                hc[4] != c->pknown.nitems || hc[5] != c->pknown.over)) {
     c->pknown.valid = 0;  // not this slice's sizes after all: build it with the read-back
     return rt_hip_cand_produce(c, f, rank, nranks, counts, nglobal_out, stream);
   }
