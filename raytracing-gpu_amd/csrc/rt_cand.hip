@@ -950,6 +950,9 @@ constexpr int kBigWaves = 4096;
 #ifndef RT_SORT_BITS
 #define RT_SORT_BITS 9
 #endif
+#ifndef RT_SORT_MERGE_LIMIT
+#define RT_SORT_MERGE_LIMIT (1u << 16)
+#endif
 
 // Pass 0: the float fast path over every prim; flags the prims it cannot
 // prove safe (visits[prim] = 1), which an exclusive scan and scatter_kernel
@@ -2247,10 +2250,14 @@ extern "C" hipError_t rt_cand_sort(uint32_t* keys_in, uint32_t* keys_out, uint32
 #if RT_SORT_BITS
   // digits of RT_SORT_BITS bits per onesweep place (rocPRIM's gfx950 u32/u32
   // tuning otherwise: 8 bits, so C5's 17-bit tile keys take three places)
+  // onesweep from RT_SORT_MERGE_LIMIT items up (rocPRIM's default switches
+  // at 2^20: a consume of ~1 M entries at N = 8 went through 9 merge passes,
+  // 0.14 ms)
   using cfg = rocprim::radix_sort_config<
       rocprim::default_config, rocprim::default_config,
       rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 16>, rocprim::kernel_config<1024, 16>,
-                                          RT_SORT_BITS, rocprim::block_radix_rank_algorithm::match>>;
+                                          RT_SORT_BITS, rocprim::block_radix_rank_algorithm::match>,
+      RT_SORT_MERGE_LIMIT>;
   return rocprim::radix_sort_pairs<cfg>(temp, *temp_bytes, keys_in, keys_out, vals_in, vals_out, (size_t)n,
                                         begin_bit, end_bit, s);
 #else

@@ -33,6 +33,20 @@ def main():
         end = int(rows[b1 - 1]["End_Timestamp"])
         print(f"span {(end - t0) / 1e3:.1f} us, kernels {busy / 1e3:.1f} us, next call at "
               f"{(int(rows[b1]['Start_Timestamp']) - t0) / 1e3:.1f} us")
+    consume_view(rows, names)
+
+
+def consume_view(rows, names):
+    u = [i for i, n in enumerate(names) if "unpack_kernel" in n]
+    if len(u) < 3:
+        return
+    b0, b1 = u[len(u) // 2], u[len(u) // 2 + 1]
+    t0 = int(rows[b0]["Start_Timestamp"])
+    print("-- consume (rank 0)")
+    for i in range(b0, b1):
+        s, e = int(rows[i]["Start_Timestamp"]), int(rows[i]["End_Timestamp"])
+        print(f"{(s - t0) / 1e3:8.1f} {(e - s) / 1e3:7.1f}  {names[i]}")
+    print(f"span {(int(rows[b1 - 1]['End_Timestamp']) - t0) / 1e3:.1f} us")
 
 
 if __name__ == "__main__":

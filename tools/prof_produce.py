@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--trace", help="kernel_trace.csv of an earlier run: per-kernel breakdown")
     ap.add_argument("--calls", type=int, default=0, help="produce calls in that trace")
+    ap.add_argument("--consume", action="store_true", help="then rank 0's consume, --steps times")
     a = ap.parse_args()
     if a.trace:
         print(json.dumps(summarize(a.trace, a.calls), indent=1))
@@ -54,6 +55,26 @@ def main():
             ts.append((time.perf_counter() - t0) * 1e3)
         med.append(round(sorted(ts)[len(ts) // 2], 3))
     print(json.dumps({"n": a.n, "produce_ms": med, "max": max(med), "calls": a.n * (a.steps + 1)}), flush=True)
+    if a.consume:  # rank 0's consume of what every producer routed to it, repeated
+        import ctypes as C
+        import numpy as np
+        L = rtgpu.lib()
+        blocks, g = [], 0
+        for r in range(a.n):
+            counts, ng = ctx.cand_produce(f, r, a.n)
+            ptr, m = ctx.cand_send_buffer()
+            host = np.empty((max(m, 1), 3), np.uint32)
+            if m:
+                assert L.rt_hip_memcpy_d2h(host.ctypes.data_as(C.c_void_p), C.c_void_p(ptr), m * 12) == 0
+            blocks.append(host[:counts[0]])
+            g += ng
+        recv = np.ascontiguousarray(np.concatenate(blocks))
+        dr = C.c_void_p()
+        assert L.rt_hip_malloc(0, max(recv.nbytes, 16), C.byref(dr)) == 0
+        assert L.rt_hip_memcpy_h2d(dr, recv.ctypes.data_as(C.c_void_p), recv.nbytes) == 0
+        for _ in range(a.steps):  # (asynchronous: the kernel trace times them)
+            ctx.cand_consume(f, 0, a.n, dr.value, len(recv), g)
+        print(json.dumps({"consume_entries": int(len(recv)), "consume_calls": a.steps}), flush=True)
 
 
 if __name__ == "__main__":
