@@ -151,8 +151,9 @@ extern "C" hipError_t rt_cand_fill_tail(uint32_t* keys, const uint32_t* total_de
                                         hipStream_t s);
 extern "C" hipError_t rt_cand_entry_skip(const uint32_t* cand, const float* skip, float* out,
                                          uint32_t n, const uint32_t* n_dev, hipStream_t s);
+// snap (optional): the build's counters, ctr[0 .. 7] copied to [16 .. 23]
 extern "C" hipError_t rt_cand_bounds(const uint32_t* keys, uint32_t n, uint32_t* start,
-                                     uint32_t ntiles, hipStream_t s);
+                                     uint32_t ntiles, uint32_t* snap, hipStream_t s);
 // Triangle-parallel multi-GPU lists (rt_hip_cand_produce / rt_hip_cand_consume):
 // a whole-frame build (one rank, scanline tiles) of a slice of the prims, its
 // entries routed to the N-rank tile map.  route: key = scanline tile ->
@@ -182,12 +183,15 @@ extern "C" hipError_t rt_cand_part_scatter(const uint32_t* keys, const uint32_t*
                                            uint32_t n, uint32_t tbits, int nranks, const uint32_t* off,
                                            uint32_t* start, uint32_t* out, const uint32_t* ctr, hipStream_t s);
 // Stable compaction of the entries whose key is not drop_key into
-// keys_out / vals_out (at most cap; beyond it *ctr7 = 1): per-wave counts
+// keys_out / vals_out (at most cap; beyond it *ctr7 = 1; a shorter result's
+// tail up to cap written as drop_key; n_dev (optional): only the first
+// *n_dev of the n entries are the build's): per-wave counts
 // (cnt, rt_cand_part_waves(n) + 1 words) -> exclusive scan (off, off[nw] =
 // the kept total) -> scatter.  tmp == NULL: *tmp_bytes = the scan's need.
-extern "C" hipError_t rt_cand_compact(const uint32_t* keys, const uint32_t* vals, uint32_t n, uint32_t drop_key,
-                                      uint32_t cap, uint32_t* cnt, uint32_t* off, void* tmp, size_t* tmp_bytes,
-                                      uint32_t* keys_out, uint32_t* vals_out, uint32_t* ctr7, hipStream_t s);
+extern "C" hipError_t rt_cand_compact(const uint32_t* keys, const uint32_t* vals, uint32_t n, const uint32_t* n_dev,
+                                      uint32_t drop_key, uint32_t cap, uint32_t* cnt, uint32_t* off, void* tmp,
+                                      size_t* tmp_bytes, uint32_t* keys_out, uint32_t* vals_out, uint32_t* ctr7,
+                                      hipStream_t s);
 extern "C" hipError_t rt_cand_unpack(const uint32_t* in, uint32_t n, uint32_t ntiles, uint32_t tpr, uint32_t* keys,
                                      uint32_t* idx, hipStream_t s);
 extern "C" hipError_t rt_cand_gather(const uint32_t* in, const uint32_t* idx, uint32_t n, uint32_t* cand,

@@ -1407,8 +1407,11 @@ __global__ __launch_bounds__(256) void prim_leaf_kernel(const float4* node, uint
 // the entries with a tile (the refinement's dropped entries, key ntiles, sort
 // after them)
 __global__ __launch_bounds__(256) void bounds_kernel(const uint32_t* keys, uint32_t n, uint32_t* start,
-                                                     uint32_t ntiles) {
+                                                     uint32_t ntiles, uint32_t* snap) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  // an asynchronous build's counters ctr[0 .. 7] -> ctr[16 .. 23] for
+  // rt_hip_stats, after every pass that may set its overflow flag
+  if (snap && t < 8u) snap[16 + t] = snap[t];
   if (t > ntiles) return;
   uint32_t lo = 0, hi = n;
   while (lo < hi) {
@@ -1563,14 +1566,15 @@ __global__ __launch_bounds__(64) void part_scatter_kernel(const uint32_t* keys, 
 // order at off[w] + their rank in the wave; past cap they are not written
 // and ctr7 is set (the host sized cap from the same frame's earlier build).
 __global__ __launch_bounds__(64) void compact_count_kernel(const uint32_t* keys, uint32_t n, uint32_t drop_key,
-                                                           uint32_t* cnt) {
+                                                           uint32_t* cnt, const uint32_t* n_dev) {
   const int lane = threadIdx.x;
   const uint32_t e0 = blockIdx.x * kPartChunk;
+  const uint32_t m = n_dev && *n_dev < n ? *n_dev : n;  // the build's own entries (the rest: unused)
   uint32_t c = 0;
 #pragma unroll
   for (uint32_t t = 0; t < kPartSteps; t++) {
     const uint32_t i = e0 + t * 64u + (uint32_t)lane;
-    c += (i < n && keys[i] != drop_key) ? 1u : 0u;
+    c += (i < m && keys[i] != drop_key) ? 1u : 0u;
   }
   for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
   if (lane == 0) cnt[blockIdx.x] = c;
@@ -1579,16 +1583,22 @@ __global__ __launch_bounds__(64) void compact_count_kernel(const uint32_t* keys,
 
 __global__ __launch_bounds__(64) void compact_scatter_kernel(const uint32_t* keys, const uint32_t* vals, uint32_t n,
                                                              uint32_t drop_key, const uint32_t* off, uint32_t cap,
-                                                             uint32_t* keys_out, uint32_t* vals_out, uint32_t* ctr7) {
+                                                             uint32_t* keys_out, uint32_t* vals_out, uint32_t* ctr7,
+                                                             const uint32_t* n_dev) {
   const int lane = threadIdx.x;
   const uint32_t e0 = blockIdx.x * kPartChunk;
   const uint64_t lt = (1ull << lane) - 1ull;
+  const uint32_t m = n_dev && *n_dev < n ? *n_dev : n;
+  // fewer kept entries than cap -- never expected for the same frame -- leave
+  // a tail: dropped (every workgroup a strided part of it)
+  for (uint32_t i = off[gridDim.x] + blockIdx.x * 64u + (uint32_t)lane; i < cap; i += gridDim.x * 64u)
+    keys_out[i] = drop_key;
   uint32_t k[kPartSteps], v[kPartSteps];
 #pragma unroll
   for (uint32_t t = 0; t < kPartSteps; t++) {
     const uint32_t i = e0 + t * 64u + (uint32_t)lane;
-    k[t] = i < n ? keys[i] : drop_key;
-    v[t] = i < n ? vals[i] : 0u;
+    k[t] = i < m ? keys[i] : drop_key;
+    v[t] = i < m ? vals[i] : 0u;
   }
   uint32_t base = off[blockIdx.x];
 #pragma unroll
@@ -1781,7 +1791,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_apply_kernel(const uint32_t
 // Exclusive scan of in[0 .. n] (n + 1 values, out[n] = their sum) in one
 // workgroup, for the short scans between list passes (the big footprints'
 // items, a partition's per-wave counts): one launch instead of rocPRIM's two.
-constexpr uint32_t kSmallScanThreads = 1024, kSmallScanPer = 16;
+constexpr uint32_t kSmallScanThreads = 1024, kSmallScanPer = 32;
 constexpr uint32_t kSmallScanMax = kSmallScanThreads * kSmallScanPer;
 
 __global__ __launch_bounds__(kSmallScanThreads) void scan_small_kernel(const uint32_t* __restrict__ in,
@@ -2275,9 +2285,9 @@ extern "C" hipError_t rt_cand_entry_skip(const uint32_t* cand, const float* skip
 }
 
 extern "C" hipError_t rt_cand_bounds(const uint32_t* keys, uint32_t n, uint32_t* start,
-                                     uint32_t ntiles, hipStream_t s) {
+                                     uint32_t ntiles, uint32_t* snap, hipStream_t s) {
   hipLaunchKernelGGL(rtc::bounds_kernel, dim3((ntiles + 1 + 255) / 256), dim3(256), 0, s, keys, n,
-                     start, ntiles);
+                     start, ntiles, snap);
   return hipGetLastError();
 }
 
@@ -2291,17 +2301,18 @@ extern "C" hipError_t rt_cand_route_globals(const uint32_t* global, uint32_t ngl
   return hipGetLastError();
 }
 
-extern "C" hipError_t rt_cand_compact(const uint32_t* keys, const uint32_t* vals, uint32_t n, uint32_t drop_key,
-                                      uint32_t cap, uint32_t* cnt, uint32_t* off, void* tmp, size_t* tmp_bytes,
-                                      uint32_t* keys_out, uint32_t* vals_out, uint32_t* ctr7, hipStream_t s) {
+extern "C" hipError_t rt_cand_compact(const uint32_t* keys, const uint32_t* vals, uint32_t n, const uint32_t* n_dev,
+                                      uint32_t drop_key, uint32_t cap, uint32_t* cnt, uint32_t* off, void* tmp,
+                                      size_t* tmp_bytes, uint32_t* keys_out, uint32_t* vals_out, uint32_t* ctr7,
+                                      hipStream_t s) {
   const uint32_t nw = rt_cand_part_waves(n);
   if (!tmp) return rt_cand_scan(cnt, off, nw, nullptr, tmp_bytes, s);
-  if (nw == 0) return hipMemsetAsync(off, 0, sizeof(uint32_t), s);
-  hipLaunchKernelGGL(rtc::compact_count_kernel, dim3(nw), dim3(64), 0, s, keys, n, drop_key, cnt);
+  if (nw == 0) return hipErrorInvalidValue;  // (the host compacts only a build with entries)
+  hipLaunchKernelGGL(rtc::compact_count_kernel, dim3(nw), dim3(64), 0, s, keys, n, drop_key, cnt, n_dev);
   hipError_t e = rt_cand_scan(cnt, off, nw, tmp, tmp_bytes, s);  // off[nw] = the kept entries
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(rtc::compact_scatter_kernel, dim3(nw), dim3(64), 0, s, keys, vals, n, drop_key, off, cap,
-                     keys_out, vals_out, ctr7);
+                     keys_out, vals_out, ctr7, n_dev);
   return hipGetLastError();
 }
 

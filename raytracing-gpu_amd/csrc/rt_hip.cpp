@@ -1566,11 +1566,10 @@ static int cand_build(rt_hip_ctx* c, CandParams& cp, hipStream_t s, uint32_t glo
       HIP_TRY(rt_cand_big(&cp, known->nbig, s));
     else
       HIP_TRY(rt_cand_big_items(&cp, known->nitems, 1, s));
-    // (a produce's route_kernel drops the unused tail itself)
-    if (!glob_copies) HIP_TRY(rt_cand_fill_tail(c->d_cand_keys, c->d_cand_ctr + 6, known->total, cp.drop_key, s));
-    // this frame's counters for rt_hip_stats, in stream order, where no build writes
-    if (!glob_copies) HIP_TRY(hipMemcpyAsync(c->d_cand_ctr + 16, c->d_cand_ctr, 8 * sizeof(uint32_t),
-                                             hipMemcpyDeviceToDevice, s));
+    // (entries past the build's own total, ctr[6] -- never expected -- are
+    // left to the caller: cand_prepare drops them before the sort, a
+    // produce's partition routes them as dropped; and cand_prepare's
+    // bounds_kernel snapshots the counters for rt_hip_stats)
     *total_out = known->total;  // the sort's length
     *nglobal_out = known->nglobal;  // (the render reads the count on the device, ctr[1])
     return RT_OK;
@@ -1658,7 +1657,7 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
     c->kept_ready = 1;
   }
   const bool compact = RT_COMPACT_LISTS && async && c->cand_refine && c->kept_ready &&
-                       c->kept_for.same(f, kp->rank, kp->nranks) && c->kept <= total;
+                       c->kept_for.same(f, kp->rank, kp->nranks) && c->kept <= total && total > 0;
   if (compact) {
     // the kept entries (stable) -> keys2 / d_cand, sorted back into keys /
     // vals, and the buffer pairs swapped so that the sorted ones are where
@@ -1675,29 +1674,30 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
     uint32_t* cnt = c->d_part;
     uint32_t* off = c->d_part + nw + 1;
     size_t tmpb = 0;
-    HIP_TRY(rt_cand_compact(c->d_cand_keys, c->d_cand_vals, total, (uint32_t)nt, c->kept, cnt, off, nullptr, &tmpb,
-                            c->d_cand_keys2, c->d_cand, c->d_cand_ctr + 7, s));
+    // (only the build's own entries, ctr[6]; fewer kept than last time --
+    // never expected -- leave a tail the scatter writes as dropped)
+    HIP_TRY(rt_cand_compact(c->d_cand_keys, c->d_cand_vals, total, c->d_cand_ctr + 6, (uint32_t)nt, c->kept, cnt, off,
+                            nullptr, &tmpb, c->d_cand_keys2, c->d_cand, c->d_cand_ctr + 7, s));
     rc = ensure_tmp(c, tmpb);
     if (rc) return rc;
     tmpb = c->scan_tmp_bytes;
-    HIP_TRY(rt_cand_compact(c->d_cand_keys, c->d_cand_vals, total, (uint32_t)nt, c->kept, cnt, off, c->d_scan_tmp,
-                            &tmpb, c->d_cand_keys2, c->d_cand, c->d_cand_ctr + 7, s));
-    // (fewer kept than last time -- never expected -- leaves a tail: dropped)
-    HIP_TRY(rt_cand_fill_tail(c->d_cand_keys2, off + nw, c->kept, (uint32_t)nt, s));
-    // the per-frame counters rt_hip_stats reads (the overflow flag was set after the snapshot)
-    HIP_TRY(hipMemcpyAsync(c->d_cand_ctr + 23, c->d_cand_ctr + 7, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    HIP_TRY(rt_cand_compact(c->d_cand_keys, c->d_cand_vals, total, c->d_cand_ctr + 6, (uint32_t)nt, c->kept, cnt, off,
+                            c->d_scan_tmp, &tmpb, c->d_cand_keys2, c->d_cand, c->d_cand_ctr + 7, s));
     rc = cand_sort(c, c->d_cand_keys2, c->d_cand_keys, c->d_cand, c->d_cand_vals, c->kept, nt + 1, s);
     if (rc) return rc;
     std::swap(c->d_cand_keys, c->d_cand_keys2);
     std::swap(c->d_cand_vals, c->d_cand);
     total = c->kept;
   } else {
+    // an asynchronous build's entries past its own total (never expected): dropped
+    if (async) HIP_TRY(rt_cand_fill_tail(c->d_cand_keys, c->d_cand_ctr + 6, total, (uint32_t)nt, s));
     // keys are tiles < nt, or nt for an entry the refinement dropped: nt + 1 keys
     rc = cand_sort(c, c->d_cand_keys, c->d_cand_keys2, c->d_cand_vals, c->d_cand, total, nt + 1, s);
     if (rc) return rc;
   }
   // start[nt] = the entries with a tile (the dropped ones sort after them)
-  HIP_TRY(rt_cand_bounds(c->d_cand_keys2, total, c->d_cand_start, (uint32_t)nt, s));
+  // (an asynchronous build's counters snapshot for rt_hip_stats, where no build writes)
+  HIP_TRY(rt_cand_bounds(c->d_cand_keys2, total, c->d_cand_start, (uint32_t)nt, async ? c->d_cand_ctr : nullptr, s));
   if (RT_COMPACT_LISTS && c->cand_refine && !compat && !c->kept_for.same(f, kp->rank, kp->nranks)) {
     // this frame's kept count, for its later builds (read back without waiting)
     if (!c->h_kept) HIP_TRY(hipHostMalloc((void**)&c->h_kept, sizeof(uint32_t), hipHostMallocDefault));
@@ -1869,7 +1869,7 @@ extern "C" int rt_hip_cand_consume(rt_hip_ctx* c, const rt_frame* f, int rank, i
   rc = cand_sort(c, c->d_cand_keys, c->d_cand_keys2, c->d_cand_vals, c->d_cand, (uint32_t)n, nt + 1, s);
   if (rc) return rc;
   const uint32_t total = (uint32_t)(n - nglobal);
-  HIP_TRY(rt_cand_bounds(c->d_cand_keys2, total, c->d_cand_start, (uint32_t)nt, s));
+  HIP_TRY(rt_cand_bounds(c->d_cand_keys2, total, c->d_cand_start, (uint32_t)nt, nullptr, s));
   // the spent unsorted keys take the skip bounds, the spent indices the prims
   HIP_TRY(rt_cand_gather(in, c->d_cand, (uint32_t)n, c->d_cand_vals, (float*)c->d_cand_keys, s));
   KParams kp;
