@@ -3,9 +3,9 @@
 
 A "step" renders one whole frame of the workload: every rank builds the
 frame's camera-ray candidate lists (per rank, or triangle-parallel with one
-all-to-all from N = 4) and renders its 8x8 tiles (4x4-tile blocks dealt
-round-robin, csrc/rt_tiles.h) through the C ABI of lib/librtgpu.so on torch's
-current stream, rank
+all-to-all from N = 4) and renders its 8x8 tiles (4x4-tile blocks, block
+(bx, by) to rank (bx + by) mod N, csrc/rt_tiles.h) through the C ABI of
+lib/librtgpu.so on torch's current stream, rank
 tile buffers are gathered to rank 0 with one RCCL gather (torch.distributed
 "nccl" backend = RCCL over xGMI), and rank 0 assembles the PPM-order float
 image.  Scene image and octree are built and uploaded before timing (inputs

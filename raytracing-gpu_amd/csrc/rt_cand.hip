@@ -1037,6 +1037,11 @@ __device__ __forceinline__ bool small_pack(const CandParams& p, const Footprint&
   return n <= kSmallEntries;
 }
 
+// the classification's leaf box loaded at its start instead of at its use
+// (A/B knob: lists 1.803 -> 1.816 ms at 128 VGPRs, profiles/r08_list_occupancy/)
+#ifndef RT_COUNT_LEAF_AHEAD
+#define RT_COUNT_LEAF_AHEAD 0
+#endif
 // Pass 1: classify the listed prims, keep each one's footprint and count the
 // tiles of the small ones (visits[j] for list entry j; visits is zero beyond
 // the list); big ones are queued for big_count_kernel.
@@ -1045,7 +1050,23 @@ __device__ __forceinline__ void count_one(const CandParams& p, uint32_t j) {
   const float* rec = (const float*)(p.tri + 3 * (size_t)prim);
   uint32_t visits = 0;
   Footprint fp;
+#if RT_COUNT_LEAF_AHEAD
+  // the leaf box in registers from the start: its loads (prim -> leaf ->
+  // box, a dependent pair) overlap the f64 bound instead of waiting at its end
+  // (no leaf map: an empty box, which no corner lies in -- the same verdicts
+  // as no box; one array either way keeps it in registers)
+  float4 b0 = make_float4(__builtin_inff(), __builtin_inff(), __builtin_inff(), 0.0f);
+  float4 b1 = make_float4(-__builtin_inff(), -__builtin_inff(), -__builtin_inff(), 0.0f);
+  if (p.prim_leaf) {
+    const float4* nb = p.node + 2 * (size_t)p.prim_leaf[prim];
+    b0 = nb[0];
+    b1 = nb[1];
+  }
+  const float lbox[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+  const float* lb = lbox;
+#else
   const float* lb = p.prim_leaf ? (const float*)(p.node + 2 * (size_t)p.prim_leaf[prim]) : nullptr;
+#endif
   const int c = classify(p, rec, lb, fp);
   if (c == GLOBAL) {
     p.global[atomicAdd(p.ctr + 1, 1u)] = prim;

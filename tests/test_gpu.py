@@ -559,13 +559,16 @@ def test_triangle_parallel_lists_match_per_rank(gpu, nranks, accel):
     assert_bitexact(t2, t_ref, "per-rank build after a consumed frame")
 
 
-@pytest.mark.parametrize("nranks", [4, 8])
-def test_cand_exchange_local_matches_per_rank(gpu, nranks):
+@pytest.mark.parametrize("nranks,grid", [(3, 6), (4, 6), (8, 6), (16, 1)])
+def test_cand_exchange_local_matches_per_rank(gpu, nranks, grid):
     """the exchange rt_raytrace_multi makes over RCCL (from 4
     GPUs up), driven with N contexts on one GPU and the device-memcpy
     transport: every rank's render from the exchanged lists equals its render
-    from its own per-rank lists, bit for bit, with the same entry count."""
-    s = gpu.Scene.synthetic(6, 6, 9776, seed=0x5EED, width=960, height=540)
+    from its own per-rank lists, bit for bit, with the same entry count.
+    Producers take interleaved blocks of 1,024 prims: 3 ranks (the blocks not
+    a multiple of N), and one sphere (9,778 prims: 10 blocks) over 16 ranks,
+    where 6 producers have no prims at all."""
+    s = gpu.Scene.synthetic(grid, grid, 9776, seed=0x5EED, width=960, height=540)
     f = s.frame()
     ctxs = [gpu.Context(s, "octree_gpu") for _ in range(nranks)]
     ref = gpu.Context(s, "octree_gpu")
@@ -573,7 +576,7 @@ def test_cand_exchange_local_matches_per_rank(gpu, nranks):
     for d in range(nranks):
         t_ext, st_ext = _tiles_of_rank(ctxs[d], f, d, nranks)
         t_ref, st_ref = _tiles_of_rank(ref, f, d, nranks)
-        assert st_ext["cand_entries"] == st_ref["cand_entries"] > 0, d
+        assert st_ext["cand_entries"] == st_ref["cand_entries"], d
         assert_bitexact(t_ext, t_ref, f"rank {d}/{nranks}: exchanged vs per-rank lists")
         assert (st_ext["closest"], st_ext["shadow"]) == (st_ref["closest"], st_ref["shadow"])
     with pytest.raises(gpu.RtError):

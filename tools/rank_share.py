@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Per-rank cost of an N-way split on ONE GPU (not part of the product).
 
-Renders rank r of an nranks-way split of the C5 frame (4x4-tile blocks dealt
-round robin, csrc/rt_tiles.h; the work one GPU does in an N-GPU run, minus
+Renders rank r of an nranks-way split of the C5 frame (4x4-tile blocks, block
+(bx, by) to rank (bx + by) mod N, csrc/rt_tiles.h; the work one GPU does in an N-GPU run, minus
 the gather) and reports the HIP-event times of its candidate lists and its
 three render kernels, for the strong-scaling estimate in DESIGN.md §7.
 
