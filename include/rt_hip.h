@@ -431,6 +431,13 @@ int rt_raytrace(const char *input, const char *output);
 int rt_raytrace_multi(const char *input, const char *output, int ngpus, int accel,
                       rt_stats *stats, double *render_ms);
 
+/* rt_raytrace_multi with rank g on device devices[g].  Distinct devices: as
+ * rt_raytrace_multi (RCCL).  A device shared by several ranks (tests running
+ * N ranks on one GPU): the same frame with device memcpys in place of the
+ * RCCL calls (the candidate lists' exchange from 4 ranks up, the gather). */
+int rt_raytrace_multi_dev(const char *input, const char *output, int ngpus, const int *devices, int accel,
+                          rt_stats *stats, double *render_ms);
+
 #ifdef __cplusplus
 }
 #endif

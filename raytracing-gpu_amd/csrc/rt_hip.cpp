@@ -2789,9 +2789,25 @@ extern "C" int rt_hip_cand_exchange_local(rt_hip_ctx** ctx, int n, const rt_fram
 #define RT_MULTI_PARTITION_MIN 4
 #endif
 
+extern "C" int rt_raytrace_multi_dev(const char* input, const char* output, int ngpus, const int* devices,
+                                     int accel, rt_stats* stats, double* render_ms);
+
 extern "C" int rt_raytrace_multi(const char* input, const char* output, int ngpus, int accel,
                                  rt_stats* stats, double* render_ms) {
-  if (!input || !output || ngpus < 1 || ngpus > 64) return rt_set_error(RT_EINVAL, "bad argument");
+  if (ngpus < 1 || ngpus > 64) return rt_set_error(RT_EINVAL, "bad argument");
+  std::vector<int> devs(ngpus);
+  for (int g = 0; g < ngpus; g++) devs[g] = g;
+  return rt_raytrace_multi_dev(input, output, ngpus, devs.data(), accel, stats, render_ms);
+}
+
+// Rank g on device devices[g].  Distinct devices: RCCL (the gather, and the
+// candidate lists' all-to-all from 4 ranks up).  A device used by several
+// ranks (a test running N ranks on one GPU): the same steps with device
+// memcpys (rt_hip_cand_exchange_local's transport, and a copy of each
+// rank's tile buffer into the gathered one).
+extern "C" int rt_raytrace_multi_dev(const char* input, const char* output, int ngpus, const int* devices,
+                                     int accel, rt_stats* stats, double* render_ms) {
+  if (!input || !output || !devices || ngpus < 1 || ngpus > 64) return rt_set_error(RT_EINVAL, "bad argument");
   rt_scene* scene = nullptr;
   int rc = rt_scene_load_svati(input, &scene);
   if (rc) return rc;
@@ -2814,7 +2830,12 @@ extern "C" int rt_raytrace_multi(const char* input, const char* output, int ngpu
   if (accel < 0) accel = choose_accel(scene);
   int ndev = 0;
   rc = rt_hip_device_count(&ndev);
-  if (!rc && ngpus > ndev) rc = rt_set_error(RT_ENODEV, "%d GPUs requested, %d present", ngpus, ndev);
+  bool shared = false;  // some device holds several ranks: memcpy transport, no RCCL
+  for (int g = 0; g < ngpus && !rc; g++) {
+    if (devices[g] < 0 || devices[g] >= ndev)
+      rc = rt_set_error(RT_ENODEV, "rank %d: device %d of %d present", g, devices[g], ndev);
+    for (int h = 0; h < g; h++) shared = shared || devices[h] == devices[g];
+  }
   std::vector<rt_hip_ctx*> ctx(ngpus, nullptr);
   std::vector<float*> d_tiles(ngpus, nullptr);
   std::vector<ncclComm_t> comms(ngpus, nullptr);
@@ -2829,26 +2850,23 @@ extern "C" int rt_raytrace_multi(const char* input, const char* output, int ngpu
   // every GPU builds its own scene image and octree at once
   if (!rc)
     rc = per_gpu(ngpus, [&](int g) {
-      int r = rt_hip_create(g, scene, accel, &ctx[g]);
-      if (!r) r = rt_hip_malloc(g, tile_floats * sizeof(float), (void**)&d_tiles[g]);
+      int r = rt_hip_create(devices[g], scene, accel, &ctx[g]);
+      if (!r) r = rt_hip_malloc(devices[g], tile_floats * sizeof(float), (void**)&d_tiles[g]);
       return r;
     });
-  if (!rc) rc = rt_hip_malloc(0, tile_floats * ngpus * sizeof(float), (void**)&d_gather);
-  if (!rc) rc = rt_hip_malloc(0, npx * 3 * sizeof(float), (void**)&d_rgb);
+  if (!rc) rc = rt_hip_malloc(devices[0], tile_floats * ngpus * sizeof(float), (void**)&d_gather);
+  if (!rc) rc = rt_hip_malloc(devices[0], npx * 3 * sizeof(float), (void**)&d_rgb);
   if (rc) goto out;
-  if (ngpus > 1) {
-    std::vector<int> devs(ngpus);
-    for (int g = 0; g < ngpus; g++) devs[g] = g;
-    NCCL_TRY(ncclCommInitAll(comms.data(), ngpus, devs.data()));
-  }
+  if (ngpus > 1 && !shared) NCCL_TRY(ncclCommInitAll(comms.data(), ngpus, devices));
   for (int g = 0; g < ngpus; g++) {
-    (void)hipSetDevice(g);
+    (void)hipSetDevice(devices[g]);
     (void)hipDeviceSynchronize();
   }
   t0 = std::chrono::steady_clock::now();
   if (ngpus >= RT_MULTI_PARTITION_MIN && ctx[0]->accel == RT_ACCEL_OCTREE && ctx[0]->d_node &&
       ctx[0]->exact_camera) {
-    rc = cand_exchange(ctx.data(), ngpus, &f, comms.data());  // each rank 1/N of the triangles, one all-to-all
+    // each rank 1/N of the triangles, one all-to-all
+    rc = cand_exchange(ctx.data(), ngpus, &f, shared ? nullptr : comms.data());
     if (rc) goto out;
   }
   rc = per_gpu(ngpus, [&](int g) {
@@ -2861,12 +2879,21 @@ extern "C" int rt_raytrace_multi(const char* input, const char* output, int ngpu
     return r;
   });
   if (rc) goto out;
-  if (ngpus > 1) {
+  if (ngpus > 1 && shared) {
+    // the ranks' tile buffers into the gathered one, rank-major (as ncclGather)
+    for (int g = 0; g < ngpus && !rc; g++) {
+      if (hipSetDevice(devices[g]) != hipSuccess || hipStreamSynchronize(ctx[g]->stream) != hipSuccess ||
+          hipMemcpyPeer(d_gather + (size_t)g * tile_floats, devices[0], d_tiles[g], devices[g],
+                        tile_floats * sizeof(float)) != hipSuccess)
+        rc = rt_set_error(RT_EHIP, "gather: rank %d", g);
+    }
+    if (!rc) rc = rt_hip_assemble(ctx[0], &f, d_gather, ngpus, d_rgb, nullptr);
+  } else if (ngpus > 1) {
     // one gather of every rank's tile buffer to device 0 over xGMI
     NCCL_TRY(ncclGroupStart());
     in_group = true;
     for (int g = 0; g < ngpus; g++) {
-      (void)hipSetDevice(g);
+      (void)hipSetDevice(devices[g]);
       NCCL_TRY(ncclGather(d_tiles[g], g == 0 ? d_gather : nullptr, tile_floats, ncclFloat, 0,
                           comms[g], ctx[g]->stream));
     }

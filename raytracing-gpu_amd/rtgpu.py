@@ -205,6 +205,8 @@ _PROTOS = [
     ("rt_raytrace_gpu", C.c_int, [C.c_char_p, C.c_char_p, C.c_int]),
     ("rt_raytrace_multi", C.c_int, [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.POINTER(Stats),
                                     C.POINTER(C.c_double)]),
+    ("rt_raytrace_multi_dev", C.c_int, [C.c_char_p, C.c_char_p, C.c_int, C.POINTER(C.c_int), C.c_int,
+                                        C.POINTER(Stats), C.POINTER(C.c_double)]),
 ]
 
 _lib = None
@@ -714,6 +716,18 @@ def raytrace_gpu(input_path, output_path, accel=None):
     a = -1 if accel is None else (ACCEL[accel] if isinstance(accel, str) else accel)
     _check(lib().rt_raytrace_gpu(os.fsencode(input_path), os.fsencode(output_path), a),
            "rt_raytrace_gpu")
+
+
+def raytrace_devices(input_path, output_path, devices, accel=None):
+    """rt_raytrace_multi_dev: rank g on device devices[g] (a device shared by
+    several ranks: memcpy transport in place of RCCL); (stats, render_ms)."""
+    st = Stats()
+    ms = C.c_double(0)
+    a = -1 if accel is None else (ACCEL[accel] if isinstance(accel, str) else accel)
+    devs = (C.c_int * len(devices))(*devices)
+    _check(lib().rt_raytrace_multi_dev(os.fsencode(input_path), os.fsencode(output_path), len(devices), devs, a,
+                                       C.byref(st), C.byref(ms)), "rt_raytrace_multi_dev")
+    return st.as_dict(), ms.value
 
 
 def raytrace(input_path, output_path, gpus=1, accel=None):

@@ -158,6 +158,26 @@ def test_raytrace_multi_one_gpu_md5(gpu, scene_dir, tmp_path, manifest):
         assert st["closest"] == case["closest"] and st["shadow"] == case["shadow"], case_id(case)
 
 
+@pytest.mark.parametrize("nranks", [3, 4, 8])
+def test_raytrace_multi_ranks_on_one_gpu(gpu, scene_dir, tmp_path, manifest, nranks):
+    """the drop-in N-GPU entry itself on one GPU --
+    rt_raytrace_multi_dev with every rank on device 0 runs the same frame as
+    rt_raytrace_multi (per-rank octrees and renders, from 4 ranks the
+    triangle-parallel candidate lists and their exchange, the gather and the
+    assemble) with device memcpys in place of RCCL, and writes the
+    reference's exact bytes."""
+    for case in manifest:
+        if case["scene"] not in ("island_smooth", "spheres", "car-on-road"):
+            continue
+        sv = tmp_path / f"{case['scene']}_{case['width']}.svati"
+        _with_camera_size(os.path.join(scene_dir, case["scene"] + ".svati"), sv, case["width"],
+                          case["height"])
+        out = tmp_path / "o.ppm"
+        st, _ = gpu.raytrace_devices(str(sv), str(out), [0] * nranks)
+        assert hashlib.md5(out.read_bytes()).hexdigest() == case["ppm_md5"], (case_id(case), nranks)
+        assert st["closest"] == case["closest"] and st["shadow"] == case["shadow"], case_id(case)
+
+
 @pytest.mark.parametrize("nranks", [2, 3, 8])
 def test_tile_partition_gather_assemble(gpu, scene_dir, nranks, manifest):
     """Rank-sharded renders + rank-major gather + assemble == the single image."""
