@@ -1811,36 +1811,47 @@ __global__ __launch_bounds__(kScanThreads) void scan_apply_kernel(const uint32_t
 
 // Exclusive scan of in[0 .. n] (n + 1 values, out[n] = their sum) in one
 // workgroup, for the short scans between list passes (the big footprints'
-// items, a partition's per-wave counts): one launch instead of rocPRIM's two.
+// items, a partition's per-wave counts, a rank's work order): one launch
+// instead of rocPRIM's two.  Wave w owns a contiguous segment of the values,
+// loaded and stored lane-consecutive (coalesced) in steps of 64, its lanes'
+// values held in registers; a wave scan per step with a running carry, the
+// 16 waves' totals combined through LDS.
 constexpr uint32_t kSmallScanThreads = 1024, kSmallScanPer = 32;
+constexpr uint32_t kSmallScanWaves = kSmallScanThreads / 64;
 constexpr uint32_t kSmallScanMax = kSmallScanThreads * kSmallScanPer;
 
 __global__ __launch_bounds__(kSmallScanThreads) void scan_small_kernel(const uint32_t* __restrict__ in,
                                                                        uint32_t* __restrict__ out, uint32_t n) {
-  __shared__ uint32_t wsum[kSmallScanThreads / 64];
-  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
-  const uint32_t m = n + 1u, per = (m + kSmallScanThreads - 1u) / kSmallScanThreads;
-  const uint32_t i0 = t * per;
-  uint32_t v[kSmallScanPer], run = 0;
+  __shared__ uint32_t wsum[kSmallScanWaves];
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint32_t m = n + 1u;
+  const uint32_t seg = ((m + kSmallScanWaves - 1u) / kSmallScanWaves + 63u) & ~63u;  // per wave, whole steps
+  const uint32_t base = wv * seg, steps = seg / 64u;
+  uint32_t v[kSmallScanPer], tot = 0;
 #pragma unroll
   for (uint32_t k = 0; k < kSmallScanPer; k++) {
-    v[k] = (k < per && i0 + k < m) ? in[i0 + k] : 0u;
-    run += v[k];
+    const uint32_t i = base + k * 64u + lane;
+    v[k] = (k < steps && i < m) ? in[i] : 0u;
+    tot += v[k];
   }
-  uint32_t inc = run;
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(inc, o, 64);
-    if ((int)lane >= o) inc += y;
-  }
-  if (lane == 63u) wsum[wv] = inc;
+  for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
+  if (lane == 0) wsum[wv] = tot;
   __syncthreads();
-  uint32_t before = 0;
-  for (uint32_t k = 0; k < wv; k++) before += wsum[k];
-  uint32_t pre = before + inc - run;
+  uint32_t carry = 0;
+  for (uint32_t k = 0; k < wv; k++) carry += wsum[k];
 #pragma unroll
   for (uint32_t k = 0; k < kSmallScanPer; k++) {
-    if (k < per && i0 + k < m) out[i0 + k] = pre;
-    pre += v[k];
+    if (k < steps) {  // (uniform)
+      uint32_t inc = v[k];
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o, 64);
+        if ((int)lane >= o) inc += y;
+      }
+      const uint32_t i = base + k * 64u + lane;
+      if (i < m) out[i] = carry + inc - v[k];
+      carry += __shfl(inc, 63, 64);
+    }
   }
 }
 

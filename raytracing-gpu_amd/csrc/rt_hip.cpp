@@ -2747,9 +2747,11 @@ static int cand_exchange(rt_hip_ctx* const* ctx, int n, const rt_frame* f, ncclC
       for (int r = 0; r < n && !rc; r++) {
         size_t so = 0;
         for (int k = 0; k < d; k++) so += counts[r][k];
+        // on the receiver's stream, so its consume is ordered after the copy
+        // (a device-to-device hipMemcpyPeer may return before it completes)
         if (counts[r][d] &&
-            hipMemcpyPeer(recv[d] + 3 * ro, ctx[d]->device, ctx[r]->d_send + 3 * so, ctx[r]->device,
-                          (size_t)counts[r][d] * 12) != hipSuccess)
+            hipMemcpyPeerAsync(recv[d] + 3 * ro, ctx[d]->device, ctx[r]->d_send + 3 * so, ctx[r]->device,
+                               (size_t)counts[r][d] * 12, ctx[d]->stream) != hipSuccess)
           rc = rt_set_error(RT_EHIP, "exchange: %d -> %d", r, d);
         ro += counts[r][d];
       }
@@ -2882,9 +2884,10 @@ extern "C" int rt_raytrace_multi_dev(const char* input, const char* output, int 
   if (ngpus > 1 && shared) {
     // the ranks' tile buffers into the gathered one, rank-major (as ncclGather)
     for (int g = 0; g < ngpus && !rc; g++) {
+      // (on rank 0's stream: the assemble that follows waits for the copies)
       if (hipSetDevice(devices[g]) != hipSuccess || hipStreamSynchronize(ctx[g]->stream) != hipSuccess ||
-          hipMemcpyPeer(d_gather + (size_t)g * tile_floats, devices[0], d_tiles[g], devices[g],
-                        tile_floats * sizeof(float)) != hipSuccess)
+          hipMemcpyPeerAsync(d_gather + (size_t)g * tile_floats, devices[0], d_tiles[g], devices[g],
+                             tile_floats * sizeof(float), ctx[0]->stream) != hipSuccess)
         rc = rt_set_error(RT_EHIP, "gather: rank %d", g);
     }
     if (!rc) rc = rt_hip_assemble(ctx[0], &f, d_gather, ngpus, d_rgb, nullptr);
