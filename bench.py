@@ -224,6 +224,23 @@ def latest_profile(workload, name):
     return None
 
 
+def frame_checked(ctx, rank, world, frame, steps, what):
+    """The device's per-frame checks of the frames rendered since the last
+    reset (rt_hip_frame_check): refuses (SystemExit, no JSON line) unless
+    every one was complete and exact by rt_hip_stats' conditions.  Returns
+    the frames' closest-hit + shadow queries summed over the ranks."""
+    fl, nf, qc, qs = ctx.frame_check()
+    has_tiles = rtgpu.rank_tile_count(frame.width, frame.height, rank, world) > 0
+    bad = fl != 0 or (has_tiles and nf != steps)
+    t = torch.tensor([1.0 if bad else 0.0, float(qc + qs)], dtype=torch.float64, device=f"cuda:{torch.cuda.current_device()}")
+    if world > 1:
+        dist.all_reduce(t)
+    if bad or t[0].item() > 0:
+        why = ", ".join(v for k, v in ctx.FRAME_FLAGS.items() if fl & k) or f"{nf} of {steps} frames checked"
+        raise SystemExit(f"[rank {rank}] {what} loop: incomplete frame(s) ({why}): no value printed")
+    return float(t[1].item())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -237,6 +254,10 @@ def main():
                     help="Mode B threads (default: this process's CPU share -- the box's "
                          "OMP_NUM_THREADS -- capped by os.cpu_count())")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--camera-pan", type=float, default=1.0,
+                    help="after the replay loop, time --steps more frames each with its own camera, "
+                         "panned this many pixels per step along the image's u axis (a new view every "
+                         "frame: nothing of an earlier identical frame is reused); 0 = skip")
     ap.add_argument("--cull-slack", type=float, default=None,
                     help="octree culling slack override (tuning; default = library default)")
     ap.add_argument("--camera-slack", type=float, default=None,
@@ -320,7 +341,7 @@ def main():
     part_ms = []  # host wall time of produce + exchange + consume enqueue, timed steps only
     timed = [False]
 
-    def exchange_lists():
+    def exchange_lists(frame):
         # triangle-parallel lists: this rank's slice of the triangles for
         # every rank's tiles -> all-to-all over RCCL -> this rank's lists
         counts, ng = ctx.cand_produce(frame, rank, world, sh)
@@ -335,10 +356,10 @@ def main():
             recv, g = send[0][:n], ng
         ctx.cand_consume(frame, rank, world, recv.data_ptr(), int(recv.shape[0]), g, sh)
 
-    def step():
+    def step(frame=frame):
         if partition:
             t = time.perf_counter()
-            exchange_lists()
+            exchange_lists(frame)
             if timed[0]:
                 part_ms.append((time.perf_counter() - t) * 1e3)
         ctx.render(frame, rank, world, tiles.data_ptr(), sh)
@@ -387,6 +408,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    ctx.frame_check()  # reset: the timed frames' own checks and query counts follow
     t0 = time.perf_counter()
     timed[0] = True
     for _ in range(args.steps):
@@ -398,7 +420,55 @@ def main():
     el = time.perf_counter() - t0
     ft = ctx.frame_times(min(args.steps, 1024))
     kt = ctx.kernel_times(min(args.steps, 1024))
+    # every timed frame complete: the conditions rt_hip_stats reports, checked
+    # on the device at the end of each frame (rt_hip_frame_check) -- a line is
+    # never printed for a timed region with an incomplete or unproven frame
+    timed_q = frame_checked(ctx, rank, world, frame, args.steps, "timed")
     ctx.set_timing(False)
+
+    # the same number of frames again, each with a new camera (panned
+    # --camera-pan pixels per step): a one-shot render or an animation
+    # reuses nothing of an earlier identical frame (the lists' sizes, kept
+    # count and work order are rebuilt with their read-backs)
+    fresh = None
+    if args.camera_pan > 0:
+        cam0 = rtgpu.Camera()
+        ctypes.pointer(cam0)[0] = scene.s.camera
+        fu = (frame.u.x, frame.u.y, frame.u.z)
+        frames = []
+        for k in range(1, args.steps + 1):
+            cam = rtgpu.Camera()
+            ctypes.pointer(cam)[0] = cam0
+            sh_ = args.camera_pan * k
+            cam.position.x = cam0.position.x + fu[0] * sh_
+            cam.position.y = cam0.position.y + fu[1] * sh_
+            cam.position.z = cam0.position.z + fu[2] * sh_
+            fr = rtgpu.Frame()
+            rtgpu._check(rtgpu.lib().rt_frame_from_camera(ctypes.byref(cam), ctypes.byref(fr)), "frame")
+            frames.append(fr)
+        ctx.set_timing(True)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        ctx.frame_check()
+        t1 = time.perf_counter()
+        for fr in frames:
+            step(fr)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el_f = time.perf_counter() - t1
+        ftf = ctx.frame_times(min(args.steps, 1024))
+        fresh_q = frame_checked(ctx, rank, world, frames[-1], args.steps, "fresh-camera")
+        ctx.set_timing(False)
+        tf = torch.tensor([el_f, sum(a for a, _ in ftf) / len(ftf)], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(tf, op=dist.ReduceOp.MAX)
+        el_f, lists_f = tf.tolist()
+        fresh = {"pan_px_per_step": args.camera_pan, "frames": args.steps,
+                 "ms_per_step": round(el_f / args.steps * 1e3, 3),
+                 "value": round(fresh_q / el_f / 1e6, 3),
+                 "candidate_lists_ms": round(lists_f, 3)}
     trace_ms = sum(a for a, _, _ in kt) / len(kt)
     shade_ms = sum(b for _, b, _ in kt) / len(kt)
     fold_ms = sum(c for _, _, c in kt) / len(kt)
@@ -418,7 +488,11 @@ def main():
     phase_share = ({k: round(v / sum(cyc), 4) for k, v in
                     zip(("camera_walk", "camera_candidates", "secondary_walks"), cyc)}
                    if sum(cyc) > 0 else None)
-    value = queries * args.steps / el / 1e6
+    # the timed frames' own queries (device-counted per frame, every rank)
+    if abs(timed_q - queries * args.steps) > 0.5:
+        raise SystemExit(f"timed frames made {timed_q:.0f} queries, {queries * args.steps:.0f} expected "
+                         "(the same frame every step): no value printed")
+    value = timed_q / el / 1e6
     # Algorithmic bytes per launch of each kernel (DESIGN.md §4 "Roofline"),
     # per rank: the records a wave pulls from the memory system (a record
     # several lanes load with one instruction counts once) plus the rays' and
@@ -520,6 +594,10 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(el / args.steps * 1e3, 3),
+            # the same number of frames with a new camera each (--camera-pan):
+            # nothing of an earlier identical frame reused
+            "ms_per_step_fresh": fresh["ms_per_step"] if fresh else None,
+            "fresh_camera": fresh,
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,

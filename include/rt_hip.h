@@ -195,6 +195,14 @@ int rt_hip_render(rt_hip_ctx *ctx, const rt_frame *frame, int rank, int nranks, 
  * RT_EINEXACT (a parity-breaking tuning knob below was active, or a
  * point-light shadow ray left from beyond the proven extent). */
 int rt_hip_stats(rt_hip_ctx *ctx, rt_stats *out);
+/* The same conditions checked on the device at the end of every render (no
+ * host wait), sticky until read: *flags = their OR since the last call (0 =
+ * every frame complete and exact; bits RT_FRAME_* of csrc/rt_kernels.h: 1
+ * hit-record overflow, 2 depth, 4 zero normal, 8 undecided exact shadow
+ * queries, 16 an asynchronous list build's overflow), *frames = renders
+ * checked, queries[0] / [1] = their closest-hit / shadow queries; all reset.
+ * For callers that render many frames between rt_hip_stats calls. */
+int rt_hip_frame_check(rt_hip_ctx *ctx, unsigned *flags, unsigned *frames, unsigned long long queries[2]);
 /* Octree culling slack, in units of 2^-24 x (ray-origin-to-scene distance):
  * boxes are grown by that much so a triangle the reference's float
  * Moller-Trumbore test accepts is never culled (DESIGN.md "Conservative

@@ -1238,7 +1238,15 @@ __global__ __launch_bounds__(RT_LIST_BLOCK) void emit_kernel(CandParams p) {
 // Pass 2b: one wave per big footprint, its tile rows over the lanes; a wave
 // prefix sum of the lanes' row counts places each lane's entries.
 __global__ __launch_bounds__(64) void big_kernel(CandParams p) {
-  if (!p.ctr[5]) return;  // big_item_kernel emits (an asynchronous build launches both)
+  // launched only when the build expects more than item_cap items (ctr[5]):
+  // read back, or -- an asynchronous build -- the same frame's earlier
+  // read-back build's shape.  A shape that differs on the device (never
+  // expected) means big_item_kernel was not launched: the frame is reported
+  // (ctr[7] -> RT_EHITBUF, built again with a read-back), never incomplete.
+  if (!p.ctr[5]) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) p.ctr[7] = 1u;
+    return;
+  }
   const int lane = threadIdx.x;
   const uint32_t nbig = p.ctr[2];
   for (uint32_t b = blockIdx.x; b < nbig; b += gridDim.x) {
@@ -1283,9 +1291,9 @@ __device__ __forceinline__ int kth_rank_col(const CandParams& p, int x0, int x1,
 // LDS.  Same (tile, prim) set as big_kernel; the sort orders it.
 // One workgroup per item.  CHECK (an asynchronous build: its grid is the
 // same frame's read-back build's) reads the item count and the over-cap flag
-// on the device: past item_cap (ctr[5]) big_kernel emits instead, and a count
-// the grid does not cover -- never expected -- sets ctr[7], so the frame is
-// reported rather than incomplete.  (The checks cost 16-18 VGPRs -- 4 waves
+// on the device: an over-cap flag (ctr[5]) the launch did not expect, or a
+// count the grid does not cover -- never expected -- sets ctr[7], so the
+// frame is reported rather than incomplete.  (The checks cost 16-18 VGPRs -- 4 waves
 // per SIMD instead of 5 -- so the read-back build's launch, whose grid is
 // the exact count, goes without them; a grid-stride loop over the items held
 // 118 VGPRs.)
@@ -1297,7 +1305,10 @@ __global__ __launch_bounds__(64) void big_item_kernel(CandParams p) {
   __shared__ int rty[64];
   const int lane = threadIdx.x;
   if (CHECK) {
-    if (p.ctr[5]) return;
+    if (p.ctr[5]) {  // more items than item_cap after all: big_kernel was not launched (as big_kernel)
+      if (blockIdx.x == 0 && lane == 0) p.ctr[7] = 1u;
+      return;
+    }
     const uint32_t n_items = p.wave_base[kBigWaves];
     if (blockIdx.x == 0 && lane == 0 && n_items > gridDim.x) p.ctr[7] = 1u;
     if (blockIdx.x >= n_items) return;

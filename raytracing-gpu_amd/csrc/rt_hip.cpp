@@ -59,6 +59,11 @@ extern "C" {
 #ifndef RT_COMPACT_LISTS
 #define RT_COMPACT_LISTS 1
 #endif
+// ... also in a fresh (non-asynchronous) build, with a read-back of the kept
+// count (A/B knob)
+#ifndef RT_COMPACT_FRESH
+#define RT_COMPACT_FRESH 1
+#endif
 #ifndef RT_COST_ORDER
 #define RT_COST_ORDER 1
 #endif
@@ -86,6 +91,10 @@ struct ListShape {
   uint32_t nbig = 0, nitems = 0, over = 0;   // the big-emission launch shape
   bool same(const rt_frame* f, int r, int n) const {
     return valid && rank == r && nranks == n && std::memcmp(&frame, f, sizeof *f) == 0;
+  }
+  // the same image size and rank split (the same tiles), any camera
+  bool same_grid(const rt_frame* f, int r, int n) const {
+    return valid && rank == r && nranks == n && frame.width == f->width && frame.height == f->height;
   }
   void set(const rt_frame* f, int r, int n) {
     valid = 1;
@@ -165,6 +174,7 @@ struct rt_hip_ctx {
   float2* d_node_mu = nullptr;
   uint4* d_oob = nullptr;       // exact-shadow mode: deferred off-box shadow queries
   uint32_t* d_oob_count = nullptr;
+  unsigned long long* d_frame_check = nullptr;  // KParams::frame_check: sticky per-frame checks (rt_hip_frame_check)
   uint32_t* d_sh_global = nullptr;
   uint32_t n_sh_global = 0;
   float sh_ulps = -1.0f;
@@ -383,6 +393,7 @@ extern "C" void rt_hip_destroy(rt_hip_ctx* c) {
   (void)hipFree(c->d_node_mu);
   (void)hipFree(c->d_oob);
   (void)hipFree(c->d_oob_count);
+  (void)hipFree(c->d_frame_check);
   (void)hipFree(c->d_sh_global);
   for (LBDevice* d : c->lb_dev) rt_lightbuf_free(d);
   (void)hipFree(c->d_lbuf);
@@ -1397,7 +1408,10 @@ static int cand_order(rt_hip_ctx* c, KParams* kp, size_t nt, uint32_t total, hip
   size_t tb = 0;
   // the item clocks of this frame's last trace on this context (its counters
   // are zeroed only by the render that follows this order)
-  const bool hist = c->cost_hist.same(f, rank, nranks) && c->d_item_cost && c->item_cost_cap >= 4 * nt;
+  // -- or of the last frame of the same size and rank split: a new camera
+  // (an animation's next frame) moves the costly tiles little, and the order
+  // is a schedule only (any order renders the same image)
+  const bool hist = c->cost_hist.same_grid(f, rank, nranks) && c->d_item_cost && c->item_cost_cap >= 4 * nt;
   const uint32_t* ic = hist ? c->d_item_cost : nullptr;
   const unsigned long long* cs = hist ? cost_sum_of(c) : nullptr;
   HIP_TRY(rt_cand_order(c->d_cand_start, (uint32_t)nt, total, c->d_order, c->d_order + nt + 1,
@@ -1656,9 +1670,17 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
     c->kept = *c->h_kept;
     c->kept_ready = 1;
   }
-  const bool compact = RT_COMPACT_LISTS && async && c->cand_refine && c->kept_ready &&
-                       c->kept_for.same(f, kp->rank, kp->nranks) && c->kept <= total && total > 0;
-  if (compact) {
+  // the kept entries compacted before the sort (the refinement drops ~55 %
+  // of them on C5): an asynchronous build takes the kept count of the same
+  // frame's earlier build; a fresh frame (a new camera: the build read its
+  // total back anyway) reads its own back after the compaction's scan -- one
+  // more short host wait instead of sorting the dropped entries
+  const bool compact_known = RT_COMPACT_LISTS && async && c->cand_refine && c->kept_ready &&
+                             c->kept_for.same(f, kp->rank, kp->nranks) && c->kept <= total && total > 0;
+  const bool compact_fresh = RT_COMPACT_LISTS && RT_COMPACT_FRESH && !async && !compat && !c->cand_store_fp &&
+                             c->cand_refine && total > 0;
+  bool kept_now = false;
+  if (compact_known || compact_fresh) {
     // the kept entries (stable) -> keys2 / d_cand, sorted back into keys /
     // vals, and the buffer pairs swapped so that the sorted ones are where
     // the uncompacted path leaves them
@@ -1676,18 +1698,31 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
     size_t tmpb = 0;
     // (only the build's own entries, ctr[6]; fewer kept than last time --
     // never expected -- leave a tail the scatter writes as dropped)
-    HIP_TRY(rt_cand_compact(c->d_cand_keys, c->d_cand_vals, total, c->d_cand_ctr + 6, (uint32_t)nt, c->kept, cnt, off,
+    const uint32_t cap = compact_known ? c->kept : total;
+    HIP_TRY(rt_cand_compact(c->d_cand_keys, c->d_cand_vals, total, c->d_cand_ctr + 6, (uint32_t)nt, cap, cnt, off,
                             nullptr, &tmpb, c->d_cand_keys2, c->d_cand, c->d_cand_ctr + 7, s));
     rc = ensure_tmp(c, tmpb);
     if (rc) return rc;
     tmpb = c->scan_tmp_bytes;
-    HIP_TRY(rt_cand_compact(c->d_cand_keys, c->d_cand_vals, total, c->d_cand_ctr + 6, (uint32_t)nt, c->kept, cnt, off,
+    HIP_TRY(rt_cand_compact(c->d_cand_keys, c->d_cand_vals, total, c->d_cand_ctr + 6, (uint32_t)nt, cap, cnt, off,
                             c->d_scan_tmp, &tmpb, c->d_cand_keys2, c->d_cand, c->d_cand_ctr + 7, s));
-    rc = cand_sort(c, c->d_cand_keys2, c->d_cand_keys, c->d_cand, c->d_cand_vals, c->kept, nt + 1, s);
+    uint32_t kept = cap;
+    if (compact_fresh) {  // off[nw] = the kept entries
+      if (!c->h_kept) HIP_TRY(hipHostMalloc((void**)&c->h_kept, sizeof(uint32_t), hipHostMallocDefault));
+      HIP_TRY(hipMemcpyAsync(c->h_kept, off + nw, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipStreamSynchronize(s));
+      kept = *c->h_kept;
+      if (kept > total) return rt_set_error(RT_EHIP, "compaction kept %u of %u entries", kept, total);
+      c->kept = kept;
+      c->kept_ready = 1;
+      c->kept_for.set(f, kp->rank, kp->nranks);
+      kept_now = true;
+    }
+    rc = cand_sort(c, c->d_cand_keys2, c->d_cand_keys, c->d_cand, c->d_cand_vals, kept, nt + 1, s);
     if (rc) return rc;
     std::swap(c->d_cand_keys, c->d_cand_keys2);
     std::swap(c->d_cand_vals, c->d_cand);
-    total = c->kept;
+    total = kept;
   } else {
     // an asynchronous build's entries past its own total (never expected): dropped
     if (async) HIP_TRY(rt_cand_fill_tail(c->d_cand_keys, c->d_cand_ctr + 6, total, (uint32_t)nt, s));
@@ -1698,7 +1733,7 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
   // start[nt] = the entries with a tile (the dropped ones sort after them)
   // (an asynchronous build's counters snapshot for rt_hip_stats, where no build writes)
   HIP_TRY(rt_cand_bounds(c->d_cand_keys2, total, c->d_cand_start, (uint32_t)nt, async ? c->d_cand_ctr : nullptr, s));
-  if (RT_COMPACT_LISTS && c->cand_refine && !compat && !c->kept_for.same(f, kp->rank, kp->nranks)) {
+  if (RT_COMPACT_LISTS && c->cand_refine && !compat && !kept_now && !c->kept_for.same(f, kp->rank, kp->nranks)) {
     // this frame's kept count, for its later builds (read back without waiting)
     if (!c->h_kept) HIP_TRY(hipHostMalloc((void**)&c->h_kept, sizeof(uint32_t), hipHostMallocDefault));
     if (!c->ev_kept) HIP_TRY(hipEventCreateWithFlags(&c->ev_kept, hipEventDisableTiming));
@@ -2136,6 +2171,12 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
     p.item_cost = c->d_item_cost;
     p.cost_sum = cost_sum_of(c);
   }
+  if (!c->d_frame_check) {
+    HIP_TRY(hipMalloc((void**)&c->d_frame_check, 4 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemsetAsync(c->d_frame_check, 0, 4 * sizeof(unsigned long long), s));
+  }
+  p.frame_check = c->d_frame_check;
+  p.list_flag = c->last_async ? c->d_cand_ctr + 16 + 7 : nullptr;  // bounds_kernel's snapshot of ctr[7]
   HIP_TRY(hipMemsetAsync(c->d_counter, 0, kFrameCounterBytes, s));  // item streams, stats, record counters
   if (c->timing) HIP_TRY(hipEventRecord(ev[1], s));
   HIP_TRY(rt_launch_trace(&p, dacc, c->count_work, pol, gt, s));
@@ -2359,6 +2400,31 @@ extern "C" int rt_hip_probe_shadows(rt_hip_ctx* c, unsigned light, const float* 
   (void)hipFree(d_o);
   (void)hipFree(d_h);
   return rc;
+}
+
+// The per-frame checks of every render since the last call (fold_kernel):
+// *flags = OR of RT_FRAME_* (0: every frame complete and exact by the
+// conditions rt_hip_stats checks), *frames = renders checked, queries[0] /
+// [1] = their closest-hit / shadow queries summed; all reset.  Lets a caller
+// that renders many frames without rt_hip_stats (bench.py's timed loops)
+// refuse a result with an incomplete frame in it, and count every frame's
+// own queries.
+extern "C" int rt_hip_frame_check(rt_hip_ctx* c, unsigned* flags, unsigned* frames, unsigned long long* queries) {
+  if (!c || !flags || !frames || !queries) return rt_set_error(RT_EINVAL, "null argument");
+  *flags = *frames = 0;
+  queries[0] = queries[1] = 0;
+  if (!c->d_frame_check) return RT_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = c->last_stream ? c->last_stream : c->stream;
+  unsigned long long h[4] = {0, 0, 0, 0};
+  HIP_TRY(hipMemcpyAsync(h, c->d_frame_check, sizeof h, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemsetAsync(c->d_frame_check, 0, sizeof h, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  *flags = (unsigned)h[0];
+  *frames = (unsigned)h[1];
+  queries[0] = h[2];
+  queries[1] = h[3];
+  return RT_OK;
 }
 
 extern "C" int rt_hip_stats(rt_hip_ctx* c, rt_stats* out) {

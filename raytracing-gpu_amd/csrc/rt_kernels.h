@@ -174,7 +174,21 @@ struct KParams {
   uint32_t* sec_count;          // appended entries (zeroed before the launch)
   uint32_t* sec_head;           // bounce_kernel's chunk counter (zeroed before the launch)
   uint32_t sec_cap;
+  // per-frame completeness check (fold_kernel, the frame's last launch): the
+  // conditions rt_hip_stats reports as errors, ORed into frame_check[0]
+  // (RT_FRAME_*), frame_check[1] += 1 frame, [2] / [3] += its closest-hit /
+  // shadow queries -- sticky across frames until rt_hip_frame_check reads
+  // them, so a timed loop of many frames is checked and counted as a whole.
+  // list_flag: the frame's asynchronous list build's overflow flag (ctr[7]),
+  // or NULL
+  unsigned long long* frame_check;
+  const uint32_t* list_flag;
 };
+#define RT_FRAME_HITBUF 1u     // hit records past a region's capacity
+#define RT_FRAME_DEPTH 2u      // bounce limit or traversal stack overflow
+#define RT_FRAME_ZERO 4u       // zero interpolated normal (closest or shadow)
+#define RT_FRAME_UNPROVEN 8u   // shadow queries the exact mode could not decide
+#define RT_FRAME_LISTS 16u     // asynchronous list build overflow
 
 // The three launches of one render (policy = RT_POLICY_*, octree only):
 // trace (closest hits -> hit records), shade (shadow queries + Phong per

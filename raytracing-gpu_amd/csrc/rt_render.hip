@@ -2391,6 +2391,22 @@ __global__ __launch_bounds__(64) void probe_closest_kernel(KParams p, const floa
 // pixel of the rank's tile buffer.
 __global__ __launch_bounds__(256) void fold_kernel(KParams p) {
   const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx == 0 && p.frame_check) {  // every earlier launch of the frame has ended (same stream)
+    uint32_t f = 0;
+    for (int x = 0; x < RT_HIT_REGIONS; x++)
+      if (p.hit_count[32 * x] > p.hit_cap) f |= RT_FRAME_HITBUF;
+    unsigned long long s[RT_NSTATS] = {};
+    for (int set = 0; set < RT_STAT_SETS; set++)
+      for (int k = 0; k < RT_NSTATS; k++) s[k] += p.stats[set * RT_STAT_STRIDE + k];
+    if (s[5]) f |= RT_FRAME_DEPTH;
+    if (s[6] || s[18]) f |= RT_FRAME_ZERO;
+    if (s[21] || (p.oob_count && *p.oob_count > p.oob_cap)) f |= RT_FRAME_UNPROVEN;
+    if (p.list_flag && *p.list_flag) f |= RT_FRAME_LISTS;
+    atomicOr(p.frame_check, (unsigned long long)f);
+    atomicAdd(p.frame_check + 1, 1ull);
+    atomicAdd(p.frame_check + 2, s[0]);
+    atomicAdd(p.frame_check + 3, s[1]);
+  }
   if (idx >= (uint32_t)p.ntiles_local * 64u) return;
   const uint32_t t = idx >> 6, lane = idx & 63u;
   int pr, pc;

@@ -152,6 +152,8 @@ _PROTOS = [
     ("rt_hip_render", C.c_int, [C.c_void_p, C.POINTER(Frame), C.c_int, C.c_int, C.c_void_p,
                                 C.c_void_p]),
     ("rt_hip_stats", C.c_int, [C.c_void_p, C.POINTER(Stats)]),
+    ("rt_hip_frame_check", C.c_int, [C.c_void_p, C.POINTER(C.c_uint), C.POINTER(C.c_uint),
+                                     C.POINTER(C.c_ulonglong)]),
     ("rt_hip_set_count_work", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_set_cull_slack", C.c_int, [C.c_void_p, C.c_float]),
     ("rt_hip_set_camera_slack", C.c_int, [C.c_void_p, C.c_float]),
@@ -604,6 +606,20 @@ class Context:
         st = Stats()
         self._check_render(lib().rt_hip_stats(self.h, C.byref(st)), "rt_hip_stats")
         return st.as_dict()
+
+    # rt_hip_frame_check flag bits (csrc/rt_kernels.h RT_FRAME_*)
+    FRAME_FLAGS = {1: "hit records past the buffer (RT_EHITBUF)", 2: "bounce limit / stack overflow (RT_EDEPTH)",
+                   4: "zero interpolated normal (RT_EZERONORMAL)", 8: "undecided exact shadow queries (RT_EINEXACT)",
+                   16: "asynchronous list build overflow (RT_EHITBUF)"}
+
+    def frame_check(self):
+        """(flags, frames, closest, shadow): the per-frame completeness checks
+        of every render since the last call, ORed (0 = every frame complete,
+        FRAME_FLAGS names the bits), the renders checked and their summed
+        closest-hit / shadow queries (rt_hip_frame_check); all reset."""
+        fl, n, q = C.c_uint(), C.c_uint(), (C.c_ulonglong * 2)()
+        _check(lib().rt_hip_frame_check(self.h, C.byref(fl), C.byref(n), q), "rt_hip_frame_check")
+        return int(fl.value), int(n.value), int(q[0]), int(q[1])
 
     def cand_produce(self, frame, rank, nranks, stream=None):
         """Triangle-parallel lists, step 1 (rt_hip_cand_produce): this rank's
