@@ -224,11 +224,12 @@ def latest_profile(workload, name):
     return None
 
 
-def frame_checked(ctx, rank, world, frame, steps, what):
+def frame_checked(ctx, rank, world, frame, steps, what, fatal=True):
     """The device's per-frame checks of the frames rendered since the last
     reset (rt_hip_frame_check): refuses (SystemExit, no JSON line) unless
     every one was complete and exact by rt_hip_stats' conditions.  Returns
-    the frames' closest-hit + shadow queries summed over the ranks."""
+    the frames' closest-hit + shadow queries summed over the ranks (not
+    fatal: None and the reason instead of exiting)."""
     fl, nf, qc, qs = ctx.frame_check()
     has_tiles = rtgpu.rank_tile_count(frame.width, frame.height, rank, world) > 0
     bad = fl != 0 or (has_tiles and nf != steps)
@@ -237,8 +238,10 @@ def frame_checked(ctx, rank, world, frame, steps, what):
         dist.all_reduce(t)
     if bad or t[0].item() > 0:
         why = ", ".join(v for k, v in ctx.FRAME_FLAGS.items() if fl & k) or f"{nf} of {steps} frames checked"
+        if not fatal:
+            return None, why
         raise SystemExit(f"[rank {rank}] {what} loop: incomplete frame(s) ({why}): no value printed")
-    return float(t[1].item())
+    return (float(t[1].item()), None) if not fatal else float(t[1].item())
 
 
 def main():
@@ -256,8 +259,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--camera-pan", type=float, default=1.0,
                     help="after the replay loop, time --steps more frames each with its own camera, "
-                         "panned this many pixels per step along the image's u axis (a new view every "
-                         "frame: nothing of an earlier identical frame is reused); 0 = skip")
+                         "moved along the image's u axis by this many pixels of image shift per step at "
+                         "the scene centre's depth (a new view every frame: nothing of an earlier "
+                         "identical frame is reused); 0 = skip")
     ap.add_argument("--cull-slack", type=float, default=None,
                     help="octree culling slack override (tuning; default = library default)")
     ap.add_argument("--camera-slack", type=float, default=None,
@@ -268,6 +272,8 @@ def main():
     ap.add_argument("--exact-shadows", type=int, default=None, choices=[0, 1],
                     help="shadow queries through proven (1) or slack-grown (0) light buffers "
                          "(rt_hip_set_exact_shadows; default = library default, proven)")
+    ap.add_argument("--exact-reflections", type=int, default=None, choices=[0, 1],
+                    help="reflection rays through the proven walk (rt_hip_set_exact_reflections; default off)")
     ap.add_argument("--lists", default=None, choices=["rank", "partition"],
                     help="camera candidate lists of an N-GPU frame: built by every rank for its "
                          "tiles over all triangles ('rank'), or triangle-parallel -- each rank "
@@ -306,6 +312,8 @@ def main():
         ctx.set_policy(args.policy)
     if args.exact_shadows is not None:
         ctx.set_exact_shadows(bool(args.exact_shadows))
+    if args.exact_reflections:
+        ctx.set_exact_reflections(True)
     info = ctx.info()
     log(f"[rank {rank}] scene {ntri} triangles, accel {wl['accel']}: {info['tri_refs']} records, "
         f"{info['nodes']} nodes, build {info['build_seconds']:.1f}s, setup {time.perf_counter()-t:.1f}s")
@@ -435,11 +443,19 @@ def main():
         cam0 = rtgpu.Camera()
         ctypes.pointer(cam0)[0] = scene.s.camera
         fu = (frame.u.x, frame.u.y, frame.u.z)
+        # cpu/rt's film lies L world units from the eye with one unit per
+        # pixel (cpu/raytracer.c:82-86), so moving the eye by D / L units
+        # shifts the image of a point at depth D by one pixel
+        ctr = info["scene_center"]
+        depth = float(np.linalg.norm(np.array(ctr) - np.array([cam0.position.x, cam0.position.y, cam0.position.z])))
+        film = float(np.linalg.norm(np.array([frame.C.x - frame.position.x, frame.C.y - frame.position.y,
+                                              frame.C.z - frame.position.z])))
+        step_units = args.camera_pan * max(depth, 1e-3) / film
         frames = []
         for k in range(1, args.steps + 1):
             cam = rtgpu.Camera()
             ctypes.pointer(cam)[0] = cam0
-            sh_ = args.camera_pan * k
+            sh_ = step_units * k
             cam.position.x = cam0.position.x + fu[0] * sh_
             cam.position.y = cam0.position.y + fu[1] * sh_
             cam.position.z = cam0.position.z + fu[2] * sh_
@@ -459,16 +475,20 @@ def main():
             dist.barrier()
         el_f = time.perf_counter() - t1
         ftf = ctx.frame_times(min(args.steps, 1024))
-        fresh_q = frame_checked(ctx, rank, world, frames[-1], args.steps, "fresh-camera")
+        # (an extra measurement: an incomplete frame here -- a new camera whose
+        # lists outgrew the estimate from the last frame, rendered again by a
+        # caller that checks rt_hip_stats -- voids only these numbers)
+        fresh_q, why = frame_checked(ctx, rank, world, frames[-1], args.steps, "fresh-camera", fatal=False)
         ctx.set_timing(False)
         tf = torch.tensor([el_f, sum(a for a, _ in ftf) / len(ftf)], dtype=torch.float64, device=dev)
         if world > 1:
             dist.all_reduce(tf, op=dist.ReduceOp.MAX)
         el_f, lists_f = tf.tolist()
-        fresh = {"pan_px_per_step": args.camera_pan, "frames": args.steps,
-                 "ms_per_step": round(el_f / args.steps * 1e3, 3),
-                 "value": round(fresh_q / el_f / 1e6, 3),
-                 "candidate_lists_ms": round(lists_f, 3)}
+        fresh = {"pan_px_per_step": args.camera_pan, "pan_world_units_per_step": round(step_units, 6),
+                 "frames": args.steps,
+                 "ms_per_step": round(el_f / args.steps * 1e3, 3) if fresh_q is not None else None,
+                 "value": round(fresh_q / el_f / 1e6, 3) if fresh_q is not None else None,
+                 "candidate_lists_ms": round(lists_f, 3), "incomplete": why}
     trace_ms = sum(a for a, _, _ in kt) / len(kt)
     shade_ms = sum(b for _, b, _ in kt) / len(kt)
     fold_ms = sum(c for _, _, c in kt) / len(kt)
@@ -519,7 +539,7 @@ def main():
     traffic_src = None
     if world == 1 and args.traffic_json is None and args.cull_slack is None and \
             args.camera_slack is None and args.policy is None and args.accel is None and \
-            args.exact_shadows is None:
+            args.exact_shadows is None and not args.exact_reflections:
         # default run: the newest committed rocprofv3 PMC passes of this
         # workload (profiles/r*_<workload>/, tools/gpu_profile.sh); a PMC
         # pass cannot run inside the bench, so the line says where it came from
@@ -625,7 +645,10 @@ def main():
                 "exactness": {"camera_rays": "proven (candidate lists, refined per tile)",
                               "shadow_rays": ("measured (slack-grown light buffers)"
                                               if args.exact_shadows == 0 else
-                                              "proven (light buffers + off-box brute force)")},
+                                              "proven (light buffers + off-box brute force)"),
+                              "reflection_rays": ("proven (error-region growth per node, csrc/rt_reflect.hip)"
+                                                  if args.exact_reflections else
+                                                  "tested (culling slack; grazing probes, whole-frame checks)")},
                 "queries_per_frame": {"closest": int(closest), "shadow": int(shadow),
                                       "closest_hits": int(hits), "pixels": int(pixels)},
             },

@@ -93,6 +93,9 @@ typedef struct rt_stats {
    * garbage hits far past a triangle), decided by brute force after the
    * shade pass (rt_hip_set_exact_shadows) */
   unsigned long long shadow_deferred;
+  /* exact reflection rays (rt_hip_set_exact_reflections): queries outside the
+   * proven walk's assumption |d| <= RT_RF_DLMAX (must be 0, RT_EINEXACT) */
+  unsigned long long closest_unproven;
 } rt_stats;
 
 /* Sizes of the device-side scene image, for the roofline accounting. */
@@ -131,6 +134,7 @@ typedef struct rt_accel_info {
   char lightbuf_fail_reason[96]; /* the last such fallback's cause ("" if none) */
   int trace_grid, shade_grid;    /* persistent one-wave workgroups of the default
                                     trace / shade kernels (occupancy-derived) */
+  float scene_center[3], scene_radius;  /* the scene's box centre and half-extent (max-norm) */
 } rt_accel_info;
 
 /* Host-only: build the acceleration structure rt_hip_create would build and
@@ -267,6 +271,17 @@ int rt_hip_set_light_buffers(rt_hip_ctx *ctx, int enable);
  * rt_accel_info.lightbuf_failed); rebuilds the buffers now. */
 int rt_hip_set_lightbuf_entry_cap(rt_hip_ctx *ctx, unsigned long long cap);
 int rt_hip_set_exact_shadows(rt_hip_ctx *ctx, int enable);
+/* Reflection rays exact by proof (default 0; builds the per-node bounds now).
+ * The reflection walk grows each node's box by the reach of the reference
+ * float Moller-Trumbore test's error region for that ray -- bounded through
+ * the node's normal cone (the ray's cosine with every plane below it) and the
+ * 1e-7f accept threshold -- and prunes with the matching distance error, so
+ * every triangle the float test could accept is tested (csrc/rt_reflect.hip,
+ * DESIGN.md §2).  0: the culling slack, whose reflection decisions are
+ * tested (rt_hip_probe_closest), not proven.  Default traversal policy only
+ * (rt_hip_render fails with RT_EINVAL otherwise); the closest-hit probe uses
+ * the same walk. */
+int rt_hip_set_exact_reflections(rt_hip_ctx *ctx, int enable);
 /* Host-only survey (no device) of light `light`'s buffer as rt_hip_create
  * builds it for this scene (exact = proven footprints), every stride-th
  * triangle: out[0] entries, [1] triangles never accepted, [2] global, [3] band

@@ -22,6 +22,7 @@
 #include "rt_kernels.h"
 #include "rt_lightbuf.h"
 #include "rt_shadow.h"
+#include "rt_reflect.h"
 #include "rt_tiles.h"
 
 extern "C" {
@@ -59,6 +60,11 @@ extern "C" {
 #ifndef RT_COMPACT_LISTS
 #define RT_COMPACT_LISTS 1
 #endif
+// asynchronous list builds for a new camera of the same size and rank split,
+// sized from the last build + headroom (cand_prepare; A/B knob)
+#ifndef RT_ASYNC_NEW_CAMERA
+#define RT_ASYNC_NEW_CAMERA 1
+#endif
 // ... also in a fresh (non-asynchronous) build, with a read-back of the kept
 // count (A/B knob)
 #ifndef RT_COMPACT_FRESH
@@ -75,10 +81,9 @@ static constexpr size_t kItemCounterBytes = 8 * 128;
 static_assert(RT_NSTATS <= RT_STAT_STRIDE, "stat copies overlap");
 static constexpr size_t kStatBytes = RT_STAT_SETS * RT_STAT_STRIDE * sizeof(unsigned long long);
 static constexpr size_t kHitCounterBytes = 2 * RT_HIT_REGIONS * 32 * sizeof(uint32_t);
-static constexpr size_t kSecCounterBytes = 2 * 32 * sizeof(uint32_t);  // secondary queue: append, chunk
 static constexpr size_t kCostBytes = 64;  // the trace's item-clock sum (KParams::cost_sum)
 static constexpr size_t kFrameCounterBytes =
-    kItemCounterBytes + kStatBytes + kHitCounterBytes + kSecCounterBytes + kCostBytes;
+    kItemCounterBytes + kStatBytes + kHitCounterBytes + kCostBytes;
 
 // The sizes of one list build, which are deterministic for its (camera
 // frame, rank, nranks): a later build of the same frame sizes its buffers and
@@ -136,28 +141,12 @@ struct rt_hip_ctx {
   size_t hit_need = 0;              // per region: what the last overflowing frame needed
   uint32_t* d_last = nullptr;       // per (item, lane): a path's deepest record
   size_t last_cap = 0;              // items
-  // secondary-ray queue (KParams::sec_q): one entry per camera ray at most
-// Measured and OFF (profiles/r07_secondary_queue/): with the reflection
-// paths queued and continued 64 to a wave by bounce_kernel after the camera
-// waves, C5 trace + bounce took 5.21 ms against 4.50 (N = 8 slowest rank 1.48
-// against 1.22 ms): a queue chunk gathers ~76 items' rays from all over the
-// frame (0.84 reflection rays per item), so its per-lane walks are incoherent
-// and the longest of them -- no longer hidden under other waves' camera
-// work -- sets the kernel's length.  RT_SEC_QUEUE=1 at context creation turns
-// it on (A/B).
 // per-rank candidate lists built without a host read-back (VERDICT r04
 // "render is async"): 1 = on (the first frame still reads its total back)
 #ifndef RT_ASYNC_LISTS_DEFAULT
 #define RT_ASYNC_LISTS_DEFAULT 1
 #endif
-#ifndef RT_SEC_QUEUE_DEFAULT
-#define RT_SEC_QUEUE_DEFAULT 0
-#endif
-  int sec_queue = RT_SEC_QUEUE_DEFAULT;  // RT_SEC_QUEUE=0 at context creation: off (A/B)
-  float4* d_sec_q = nullptr;
-  uint32_t* d_sec_slot = nullptr;
-  size_t sec_cap = 0;
-  int grid_of[2][5][2] = {};        // persistent grids [trace][policy][count_work] (policy 4: shade only)
+  int grid_of[2][RT_NPOLICIES][2] = {};  // persistent grids [trace][policy][count_work] (4: shade only, 5: trace only)
   int cus = 0;                      // compute units of the device
   std::vector<uint32_t> light_type; // per light (rt_hip_verify_shadows)
   std::vector<float> light_v;       // per light: l.v (3 floats)
@@ -177,6 +166,11 @@ struct rt_hip_ctx {
   unsigned long long* d_frame_check = nullptr;  // KParams::frame_check: sticky per-frame checks (rt_hip_frame_check)
   uint32_t* d_sh_global = nullptr;
   uint32_t n_sh_global = 0;
+  // exact reflection rays (csrc/rt_reflect.hip, rt_hip_set_exact_reflections):
+  // per-node error-region bounds, built once per tree when the mode is enabled
+  int exact_refl = 0;
+  float4* d_node_rf = nullptr;
+  unsigned long long rf_unbounded = 0;  // leaves holding a triangle no bound covers
   float sh_ulps = -1.0f;
   float sh_omax = 0.0f;
   float sh_mu_max = 1.0f;
@@ -240,8 +234,9 @@ struct rt_hip_ctx {
   // frame's asynchronous builds compact the entries to that many before the
   // sort instead of sorting the dropped ones too
   ListShape kept_for;
-  uint32_t* h_kept = nullptr;   // pinned
+  uint32_t* h_kept = nullptr;   // pinned: [0] the kept count, [1..8] an asynchronous build's counters ctr[0..7]
   hipEvent_t ev_kept = nullptr;
+  int snap_pending = 0;         // h_kept[1..8] will hold the last estimated-shape build's counters (ev_kept)
   int kept_ready = 0;           // h_kept holds kept_for's count
   uint32_t kept = 0;
   ListShape cost_hist;
@@ -387,13 +382,12 @@ extern "C" void rt_hip_destroy(rt_hip_ctx* c) {
   (void)hipFree(c->d_hit_prev);
   (void)hipFree(c->d_hit_term);
   (void)hipFree(c->d_last);
-  (void)hipFree(c->d_sec_q);
-  (void)hipFree(c->d_sec_slot);
   (void)hipFree(c->d_prim_mu);
   (void)hipFree(c->d_node_mu);
   (void)hipFree(c->d_oob);
   (void)hipFree(c->d_oob_count);
   (void)hipFree(c->d_frame_check);
+  (void)hipFree(c->d_node_rf);
   (void)hipFree(c->d_sh_global);
   for (LBDevice* d : c->lb_dev) rt_lightbuf_free(d);
   (void)hipFree(c->d_lbuf);
@@ -698,7 +692,6 @@ extern "C" int rt_hip_create(int device, const rt_scene* scene, int accel, rt_hi
 
   rt_hip_ctx* c = new rt_hip_ctx();
   if (const char* e = std::getenv("RT_CAND_REFINE")) c->cand_refine = std::atoi(e) != 0;  // A/B knob
-  if (const char* e = std::getenv("RT_SEC_QUEUE")) c->sec_queue = std::atoi(e) != 0;      // A/B knob
   if (const char* e = std::getenv("RT_ASYNC_LISTS")) c->async_lists = std::atoi(e) != 0;  // A/B knob
   c->device = device;
   c->accel = dev_build ? (fs.ntri ? RT_ACCEL_OCTREE : RT_ACCEL_FLAT) : accel;
@@ -802,7 +795,7 @@ extern "C" int rt_hip_create(int device, const rt_scene* scene, int accel, rt_hi
   int gmax = c->grid;
   const int dacc = c->accel == RT_ACCEL_FLAT ? RT_ACCEL_FLAT_D : RT_ACCEL_OCTREE_D;
   for (int tr = 0; tr < 2; tr++)
-    for (int pol = 0; pol < (tr ? 4 : 5); pol++)
+    for (int pol = 0; pol < RT_NPOLICIES; pol++)
       for (int cw = 0; cw < 2; cw++) {
         int g = 0;
         hipError_t he = rt_render_grid(tr, dacc, cw, pol, prop.multiProcessorCount, &g);
@@ -815,6 +808,8 @@ extern "C" int rt_hip_create(int device, const rt_scene* scene, int accel, rt_hi
       }
   c->info.trace_grid = c->grid_of[1][RT_POLICY_DEFAULT][0];
   c->info.shade_grid = c->grid_of[0][RT_POLICY_LBUF][0];
+  for (int a = 0; a < 3; a++) c->info.scene_center[a] = c->scene_c[a];
+  c->info.scene_radius = c->scene_r;
   // per-lane traversal stack spill area, [entry][lane] for the largest grid
   if (c->accel == RT_ACCEL_OCTREE &&
       hipMalloc((void**)&c->d_spill, (size_t)gmax * 64 * RT_SPILL_STACK * sizeof(uint2)) != hipSuccess) {
@@ -895,6 +890,49 @@ extern "C" int rt_hip_set_exact_shadows(rt_hip_ctx* c, int enable) {
   if (rc) return rc;
   if (c->exact_shadows) return shadow_prepare(c, c->stream);
   return RT_OK;
+}
+
+// The exact reflection walk's per-node bounds (csrc/rt_reflect.hip): once
+// per tree, synchronous (setup).
+static int reflect_prepare(rt_hip_ctx* c, hipStream_t s) {
+  if (c->d_node_rf || c->accel != RT_ACCEL_OCTREE || !c->d_node) return RT_OK;
+  const size_t nn = c->info.nodes;
+  float* phi = nullptr;
+  uint32_t* d_u = nullptr;
+  HIP_TRY(hipMalloc((void**)&c->d_node_rf, (3 * nn + 3) * sizeof(float4)));
+  hipError_t he = hipMalloc((void**)&phi, (nn + 1) * sizeof(float));
+  if (he == hipSuccess) he = hipMalloc((void**)&d_u, sizeof(uint32_t));
+  ReflParams rp;
+  std::memset(&rp, 0, sizeof rp);
+  rp.node = c->d_node;
+  rp.nnode = (uint32_t)nn;
+  rp.rec = c->d_tri;
+  rp.node_rf = c->d_node_rf;
+  rp.node_phi = phi;
+  rp.unbounded = d_u;
+  uint32_t u = 0;
+  if (he == hipSuccess) he = hipMemsetAsync(c->d_node_rf, 0, (3 * nn + 3) * sizeof(float4), s);
+  if (he == hipSuccess) he = hipMemsetAsync(d_u, 0, sizeof(uint32_t), s);
+  if (he == hipSuccess) he = rt_reflect_build(&rp, (int)c->info.max_depth + 2, s);
+  if (he == hipSuccess) he = hipMemcpyAsync(&u, d_u, sizeof u, hipMemcpyDeviceToHost, s);
+  if (he == hipSuccess) he = hipStreamSynchronize(s);
+  (void)hipFree(phi);
+  (void)hipFree(d_u);
+  if (he != hipSuccess) {
+    (void)hipFree(c->d_node_rf);
+    c->d_node_rf = nullptr;
+    return rt_set_error(RT_EHIP, "reflection bounds: %s", hipGetErrorString(he));
+  }
+  c->rf_unbounded = u;
+  return RT_OK;
+}
+
+extern "C" int rt_hip_set_exact_reflections(rt_hip_ctx* c, int enable) {
+  if (!c) return rt_set_error(RT_EINVAL, "null context");
+  c->exact_refl = enable ? 1 : 0;
+  if (!c->exact_refl) return RT_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  return reflect_prepare(c, c->stream);
 }
 
 extern "C" int rt_hip_set_policy(rt_hip_ctx* c, int policy) {
@@ -1211,8 +1249,7 @@ extern "C" int rt_hip_set_cand_item_cap(rt_hip_ctx* c, unsigned cap) {
 
 // the trace's item-clock sum in the frame counters (KParams::cost_sum)
 static unsigned long long* cost_sum_of(rt_hip_ctx* c) {
-  return (unsigned long long*)((char*)c->d_counter + kItemCounterBytes + kStatBytes + kHitCounterBytes +
-                               kSecCounterBytes);
+  return (unsigned long long*)((char*)c->d_counter + kItemCounterBytes + kStatBytes + kHitCounterBytes);
 }
 
 // Frame constants of the candidate lists for rank/nranks (no device work).
@@ -1649,12 +1686,41 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
   cp.prim1 = c->nprim;
   const size_t nt = (size_t)kp->ntiles_local;
   uint32_t total = 0, nglobal = 0;
-  // asynchronous for a frame whose lists were built before (a new camera
-  // frame, rank split or the compatibility mode's lists read their total
-  // back once; so does cand_verify's rebuild, which keeps every footprint)
-  const bool async = RT_DEV_SCAN && c->async_lists && !c->cand_store_fp && !compat &&
-                     c->known.same(f, kp->rank, kp->nranks);
-  rc = cand_build(c, cp, s, 0, &total, &nglobal, async ? &c->known : nullptr, async ? nullptr : &c->known);
+  // The last build's counters, read back without waiting after an
+  // estimated-shape build below: the next estimate starts from them
+  if (c->snap_pending && c->ev_kept && hipEventQuery(c->ev_kept) == hipSuccess) {
+    const uint32_t* h = c->h_kept + 1;  // ctr[0..7]
+    if (h[7]) {  // that frame outgrew its estimate (reported): the next build reads back
+      c->known.valid = c->kept_for.valid = 0;
+    } else if (c->known.valid) {
+      c->known.total = h[6];
+      c->known.nglobal = h[1];
+      c->known.nbig = h[2];
+      c->known.nitems = h[4];
+      c->known.over = h[5];
+    }
+    c->snap_pending = 0;
+  }
+  // Asynchronous (no host wait) for a frame whose lists were built before
+  // with a read-back -- its sizes are deterministic -- and, with headroom,
+  // for a new camera of the same size and rank split (an animation's next
+  // frame, a panned view): the last build's sizes + 1/4 size the buffers and
+  // launches, every kernel checks its counts on the device, and a frame past
+  // them is reported (RT_EHITBUF via ctr[7], rt_hip_stats / the frame check)
+  // and built again with a read-back.  The first frame of a size or split,
+  // the compatibility mode and cand_verify's rebuild (every footprint kept)
+  // read their sizes back.
+  const bool exact_shape = c->known.same(f, kp->rank, kp->nranks);
+  const bool est_shape = !exact_shape && RT_ASYNC_NEW_CAMERA && c->known.same_grid(f, kp->rank, kp->nranks);
+  const bool async = RT_DEV_SCAN && c->async_lists && !c->cand_store_fp && !compat && (exact_shape || est_shape);
+  ListShape est = c->known;
+  if (est_shape) {
+    est.total = c->known.total + c->known.total / 4 + 4096;
+    est.nglobal = c->known.nglobal + c->known.nglobal / 4 + 64;
+    est.nbig = c->known.nbig + c->known.nbig / 4 + 64;
+    est.nitems = c->known.nitems + c->known.nitems / 4 + 64;
+  }
+  rc = cand_build(c, cp, s, 0, &total, &nglobal, async ? &est : nullptr, async ? nullptr : &c->known);
   if (rc) return rc;
   c->last_async = async ? 1 : 0;
   if (async) nglobal = 0;  // on the device (ctr[1])
@@ -1665,7 +1731,8 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
   }
   rc = cand_tile_buffers(c, nt);
   if (rc) return rc;
-  // the kept count of this frame's earlier build, once its read-back is done
+  // the kept count of the last build of this size and split, once its
+  // read-back is done
   if (!c->kept_ready && c->kept_for.valid && c->ev_kept && hipEventQuery(c->ev_kept) == hipSuccess) {
     c->kept = *c->h_kept;
     c->kept_ready = 1;
@@ -1675,8 +1742,12 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
   // frame's earlier build; a fresh frame (a new camera: the build read its
   // total back anyway) reads its own back after the compaction's scan -- one
   // more short host wait instead of sorting the dropped entries
+  // (for a new camera the last frame's kept count + 1/8: the scatter writes
+  // the unused tail as dropped, and a count past it sets ctr[7])
+  const bool kept_same = c->kept_for.same(f, kp->rank, kp->nranks);
   const bool compact_known = RT_COMPACT_LISTS && async && c->cand_refine && c->kept_ready &&
-                             c->kept_for.same(f, kp->rank, kp->nranks) && c->kept <= total && total > 0;
+                             (kept_same || (RT_ASYNC_NEW_CAMERA && c->kept_for.same_grid(f, kp->rank, kp->nranks))) &&
+                             c->kept <= total && total > 0;
   const bool compact_fresh = RT_COMPACT_LISTS && RT_COMPACT_FRESH && !async && !compat && !c->cand_store_fp &&
                              c->cand_refine && total > 0;
   bool kept_now = false;
@@ -1698,7 +1769,11 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
     size_t tmpb = 0;
     // (only the build's own entries, ctr[6]; fewer kept than last time --
     // never expected -- leave a tail the scatter writes as dropped)
-    const uint32_t cap = compact_known ? c->kept : total;
+    uint32_t cap = total;
+    if (compact_known) {
+      cap = kept_same ? c->kept : c->kept + c->kept / 8 + 4096;
+      if (cap > total) cap = total;
+    }
     HIP_TRY(rt_cand_compact(c->d_cand_keys, c->d_cand_vals, total, c->d_cand_ctr + 6, (uint32_t)nt, cap, cnt, off,
                             nullptr, &tmpb, c->d_cand_keys2, c->d_cand, c->d_cand_ctr + 7, s));
     rc = ensure_tmp(c, tmpb);
@@ -1708,7 +1783,7 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
                             c->d_scan_tmp, &tmpb, c->d_cand_keys2, c->d_cand, c->d_cand_ctr + 7, s));
     uint32_t kept = cap;
     if (compact_fresh) {  // off[nw] = the kept entries
-      if (!c->h_kept) HIP_TRY(hipHostMalloc((void**)&c->h_kept, sizeof(uint32_t), hipHostMallocDefault));
+      if (!c->h_kept) HIP_TRY(hipHostMalloc((void**)&c->h_kept, 9 * sizeof(uint32_t), hipHostMallocDefault));
       HIP_TRY(hipMemcpyAsync(c->h_kept, off + nw, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
       HIP_TRY(hipStreamSynchronize(s));
       kept = *c->h_kept;
@@ -1733,14 +1808,18 @@ static int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream
   // start[nt] = the entries with a tile (the dropped ones sort after them)
   // (an asynchronous build's counters snapshot for rt_hip_stats, where no build writes)
   HIP_TRY(rt_cand_bounds(c->d_cand_keys2, total, c->d_cand_start, (uint32_t)nt, async ? c->d_cand_ctr : nullptr, s));
-  if (RT_COMPACT_LISTS && c->cand_refine && !compat && !kept_now && !c->kept_for.same(f, kp->rank, kp->nranks)) {
-    // this frame's kept count, for its later builds (read back without waiting)
-    if (!c->h_kept) HIP_TRY(hipHostMalloc((void**)&c->h_kept, sizeof(uint32_t), hipHostMallocDefault));
+  if (RT_COMPACT_LISTS && c->cand_refine && !compat && !kept_now && (!kept_same || est_shape)) {
+    // this frame's kept count -- and after an estimated-shape build its
+    // counters (bounds_kernel's snapshot) -- for the later builds, read back
+    // without waiting
+    if (!c->h_kept) HIP_TRY(hipHostMalloc((void**)&c->h_kept, 9 * sizeof(uint32_t), hipHostMallocDefault));
     if (!c->ev_kept) HIP_TRY(hipEventCreateWithFlags(&c->ev_kept, hipEventDisableTiming));
     HIP_TRY(hipMemcpyAsync(c->h_kept, c->d_cand_start + nt, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    if (est_shape) HIP_TRY(hipMemcpyAsync(c->h_kept + 1, c->d_cand_ctr + 16, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipEventRecord(c->ev_kept, s));
     c->kept_for.set(f, kp->rank, kp->nranks);
     c->kept_ready = 0;
+    c->snap_pending = est_shape ? 1 : 0;
   }
   // the sorted keys are spent: their buffer takes the per-entry skip bounds
   float* entry_skip = (float*)c->d_cand_keys2;
@@ -1937,16 +2016,6 @@ static int hit_buffers(rt_hip_ctx* c, size_t ntiles) {
     HIP_TRY(hipMalloc((void**)&c->d_last, items * 64 * sizeof(uint32_t)));
     c->last_cap = items;
   }
-  if (c->sec_queue && items * 64 > c->sec_cap) {  // one queue entry per camera ray at most
-    (void)hipFree(c->d_sec_q);
-    (void)hipFree(c->d_sec_slot);
-    c->d_sec_q = nullptr;
-    c->d_sec_slot = nullptr;
-    c->sec_cap = 0;
-    HIP_TRY(hipMalloc((void**)&c->d_sec_q, items * 64 * 2 * sizeof(float4)));
-    HIP_TRY(hipMalloc((void**)&c->d_sec_slot, items * 64 * sizeof(uint32_t)));
-    c->sec_cap = items * 64;
-  }
   size_t want = (2 * items * 64 + RT_HIT_REGIONS - 1) / RT_HIT_REGIONS + 1024;
   if (c->hit_need > want) want = c->hit_need;
   if (want > (1ull << 29) - 1) want = (1ull << 29) - 1;  // slot field of a record index
@@ -2048,13 +2117,6 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
   p.shade_counter = c->d_hit_count + RT_HIT_REGIONS * 32;
   p.hit_cap = (uint32_t)c->hit_cap;
   p.last = c->d_last;
-  if (c->sec_queue && c->d_sec_q) {
-    p.sec_q = c->d_sec_q;
-    p.sec_slot = c->d_sec_slot;
-    p.sec_cap = (uint32_t)c->sec_cap;
-    p.sec_count = (uint32_t*)((char*)c->d_counter + kItemCounterBytes + kStatBytes + kHitCounterBytes);
-    p.sec_head = p.sec_count + 32;
-  }
   if (c->count_work) {  // per-item clocks of the instrumented pass (rt_hip_tile_cycles)
     const size_t items = 4 * (size_t)p.ntiles_local;
     if (items > c->tile_cycles_cap) {
@@ -2139,7 +2201,18 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
       if (c->light_type[li] == 1 || c->light_type[li] == 2) all = c->lb_dev[li] != nullptr;
     if (all) spol = RT_POLICY_LBUF;
   }
-  int gt = empty ? c->grid : c->grid_of[1][pol][cw], gs = empty ? c->grid : c->grid_of[0][spol][cw];
+  // exact reflection rays: the default policy's trace kernel with the proven
+  // reflection walk (its own instantiation: the default has no switch)
+  int tpol = pol;
+  if (dacc == RT_ACCEL_OCTREE_D && c->exact_refl) {
+    if (pol != RT_POLICY_DEFAULT)
+      return rt_set_error(RT_EINVAL, "exact reflections need the default traversal policy (have %d)", pol);
+    int rc = reflect_prepare(c, s);
+    if (rc) return rc;
+    p.node_rf = c->d_node_rf;
+    tpol = RT_POLICY_EXACT_REFL;
+  }
+  int gt = empty ? c->grid : c->grid_of[1][tpol][cw], gs = empty ? c->grid : c->grid_of[0][spol][cw];
   // small frames: no more persistent waves than work items (every wave pulls
   // items until all 8 streams drain, so any grid covers the frame; the
   // surplus waves of a full grid only cost dispatch on a frame of a few
@@ -2179,7 +2252,7 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
   p.list_flag = c->last_async ? c->d_cand_ctr + 16 + 7 : nullptr;  // bounds_kernel's snapshot of ctr[7]
   HIP_TRY(hipMemsetAsync(c->d_counter, 0, kFrameCounterBytes, s));  // item streams, stats, record counters
   if (c->timing) HIP_TRY(hipEventRecord(ev[1], s));
-  HIP_TRY(rt_launch_trace(&p, dacc, c->count_work, pol, gt, s));
+  HIP_TRY(rt_launch_trace(&p, dacc, c->count_work, tpol, gt, s));
   if (p.item_cost) {
     c->cost_hist.set(f, rank, nranks);
     c->cost_waves = (uint32_t)gt;
@@ -2321,6 +2394,11 @@ extern "C" int rt_hip_probe_closest(rt_hip_ctx* c, const float* origins, const f
   p.scene_cmag = std::fmax(std::fabs(c->scene_c[0]), std::fmax(std::fabs(c->scene_c[1]),
                                                                std::fabs(c->scene_c[2])));
   p.eps_rel = c->eps_ulps * 5.9604645e-8f;  // the secondary rays' slack (make_ray at depth > 0)
+  if (!brute && c->exact_refl) {  // the exact reflection mode's walk
+    int rc0 = reflect_prepare(c, s);
+    if (rc0) return rc0;
+    p.node_rf = c->d_node_rf;
+  }
   int gmax = 0;  // waves the spill area holds (rt_hip_create: the largest persistent grid)
   for (auto& a : c->grid_of)
     for (auto& b2 : a)
@@ -2487,6 +2565,7 @@ extern "C" int rt_hip_stats(rt_hip_ctx* c, rt_stats* out) {
   out->shadow_node_visits = h[19];
   out->shadow_tri_tests = h[20];
   out->shadow_unproven = h[21];
+  out->closest_unproven = h[22];
   out->hit_records = records;
   out->cand_prims = c->cand_prims;
   out->cand_entries = c->cand_entries;
@@ -2518,6 +2597,10 @@ extern "C" int rt_hip_stats(rt_hip_ctx* c, rt_stats* out) {
       return rt_set_error(RT_EINEXACT, "%u shadow queries from off the exact mode's proof box, %u decided",
                           q, RT_OOB_CAP);
   }
+  if (out->closest_unproven)
+    return rt_set_error(RT_EINEXACT,
+                        "%llu reflection rays with |d| past the exact reflection walk's bound "
+                        "(csrc/rt_reflect.h RT_RF_DLMAX)", out->closest_unproven);
   if (out->shadow_unproven)
     return rt_set_error(RT_EINEXACT,
                         "%llu shadow rays left from beyond the extent the exact shadow mode's "

@@ -16,7 +16,7 @@
 // cpu/rt recurses while coef >= 0.01 (cpu/raytracer.c:19-34), which is
 // unbounded for mirrors of Nr >= 1; paths of Nr < 1 end long before this
 #define RT_MAX_BOUNCES 16384
-#define RT_NSTATS 22
+#define RT_NSTATS 23
 // the counters are kept in RT_STAT_SETS copies RT_STAT_STRIDE words apart,
 // wave b adding to copy b % 8 (its XCD's): every wave of a launch flushes
 // its counters with a few 64-bit atomics, and on a small frame (C1: 4,096
@@ -76,6 +76,11 @@
 // the shadow queries compile to the buffer scan alone, without the octree
 // walk's registers and code (the default's fallback for lights without one)
 #define RT_POLICY_LBUF 4
+// trace kernel only, chosen by the host (rt_hip_set_exact_reflections with
+// the default policy): the default plus reflection rays through the proven
+// walk (csrc/rt_reflect.hip: per-node error-region growth)
+#define RT_POLICY_EXACT_REFL 5
+#define RT_NPOLICIES 6
 
 // wave-total counters (wave-uniform, so they live in SGPRs; 32-bit per wave,
 // widened to 64-bit by the final atomics)
@@ -92,6 +97,7 @@ struct WorkCount {
   uint32_t stack_spills;   // per-lane stack pushes past the LDS entries (COUNT pass)
   uint32_t zero_risk;      // shadow hits on objects whose interpolated normal can vanish
   uint32_t sh_unproven;    // point-light shadow rays from beyond the proof's assumed extent
+  uint32_t cl_unproven;    // exact reflection walk: queries with |d| past RT_RF_DLMAX
   // COUNT pass, per work item (rt_hip_tile_phase_cycles phases 4, 5): the
   // most node visits / triangle tests one lane made in per-lane secondary walks
   uint32_t sec_lane_nodes, sec_lane_tris;
@@ -129,6 +135,9 @@ struct KParams {
   // light buffers (csrc/rt_lightbuf.hip), per light; NULL: every shadow query walks
   const RtLightBuf* lbuf;
   const float2* node_mu;
+  // exact reflection rays (csrc/rt_reflect.hip, policy RT_POLICY_EXACT_REFL
+  // and the closest-hit probe): 3 float4 of error-region bounds per node
+  const float4* node_rf;
   const uint32_t* sh_global;
   uint32_t n_sh_global;
   float sh_omax;  // point-light shadow origins with |o - c|_max beyond this are counted unproven
@@ -165,15 +174,6 @@ struct KParams {
   // the heavy tiles at the front of tile_order (rt_cand_order's count, on
   // the device; NULL: none): their items run at raised wave priority
   const uint32_t* n_heavy;
-  // secondary-ray queue (NULL: camera waves follow their paths to the end):
-  // trace_kernel appends each camera path that goes on as {o.xyz, coef},
-  // {d.xyz, deepest record} plus its (item, lane) slot of last[];
-  // bounce_kernel continues them from depth 1
-  float4* sec_q;
-  uint32_t* sec_slot;
-  uint32_t* sec_count;          // appended entries (zeroed before the launch)
-  uint32_t* sec_head;           // bounce_kernel's chunk counter (zeroed before the launch)
-  uint32_t sec_cap;
   // per-frame completeness check (fold_kernel, the frame's last launch): the
   // conditions rt_hip_stats reports as errors, ORed into frame_check[0]
   // (RT_FRAME_*), frame_check[1] += 1 frame, [2] / [3] += its closest-hit /

@@ -25,6 +25,7 @@
 #include "rt_cull.h"
 #include "rt_device.h"
 #include "rt_kernels.h"
+#include "rt_reflect.h"
 #include "rt_tiles.h"
 
 namespace rt {
@@ -277,6 +278,7 @@ struct LaneCount {
   uint32_t risk;           // any hit on an object whose normal can vanish (any_hit_rec)
   uint32_t lnodes, ltris;  // this lane's own visits / tests (COUNT pass)
   uint32_t spills;         // pushes beyond the LDS part of the stack (COUNT pass)
+  uint32_t unproven;       // exact reflection walk: queries outside its bound's assumptions
 };
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
@@ -320,6 +322,7 @@ __device__ __forceinline__ void absorb(WorkCount& wc, const LaneCount& lc, bool 
   }
   wc.overflow += wave_sum(lc.overflow);
   wc.zero_risk += (uint32_t)__popcll(__ballot(lc.risk != 0));
+  wc.cl_unproven += (uint32_t)__popcll(__ballot(lc.unproven != 0));
   if (COUNT) wc.stack_spills += wave_sum(lc.spills);
 }
 
@@ -644,6 +647,169 @@ __device__ bool oct_any(const KParams& p, const Ray& r, Stack& s, LaneCount& wc)
   return false;
 }
 
+// ------------------------------------------- exact reflection walk (policy 5)
+// Reflection rays (bounce depth >= 1) with each node's box grown by the
+// reach of the float Moller-Trumbore test's error region for THIS ray
+// (csrc/rt_reflect.hip, DESIGN.md §2 "Reflection rays: exact by proof"): the
+// node's normal cone bounds the ray's cosine with every plane below it, the
+// 1e-7f accept threshold bounds it from below where the cone does not, and
+// the origin's distance to the box bounds |S| = |o - v0|.  Pruning and the
+// crossings behind the origin take the distance error the same way.
+struct RfRay {
+  f3 dh;     // d / |d| (rounded; psi covers the rounding of |axis . dh|)
+  bool ok;   // |d| <= RT_RF_DLMAX (the floor factors' assumption), else counted
+};
+
+__device__ __forceinline__ RfRay rf_ray(const Ray& r) {
+  RfRay q;
+  const float inv = 1.0f / r.dlen;
+  q.dh = f3{r.d.x * inv, r.d.y * inv, r.d.z * inv};
+  q.ok = r.dlen <= RT_RF_DLMAX;
+  return q;
+}
+
+// Node ni's bound for this ray: e = the box growth (world units, the walk's
+// slack included; +inf: enter unconditionally), bh = how far behind the
+// origin a crossing may lie (parametric), and the prune coefficients: a
+// float accept below the node has t_f >= (t_enter * pa - pb) (parametric,
+// when positive), so the node cannot win once that exceeds the best's t_cut.
+struct RfB {
+  float e, bh, pa, pb;
+};
+
+__device__ __forceinline__ RfB rf_bound(const float4* __restrict__ rf, uint32_t ni, const Ray& r, const RfRay& q,
+                                        const float4& lo, const float4& hi) {
+  const float4 A = rf[3 * (size_t)ni], B = rf[3 * (size_t)ni + 1], F = rf[3 * (size_t)ni + 2];
+  const float inf = __builtin_inff();
+  RfB o;
+  // |S| <= (L1 distance to the box's farthest corner) + the longest edge below
+  const float M = fmaxf(fabsf(r.o.x - lo.x), fabsf(r.o.x - hi.x)) + fmaxf(fabsf(r.o.y - lo.y), fabsf(r.o.y - hi.y)) +
+                  fmaxf(fabsf(r.o.z - lo.z), fabsf(r.o.z - hi.z));
+  const float Sb = M + B.w;
+  const float c = fabsf(A.x * q.dh.x + A.y * q.dh.y + A.z * q.dh.z) - A.w;  // cosine lower bound
+  float rps = inf, rho = 1.0f, kd = inf, r0 = inf;
+  if (c > 2.0f * B.y) {  // the cone closes: rho <= Ra / c < 1/2
+    rho = B.y / c;
+    rps = B.x / (c - B.y);
+    kd = B.z / c;
+    r0 = B.w * (2.3841858e-7f + rho) / (1.0f - rho);
+  }
+  if (F.w < 0.5f) {  // the floor closes
+    rps = fminf(rps, F.x);
+    rho = fminf(rho, F.w);
+    kd = fminf(kd, F.z);
+    r0 = fminf(r0, F.y);
+  }
+  if (!(rho < 0.5f) || !q.ok) {
+    o.e = inf;
+    o.bh = inf;
+    o.pa = 0.0f;
+    o.pb = inf;
+    return o;
+  }
+  // float evaluation of the bound: relative margins of 1e-5 (~100 roundings)
+  const float up = 1.0f + 1e-5f, rho2 = rho * up;
+  const float g = (rps * Sb + r0) * up;
+  const float dist = Sb * kd * up;  // |S| kd: the crossing's distance error (world)
+  o.e = r.eps + g;
+  o.bh = dist / (1.0f - 2.0f * rho2) / r.dlen * up;
+  // t* |d| <= [t_f |d| (1 + 2 eps)(1 - rho) + dist] / (1 - 2 rho) and t* >= the
+  // grown box's entry (less the slab's rounding, covered by 2 eps as rt_prune):
+  // t_f >= ((t_enter |d| (1 - 2^-21) - 2 eps)(1 - 2 rho) - dist) / (|d| (1 + 2 eps))
+  const float s = (1.0f - 2.0f * rho2) * (1.0f - 4.8e-7f);
+  o.pa = s * (1.0f - 1e-5f);
+  o.pb = ((2.0f * r.eps) * (1.0f - 2.0f * rho2) + dist) / r.dlen * up;
+  return o;
+}
+
+// slab test of the box grown by e (world), accepting parameters t >= -bh
+__device__ __forceinline__ bool box_rf(const Ray& r, f3 inv, const float4& lo, const float4& hi, float e, float bh,
+                                       float& tmin) {
+  if (e == __builtin_inff()) {
+    tmin = -__builtin_inff();
+    return true;
+  }
+  const float ohx = r.o.x + e, ohy = r.o.y + e, ohz = r.o.z + e;
+  const float olx = r.o.x - e, oly = r.o.y - e, olz = r.o.z - e;
+  const float tx0 = fmaf(lo.x, inv.x, -(ohx * inv.x)), tx1 = fmaf(hi.x, inv.x, -(olx * inv.x));
+  const float ty0 = fmaf(lo.y, inv.y, -(ohy * inv.y)), ty1 = fmaf(hi.y, inv.y, -(oly * inv.y));
+  const float tz0 = fmaf(lo.z, inv.z, -(ohz * inv.z)), tz1 = fmaf(hi.z, inv.z, -(olz * inv.z));
+  tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
+  const float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+  return tmax >= fmaxf(tmin, -bh);
+}
+
+// Test node ci's box for the rf walk; true: visit, key = the node's lower
+// bound on an accept's t_f (-inf: none) for pruning at push and pop.
+__device__ __forceinline__ bool rf_visit(const float4* __restrict__ rf, uint32_t ci, const Ray& r, const RfRay& q,
+                                         f3 inv, const float4& lo, const float4& hi, float& key) {
+  const RfB bd = rf_bound(rf, ci, r, q, lo, hi);
+  float tmin;
+  if (!box_rf(r, inv, lo, hi, bd.e, bd.bh, tmin)) return false;
+  key = bd.e == __builtin_inff() ? -__builtin_inff() : tmin * bd.pa - bd.pb;  // unbounded: never pruned
+  return true;
+}
+
+template <bool COUNT>
+__device__ void oct_closest_rf(const KParams& p, const Ray& r, Best& b, Stack& s, LaneCount& wc) {
+  const float4* __restrict__ node = p.node;
+  const float4* __restrict__ rf = p.node_rf;
+  const f3 inv = inv_dir(r.d);
+  const uint32_t dm = near_octant(r.d);
+  const RfRay q = rf_ray(r);
+  if (!q.ok) wc.unproven++;  // counted (RT_EINEXACT), and walked with every node unbounded
+  s.sp = 0;
+  wave_sync();
+  {
+    float key;
+    if (rf_visit(rf, 0, r, q, inv, node[0], node[1], key)) push(s, 0, key, wc);
+  }
+  while (s.sp > 0) {
+    uint32_t ni;
+    float key;
+    pop(s, ni, key);
+    if (b.dist != __builtin_inff() && key > b.t_cut) continue;
+    const float4 lo = node[2 * ni], hi = node[2 * ni + 1];
+    const uint32_t first = __float_as_uint(lo.w), info = __float_as_uint(hi.w);
+    if (COUNT) {
+      wc.nodes += lanes_distinct(ni);
+      wc.lnodes++;
+    }
+    if (info & RT_NODE_LEAF) {
+      leaf_lane<false, COUNT>(p.tri, first, RT_LEAF_COUNT(info), r, b, wc);
+      continue;
+    }
+    // children far-to-near in octant order (push_children), each tested with
+    // its own bound; child k+1's box and bound data in flight while k is tested
+    const uint32_t mask = RT_NODE_MASK(info);
+    uint32_t mj = mask_xor(mask, dm);
+    if (!mj) continue;
+    int j = 31 - __clz(mj);
+    mj &= ~(1u << j);
+    uint32_t ci = first + (uint32_t)__popc(mask & ((1u << ((uint32_t)j ^ dm)) - 1u));
+    float4 nlo = node[2 * ci], nhi = node[2 * ci + 1];
+    if (COUNT) wc.nodes += lanes_distinct(ci);
+    for (;;) {
+      const float4 clo = nlo, chi = nhi;
+      const uint32_t cc = ci;
+      const bool more = mj != 0u;
+      if (more) {
+        j = 31 - __clz(mj);
+        mj &= ~(1u << j);
+        ci = first + (uint32_t)__popc(mask & ((1u << ((uint32_t)j ^ dm)) - 1u));
+        nlo = node[2 * ci];
+        nhi = node[2 * ci + 1];
+        if (COUNT) wc.nodes += lanes_distinct(ci);
+      }
+      float ck;
+      if (rf_visit(rf, cc, r, q, inv, clo, chi, ck) && !(b.dist != __builtin_inff() && ck > b.t_cut))
+        push(s, cc, ck, wc);
+      if (!more) break;
+    }
+  }
+  wave_sync();
+}
+
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 // Wave-uniform loads through the constant address space: with a uniform
 // address they become scalar (SMEM) loads straight into SGPRs.  The scene
@@ -695,7 +861,6 @@ struct WaveCtx {
   float4* stk2;    // kStack2 x 2 float4
   uint64_t* stkm;  // kStack2 lane masks: lanes that wanted the pushed node
   float4* stage;   // kStageFlat / kStageOct float4
-  float4* stage2;  // a second kStageOct stage (the prefetching packet walk), or null
   int lane;
 };
 
@@ -968,156 +1133,6 @@ __device__ __forceinline__ void stage_push_children(const Ray& r, f3 inv, uint32
   }
 }
 
-// Asynchronous global -> LDS copies (global_load_lds_dwordx4, "glds"): lane l
-// copies src[l] to dst[l] with no VGPR destination -- a node payload (<= 96
-// float4) in one or two wave instructions.  hipcc does not order the LDS
-// reads of dst after these copies (no s_waitcnt is inserted for them), so
-// every read of a glds buffer is preceded by glds_wait: vmcnt(k) retires
-// every vector-memory load but the last k issued.  The walk that uses them
-// issues no other vector-memory loads while one is in flight.
-#ifndef RT_PF_AHEAD
-#define RT_PF_AHEAD 1  // 0: glds copies of the popped node only (A/B)
-#endif
-#ifndef RT_PF_STAGE2
-#define RT_PF_STAGE2 96  // float4 of the second stage (72 = a 24-record leaf)
-#endif
-static constexpr int kStage2 = RT_PF_STAGE2;
-typedef __attribute__((address_space(3))) float4 lds_float4_t;
-// One glds wave instruction: lane l copies 16 bytes from its own global
-// address to dst + 16 l (dst wave-uniform, in M0).  Inline asm, so hipcc's
-// s_waitcnt bookkeeping does not see it: the builtin made hipcc wait
-// vmcnt(0) before every LDS read of the walk while a copy was in flight --
-// including a prefetch not yet needed (C5 trace 4.52 -> 5.57 ms).  An extra
-// vector-memory load the compiler does not know about only makes its own
-// vmcnt waits stricter (loads retire in order), so its loads stay safe; the
-// reads of a glds buffer are ordered by glds_wait.
-__device__ __forceinline__ void glds16(const float4* g, float4* dst) {
-  const uint32_t m = (uint32_t)(uintptr_t)(lds_float4_t*)dst;  // LDS byte address
-  uint32_t keep;
-  __asm__ volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                   : "=&s"(keep)
-                   : "v"(g), "s"(m)
-                   : "memory");
-}
-__device__ __forceinline__ int glds_issue(const float4* __restrict__ src, int n, float4* dst, int l) {
-  if (l < n) glds16(src + l, dst);
-  if (n <= 64) return 1;
-  if (l + 64 < n) glds16(src + 64 + l, dst + 64);
-  return 2;
-}
-__device__ __forceinline__ void glds_wait(int k) {  // k: glds instructions allowed to stay in flight
-  if (k <= 0)
-    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if (k == 1)
-    __asm__ volatile("s_waitcnt vmcnt(1)" ::: "memory");
-  else
-    __asm__ volatile("s_waitcnt vmcnt(2)" ::: "memory");
-}
-
-// The packet walk with the next node's payload in flight while a leaf is
-// tested (round 5; VERDICT r04 "two nodes in flight").  After a leaf nothing
-// is pushed, so the next pop is the stack top: its payload (child boxes or
-// leaf records) is copied global -> LDS into the second stage (glds, no
-// registers) as soon as the leaf's own copy is under way, and the next
-// iteration finds it there.  Same pops in the same order, same tests, same
-// decisions as staged_closest; a prefetched node the pruning then skips
-// costs only its copy.
-template <bool COUNT>
-__device__ void staged_closest_pf(const KParams& p, const Ray& r, bool act, Best& b, WaveCtx& w,
-                                  WorkCount& wc) {
-  const float4* __restrict__ node = p.node;
-  const float4* __restrict__ tri = p.tri;
-  uint64_t am = __ballot(act);
-  if (am == 0) return;
-  f3 inv = inv_dir(r.d);
-  uint32_t dm = wave_near_octant(act, r.d, am);
-  int sp = 0;
-  wave_sync();
-  if (w.lane < 2) w.stk2[w.lane] = node[w.lane];
-  if (w.lane == 0) w.stkm[0] = am;
-  sp = 1;
-  float limit = rt_prune_limit(b.dist, r.eps);
-  float4* cur = w.stage;
-  float4* alt = w.stage2;
-  int pf = -1;  // the stack slot whose payload is in flight into alt (RT_PF_AHEAD)
-  if (!RT_PF_AHEAD) alt = w.stage;
-  while (sp > 0) {
-    --sp;
-    wave_sync();
-    float4 lo = w.stk2[2 * sp], hi = w.stk2[2 * sp + 1];
-    uint64_t lm = w.stkm[sp];
-    uint32_t first = uni(__float_as_uint(lo.w)), info = uni(__float_as_uint(hi.w));
-    bool leaf = (info & RT_NODE_LEAF) != 0;
-    uint32_t cnt = leaf ? RT_LEAF_COUNT(info) : RT_NODE_COUNT(info);
-    if (pf == sp) {
-      float4* t = cur;  // the payload is already on its way into alt
-      cur = alt;
-      alt = t;
-    } else {
-      const int nn = leaf ? 3 * (int)chunk<kOctRecs>(cnt, 0) : 2 * (int)cnt;
-      if (nn > kStage2 && cur != w.stage) {  // only the first stage holds kStageOct
-        alt = cur;
-        cur = w.stage;
-      }
-      __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // no LDS read of cur still pending
-      glds_issue(leaf ? tri + 3 * (size_t)first : node + 2 * (size_t)first, nn, cur, w.lane);
-    }
-    pf = -1;
-    // lanes that wanted it when pushed, re-tested against their best so far
-    bool want = ((lm >> w.lane) & 1) != 0;
-    if (want && b.dist != __builtin_inff()) {
-      float tn = box_enter(r, inv, lo, hi);
-      want = !(tn * r.dlen > limit);
-    }
-    if (__ballot(want) == 0) continue;
-    if (COUNT) {
-      wc.nodes++;
-      wc.cl_nodes += (uint32_t)__popcll(__ballot(want));
-    }
-    int behind = 0;  // glds instructions issued after cur's
-    if (RT_PF_AHEAD && leaf && sp > 0) {
-      // the next pop is the stack top: start its payload now
-      const float4 nlo = w.stk2[2 * (sp - 1)], nhi = w.stk2[2 * (sp - 1) + 1];
-      const uint32_t nf = uni(__float_as_uint(nlo.w)), ni = uni(__float_as_uint(nhi.w));
-      const bool nleaf = (ni & RT_NODE_LEAF) != 0;
-      const uint32_t nc = nleaf ? RT_LEAF_COUNT(ni) : RT_NODE_COUNT(ni);
-      const int nn = nleaf ? 3 * (int)chunk<kOctRecs>(nc, 0) : 2 * (int)nc;
-      if (nn <= kStage2) {  // (a payload larger than the second stage is fetched when popped)
-        __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        behind = glds_issue(nleaf ? tri + 3 * (size_t)nf : node + 2 * (size_t)nf, nn, alt, w.lane);
-        pf = sp - 1;
-      }
-    }
-    glds_wait(behind);
-    wave_sync();
-    if (leaf) {
-      for (uint32_t base = 0; base < cnt; base += kOctRecs) {
-        uint32_t m = chunk<kOctRecs>(cnt, base);
-        if (base) {  // a leaf of more than kOctRecs records: the rest synchronously
-          glds_wait(0);
-          pf = -1;
-          stage_load(tri + 3 * (size_t)(first + base), 3 * (int)m, w);
-          stage_test(r, want, m, b, w.stage);
-        } else {
-          stage_test(r, want, m, b, cur);
-        }
-      }
-      limit = rt_prune_limit(b.dist, r.eps);
-      if (COUNT) {
-        wc.tris += cnt;
-        wc.cl_tris += cnt * (uint32_t)__popcll(__ballot(want));
-      }
-    } else {
-      float4* keep = w.stage;
-      w.stage = cur;  // stage_push_children reads the child boxes from w.stage
-      stage_push_children<false>(r, inv, dm, info, want, limit, sp, w, wc);
-      w.stage = keep;
-    }
-  }
-  glds_wait(0);  // no copy may land in a stage after the walk
-  wave_sync();
-}
-
 template <bool COUNT>
 __device__ void staged_closest(const KParams& p, const Ray& r, bool act, Best& b, WaveCtx& w,
                                WorkCount& wc) {
@@ -1237,19 +1252,10 @@ __device__ bool staged_any(const KParams& p, const Ray& r, bool act, WaveCtx& w,
 // shadow queries walk per lane, except directional-light shadows (parallel
 // rays, cpu/light.c:53) under RT_POLICY_DIR_STAGED.
 static constexpr int kPacketMin = 8;
-// The camera packet walk with the next payload in flight (staged_closest_pf,
-// VERDICT r04 item 2a) -- measured and OFF (profiles/r07_prefetch/): with the
-// second stage in LDS the trace kernel holds fewer waves per CU (8,192 B per
-// workgroup: 18 resident instead of 21, tools/micro/lds_occupancy.hip; trace
-// 4.52 -> 5.53 ms), and at full occupancy (a 64-float4 second stage, or an
-// 8-entry per-lane stack) still 4.50 -> 4.66-4.70 ms: with 5 waves per SIMD
-// the other waves already cover the payload latency, and the prefetch adds
-// the stack-top read, its waits and the copies of nodes the pruning skips.
-// The same walk with glds copies and no prefetch runs at the baseline
-// (4.51 ms).
-#ifndef RT_WALK_PREFETCH
-#define RT_WALK_PREFETCH 0
-#endif
+// (The camera packet walk with the next node's payload copied global -> LDS
+// while a leaf is tested measured slower -- round 5, profiles/r07_prefetch/:
+// a second LDS stage costs occupancy, and at full occupancy the other waves
+// already cover the payload latency -- and was removed.)
 // Camera rays only (round 4): the reflection rays of a wave diverge, and a
 // packet walks the union of their paths through cold nodes; per lane, the
 // longest items of an 8-way split (reflection-heavy tiles, tools/tile_cost.py)
@@ -1286,16 +1292,19 @@ __device__ __forceinline__ void closest_q(const KParams& p, const Ray& r, bool a
       flat_closest_w<COUNT>(p, r, act, b, w, wc);
     return;
   }
+  if (POL == RT_POLICY_EXACT_REFL && depth > 0) {  // reflection rays: the proven walk
+    LaneCount lc = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (act) oct_closest_rf<COUNT>(p, r, b, s, lc);
+    absorb<COUNT>(wc, lc, false);
+    return;
+  }
   bool staged = POL == RT_POLICY_STAGED ||
                 (POL != RT_POLICY_LANE && __popcll(__ballot(act)) >= kPacketMin &&
                  depth <= kPacketMaxDepth);
   if (staged) {
-    if (RT_WALK_PREFETCH && w.stage2)
-      staged_closest_pf<COUNT>(p, r, act, b, w, wc);
-    else
-      staged_closest<COUNT>(p, r, act, b, w, wc);
+    staged_closest<COUNT>(p, r, act, b, w, wc);
   } else {
-    LaneCount lc = {0, 0, 0, 0, 0, 0, 0};
+    LaneCount lc = {0, 0, 0, 0, 0, 0, 0, 0};
     if (act) oct_closest<COUNT>(p, r, b, s, lc);
     absorb<COUNT>(wc, lc, false);
     if (COUNT && depth > 0) {
@@ -1466,7 +1475,7 @@ __device__ __forceinline__ bool shadow_q(const KParams& p, f3 o, f3 d, uint32_t 
     return use_tp(p, act) ? flat_any_tp<COUNT>(p, r, act, wc) : flat_any_w<COUNT>(p, r, act, w, wc);
   if (POL == RT_POLICY_LBUF) {  // every such light has a buffer (rt_hip.cpp): no walk, no global prims
     const RtLightBuf& L = p.lbuf[li];
-    LaneCount lc = {0, 0, 0, 0, 0, 0, 0};
+    LaneCount lc = {0, 0, 0, 0, 0, 0, 0, 0};
     bool hit = act && (pre ? lbuf_scan<COUNT>(p, L, r, *pre, lc) : lbuf_any<COUNT>(p, L, r, lc));
     absorb<COUNT>(wc, lc, true);
     if (L.proven) {  // as below
@@ -1489,7 +1498,7 @@ __device__ __forceinline__ bool shadow_q(const KParams& p, f3 o, f3 d, uint32_t 
   } else if (p.lbuf && p.lbuf[li].kind != RT_LB_NONE) {
     walked = false;
     const RtLightBuf& L = p.lbuf[li];
-    LaneCount lc = {0, 0, 0, 0, 0, 0, 0};
+    LaneCount lc = {0, 0, 0, 0, 0, 0, 0, 0};
     hit = act && (pre ? lbuf_scan<COUNT>(p, L, r, *pre, lc) : lbuf_any<COUNT>(p, L, r, lc));
     absorb<COUNT>(wc, lc, true);
     if (L.proven) {
@@ -1507,7 +1516,7 @@ __device__ __forceinline__ bool shadow_q(const KParams& p, f3 o, f3 d, uint32_t 
       }
     }
   } else {
-    LaneCount lc = {0, 0, 0, 0, 0, 0, 0};
+    LaneCount lc = {0, 0, 0, 0, 0, 0, 0, 0};
     hit = act && oct_any<COUNT>(p, r, s, lc);
     absorb<COUNT>(wc, lc, true);
   }
@@ -1737,7 +1746,7 @@ __device__ __forceinline__ void flush_counts(const KParams& p, const WorkCount& 
                            wc.cl_nodes, wc.cl_tris, wc.sh_nodes,   wc.sh_tris,
                            wc.cy_cam,   wc.cy_cand, wc.cy_sec,     wc.cy_shadow,
                            wc.cy_shadow_dir, wc.stack_spills, wc.zero_risk,
-                           shade ? wc.nodes : 0u, shade ? wc.tris : 0u, wc.sh_unproven};
+                           shade ? wc.nodes : 0u, shade ? wc.tris : 0u, wc.sh_unproven, wc.cl_unproven};
 #pragma unroll
   for (int k = 0; k < RT_NSTATS; k++)
     if (lane == 0 && v[k])
@@ -1793,9 +1802,8 @@ template <int ACCEL, bool COUNT, int POL>
 __device__ __forceinline__ uint32_t trace_path(const KParams& p, bool valid, f3 o, f3 d,
                                                uint32_t x, Stack& s, WaveCtx& w, WorkCount& wc,
                                                uint32_t tile, int depth = 0, float coef = 1.0f,
-                                               uint32_t prev = RT_NO_REC, uint32_t path_slot = 0) {
-  // depth: wave-uniform, queries so far on this path (bounce_kernel resumes
-  // queued paths at depth 1 with their coefficient and deepest record)
+                                               uint32_t prev = RT_NO_REC) {
+  // depth: wave-uniform, queries so far on this path
   bool alive = valid;
   for (;;) {
     alive = alive && !((double)coef < 0.01);  // checked before the query
@@ -1859,29 +1867,6 @@ __device__ __forceinline__ uint32_t trace_path(const KParams& p, bool valid, f3 
     wc.overflow += (uint32_t)__popcll(__ballot(deep));
     alive = hit && depth + 1 < RT_MAX_BOUNCES;
     ++depth;
-    if (depth == 1 && p.sec_q) {
-      // camera paths end here: the lanes whose path goes on (checked as the
-      // loop would, coef >= 0.01) append their reflection ray to the
-      // secondary queue -- one atomic per wave -- and bounce_kernel continues
-      // them 64 to a wave, so a tile of long reflection paths no longer holds
-      // its camera wave (the N = 8 tail)
-      alive = alive && !((double)coef < 0.01);
-      const uint64_t qm = __ballot(alive);
-      if (qm) {
-        uint32_t qb = 0;
-        if (w.lane == 0) qb = atomicAdd(p.sec_count, (uint32_t)__popcll(qm));
-        qb = uni(qb);
-        if (alive) {
-          const uint32_t e = qb + (uint32_t)__popcll(qm & ((1ull << w.lane) - 1ull));
-          if (e < p.sec_cap) {  // (the queue holds every camera ray's: never full)
-            p.sec_q[2 * (size_t)e] = make_float4(o.x, o.y, o.z, coef);
-            p.sec_q[2 * (size_t)e + 1] = make_float4(d.x, d.y, d.z, __uint_as_float(prev));
-            p.sec_slot[e] = path_slot;
-          }
-        }
-      }
-      break;
-    }
   }
   return prev;
 }
@@ -1895,9 +1880,6 @@ __global__ __launch_bounds__(64, RT_TRACE_MIN_WAVES) void trace_kernel(KParams p
   // empty stack (wave_sync() at both ends orders the accesses).
   __shared__ float4 s_stack[ACCEL == RT_ACCEL_FLAT_D ? 1 : kStackArea];
   __shared__ float4 s_stage[ACCEL == RT_ACCEL_FLAT_D ? kStageFlat : kStageOct];
-  // the prefetching packet walk's second stage (8 KB of LDS per one-wave
-  // workgroup in all: 20 workgroups = 5 waves per SIMD fill the CU's 160 KB)
-  __shared__ float4 s_stage2[ACCEL == RT_ACCEL_FLAT_D || !RT_WALK_PREFETCH ? 1 : kStage2];
   const size_t gl = (size_t)blockIdx.x * 64 + (size_t)lane;
   Stack stk;
   stk.idx = (uint32_t*)s_stack;
@@ -1910,7 +1892,6 @@ __global__ __launch_bounds__(64, RT_TRACE_MIN_WAVES) void trace_kernel(KParams p
   w.stk2 = s_stack;
   w.stkm = (uint64_t*)(s_stack + 2 * kStack2);
   w.stage = s_stage;
-  w.stage2 = ACCEL == RT_ACCEL_FLAT_D || !RT_WALK_PREFETCH ? nullptr : s_stage2;
   w.lane = lane;
   // Work item = (tile t, sample s): the four samples of a tile run on four
   // waves, so a tile of long mirror paths (C2: the worst tile cost 7.7x a
@@ -1965,8 +1946,7 @@ __global__ __launch_bounds__(64, RT_TRACE_MIN_WAVES) void trace_kernel(KParams p
     const bool valid = camera_sample(p, t, smp, lane, point, dir);
     if (smp == 0) wc.pixels += (uint32_t)__popcll(__ballot(valid));
     p.last[(size_t)u * 64 + lane] =
-        trace_path<ACCEL, COUNT, POL>(p, valid, point, dir, x, stk, w, wc, t, 0, 1.0f, RT_NO_REC,
-                                      u * 64u + (uint32_t)lane);
+        trace_path<ACCEL, COUNT, POL>(p, valid, point, dir, x, stk, w, wc, t, 0, 1.0f, RT_NO_REC);
     if (prio) __builtin_amdgcn_s_setprio(0);
     if (p.item_cost && lane == 0) {  // the next frame's work order (rt_cand_order)
       const unsigned long long cy = __builtin_readcyclecounter() - c0;
@@ -1986,59 +1966,6 @@ __global__ __launch_bounds__(64, RT_TRACE_MIN_WAVES) void trace_kernel(KParams p
     }
   }
   if (p.cost_sum && lane == 0 && wave_cost) atomicAdd(p.cost_sum, wave_cost);
-  flush_counts(p, wc, lane);
-}
-
-// bounce_kernel: the reflection paths trace_kernel queued (p.sec_q), 64 per
-// wave in queue order (neighbouring camera waves' rays, so still coherent),
-// each continued from depth 1 exactly as trace_path's loop would -- same
-// queries, same records, same links -- to its end; the path's deepest record
-// replaces the camera record in last[] when the path made further hits.
-// Persistent one-wave workgroups pull 64-entry chunks from one counter.
-template <int ACCEL, bool COUNT, int POL>
-__global__ __launch_bounds__(64, RT_TRACE_MIN_WAVES) void bounce_kernel(KParams p) {
-  const int lane = threadIdx.x & 63;
-  WorkCount wc = {};
-  __shared__ float4 s_stack[ACCEL == RT_ACCEL_FLAT_D ? 1 : kStackArea];
-  __shared__ float4 s_stage[ACCEL == RT_ACCEL_FLAT_D ? kStageFlat : kStageOct];
-  const size_t gl = (size_t)blockIdx.x * 64 + (size_t)lane;
-  Stack stk;
-  stk.idx = (uint32_t*)s_stack;
-  stk.tt = (float*)s_stack + kLdsStack * 64;
-  stk.spill = p.spill + gl;
-  stk.stride = gridDim.x * 64u;
-  stk.lane = lane;
-  stk.sp = 0;
-  WaveCtx w;
-  w.stk2 = s_stack;
-  w.stkm = (uint64_t*)(s_stack + 2 * kStack2);
-  w.stage = s_stage;
-  w.stage2 = nullptr;
-  w.lane = lane;
-  const uint32_t n = min(*p.sec_count, p.sec_cap);
-  const uint32_t x = (uint32_t)blockIdx.x & 7u;  // hit-record region
-  for (uint32_t q = blockIdx.x;; ) {
-    if (q * 64u >= n) break;
-    const uint32_t e = q * 64u + (uint32_t)lane;
-    const bool valid = e < n;
-    f3 o{0.0f, 0.0f, 0.0f}, d{0.0f, 0.0f, 1.0f};
-    float coef = 0.0f;
-    uint32_t prev = RT_NO_REC, slot = 0;
-    if (valid) {
-      const float4 a = p.sec_q[2 * (size_t)e], b = p.sec_q[2 * (size_t)e + 1];
-      o = f3{a.x, a.y, a.z};
-      coef = a.w;
-      d = f3{b.x, b.y, b.z};
-      prev = __float_as_uint(b.w);
-      slot = p.sec_slot[e];
-    }
-    const uint32_t deepest = trace_path<ACCEL, COUNT, POL>(p, valid, o, d, x, stk, w, wc, 0u, 1, coef, prev, slot);
-    if (valid && deepest != prev) p.last[slot] = deepest;
-    // the first chunk of every wave without an atomic, the rest through the counter
-    uint32_t nq = 0;
-    if (lane == 0) nq = atomicAdd(p.sec_head, 1u);
-    q = uni(nq) + gridDim.x;
-  }
   flush_counts(p, wc, lane);
 }
 
@@ -2137,7 +2064,6 @@ __global__ __launch_bounds__(64, ACCEL == RT_ACCEL_FLAT_D ? RT_FLAT_SHADE_MIN_WA
   w.stk2 = s_stack;
   w.stkm = (uint64_t*)(s_stack + 2 * kStack2);
   w.stage = s_stage;
-  w.stage2 = nullptr;
   w.lane = lane;
   const uint32_t home = (uint32_t)blockIdx.x & 7u;
   uint32_t probe = 0;
@@ -2328,7 +2254,7 @@ __global__ __launch_bounds__(256) void probe_shadow_kernel(KParams p, const floa
       hit = any_hit_rec(r, t[0], t[1], t[2], risk);
     }
   } else {
-    LaneCount lc = {0, 0, 0, 0, 0, 0, 0};
+    LaneCount lc = {0, 0, 0, 0, 0, 0, 0, 0};
     hit = lbuf_any<false>(p, p.lbuf[li], r, lc);
   }
   out[i] = hit ? 1u : 0u;
@@ -2374,8 +2300,14 @@ __global__ __launch_bounds__(64) void probe_closest_kernel(KParams p, const floa
         consider(r, t[0], t[1], t[2], b);
       }
   } else {
-    LaneCount lc = {0, 0, 0, 0, 0, 0, 0};
-    if (act) oct_closest<false>(p, r, b, stk, lc);
+    LaneCount lc = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (act) {
+      if (p.node_rf)  // the exact reflection mode's walk (rt_hip_set_exact_reflections)
+        oct_closest_rf<false>(p, r, b, stk, lc);
+      else
+        oct_closest<false>(p, r, b, stk, lc);
+    }
+    if (act && lc.unproven) out[2 * (size_t)i + 1] = 0x7fc00001u;  // (never: |d| past RT_RF_DLMAX)
   }
   if (act) {
     out[2 * (size_t)i] = b.dist == __builtin_inff() ? 0xffffffffu : b.prim;
@@ -2400,7 +2332,7 @@ __global__ __launch_bounds__(256) void fold_kernel(KParams p) {
       for (int k = 0; k < RT_NSTATS; k++) s[k] += p.stats[set * RT_STAT_STRIDE + k];
     if (s[5]) f |= RT_FRAME_DEPTH;
     if (s[6] || s[18]) f |= RT_FRAME_ZERO;
-    if (s[21] || (p.oob_count && *p.oob_count > p.oob_cap)) f |= RT_FRAME_UNPROVEN;
+    if (s[21] || s[22] || (p.oob_count && *p.oob_count > p.oob_cap)) f |= RT_FRAME_UNPROVEN;
     if (p.list_flag && *p.list_flag) f |= RT_FRAME_LISTS;
     atomicOr(p.frame_check, (unsigned long long)f);
     atomicAdd(p.frame_check + 1, 1ull);
@@ -2539,7 +2471,6 @@ __global__ __launch_bounds__(64, RT_MIN_WAVES) void compat_kernel(KParams p) {
   w.stk2 = s_stack;
   w.stkm = (uint64_t*)(s_stack + 2 * kStack2);
   w.stage = s_stage;
-  w.stage2 = nullptr;
   w.lane = lane;
   uint32_t* img = (uint32_t*)p.out;
   for (;;) {
@@ -2665,18 +2596,6 @@ __global__ __launch_bounds__(256) void assemble_kernel(const float* __restrict__
 template <bool TRACE>
 static const void* kernel_of(int accel, int count_work, int policy);
 
-// bounce_kernel of the same instantiation as trace_kernel
-static const void* bounce_of(int accel, int count_work, int policy) {
-  using namespace rt;
-  if (accel == RT_ACCEL_FLAT_D)
-    return count_work ? (const void*)bounce_kernel<RT_ACCEL_FLAT_D, true, 0>
-                      : (const void*)bounce_kernel<RT_ACCEL_FLAT_D, false, 0>;
-  if (policy == RT_POLICY_LANE) return (const void*)bounce_kernel<RT_ACCEL_OCTREE_D, false, RT_POLICY_LANE>;
-  if (policy == RT_POLICY_STAGED) return (const void*)bounce_kernel<RT_ACCEL_OCTREE_D, false, RT_POLICY_STAGED>;
-  return count_work ? (const void*)bounce_kernel<RT_ACCEL_OCTREE_D, true, RT_POLICY_DEFAULT>
-                    : (const void*)bounce_kernel<RT_ACCEL_OCTREE_D, false, RT_POLICY_DEFAULT>;
-}
-
 template <bool TRACE>
 static const void* kernel_of(int accel, int count_work, int policy) {
   using namespace rt;
@@ -2688,6 +2607,9 @@ static const void* kernel_of(int accel, int count_work, int policy) {
                       : (const void*)shade_kernel<RT_ACCEL_FLAT_D, false, 0>;
   }
   if (TRACE) {
+    if (policy == RT_POLICY_EXACT_REFL)
+      return count_work ? (const void*)trace_kernel<RT_ACCEL_OCTREE_D, true, RT_POLICY_EXACT_REFL>
+                        : (const void*)trace_kernel<RT_ACCEL_OCTREE_D, false, RT_POLICY_EXACT_REFL>;
     if (policy == RT_POLICY_LANE) return (const void*)trace_kernel<RT_ACCEL_OCTREE_D, false, RT_POLICY_LANE>;
     if (policy == RT_POLICY_STAGED)
       return (const void*)trace_kernel<RT_ACCEL_OCTREE_D, false, RT_POLICY_STAGED>;
@@ -2727,11 +2649,7 @@ static hipError_t launch_kernel(const void* k, int grid, const KParams* p, hipSt
 
 extern "C" hipError_t rt_launch_trace(const KParams* p, int accel, int count_work, int policy,
                                       int grid, hipStream_t stream) {
-  hipError_t e = launch_kernel(kernel_of<true>(accel, count_work, policy), grid, p, stream);
-  if (e != hipSuccess || !p->sec_q) return e;
-  // the queued reflection paths (the queue's length is on the device: every
-  // wave exits at once on an empty queue)
-  return launch_kernel(bounce_of(accel, count_work, policy), grid, p, stream);
+  return launch_kernel(kernel_of<true>(accel, count_work, policy), grid, p, stream);
 }
 
 extern "C" hipError_t rt_launch_shade(const KParams* p, int accel, int count_work, int policy,

@@ -95,7 +95,8 @@ class Stats(C.Structure):
                 ("cycles_shadow_directional", C.c_ulonglong), ("stack_spills", C.c_ulonglong),
                 ("shadow_zero_risk", C.c_ulonglong), ("hit_records", C.c_ulonglong),
                 ("shadow_node_visits", C.c_ulonglong), ("shadow_tri_tests", C.c_ulonglong),
-                ("shadow_unproven", C.c_ulonglong), ("shadow_deferred", C.c_ulonglong)]
+                ("shadow_unproven", C.c_ulonglong), ("shadow_deferred", C.c_ulonglong),
+                ("closest_unproven", C.c_ulonglong)]
 
     def as_dict(self):
         return {k: int(getattr(self, k)) for k, _ in self._fields_}
@@ -111,11 +112,13 @@ class AccelInfo(C.Structure):
                 ("lightbuf_global", C.c_ulonglong), ("lightbuf_seconds", C.c_double),
                 ("lightbuf_never", C.c_ulonglong), ("lightbuf_band", C.c_ulonglong),
                 ("lightbuf_failed", C.c_ulonglong), ("lightbuf_fail_reason", C.c_char * 96),
-                ("trace_grid", C.c_int), ("shade_grid", C.c_int)]
+                ("trace_grid", C.c_int), ("shade_grid", C.c_int),
+                ("scene_center", C.c_float * 3), ("scene_radius", C.c_float)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_}
         d["lightbuf_fail_reason"] = d["lightbuf_fail_reason"].decode(errors="replace")
+        d["scene_center"] = list(d["scene_center"])
         return d
 
 
@@ -166,6 +169,7 @@ _PROTOS = [
     ("rt_hip_set_exact_camera", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_set_policy", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_set_exact_shadows", C.c_int, [C.c_void_p, C.c_int]),
+    ("rt_hip_set_exact_reflections", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_set_light_buffers", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_hip_set_lightbuf_entry_cap", C.c_int, [C.c_void_p, C.c_ulonglong]),
     ("rt_lightbuf_survey", C.c_int, [C.c_void_p, C.c_uint, C.c_int, C.c_uint, C.c_void_p]),
@@ -539,6 +543,13 @@ class Context:
         proven light buffers, the proven walk where a light's queries walk.
         Off: slack-grown buffers, measured against brute force, not proven."""
         _check(lib().rt_hip_set_exact_shadows(self.h, 1 if on else 0), "exact_shadows")
+
+    def set_exact_reflections(self, on=True):
+        """Reflection rays exact by proof (rt_hip_set_exact_reflections):
+        the reflection walk grows every node's box by the float test's error
+        region for the ray (csrc/rt_reflect.hip); the closest-hit probe uses
+        the same walk.  Off (the default): the culling slack, tested."""
+        _check(lib().rt_hip_set_exact_reflections(self.h, 1 if on else 0), "exact_reflections")
 
     def set_policy(self, policy):
         """Octree traversal policy (rt_hip_set_policy): 0 default, 1 per-lane,

@@ -71,6 +71,66 @@ def test_deep_reflections_bitexact(case, accel, gpu, tmp_path):
     assert st["depth_overflow"] == 0 and st["hit_records"] == st["closest"]
 
 
+@pytest.mark.parametrize("accel", ["octree", "octree_gpu"])
+@pytest.mark.parametrize("case", CASES + OWN_CASES, ids=[case_id(c) for c in CASES + OWN_CASES])
+def test_golden_exact_reflections(case, accel, gpu, scene_dir, tmp_path):
+    """The exact reflection mode (rt_hip_set_exact_reflections: the proven
+    reflection walk, csrc/rt_reflect.hip) renders every golden case -- the
+    reference's 20 scenes and the 44-bounce mirrors -- bit-exact, with the
+    reference's query counts."""
+    own = case in OWN_CASES
+    path = own_scene_path(case, tmp_path) if own else os.path.join(scene_dir, case["scene"] + ".svati")
+    s = gpu.Scene.load_svati(path)
+    if not own:
+        s.set_size(case["width"], case["height"])
+    ctx = gpu.Context(s, accel)
+    ctx.set_exact_reflections(True)
+    img, st = ctx.render_image(s.frame())
+    assert_bitexact(img, own_golden_image(case) if own else golden_image(case), f"{case_id(case)}/{accel}/exact-refl")
+    assert (st["closest"], st["shadow"]) == (case["closest"], case["shadow"])
+    assert st["depth_overflow"] == 0 and st["closest_unproven"] == 0
+
+
+@pytest.mark.parametrize("scene,W,H", [("car-on-road", 1920, 1080), ("spheres", 960, 540)])
+def test_exact_reflections_whole_frame(gpu, scene_dir, scene, W, H):
+    """Whole frames with the exact reflection walk == brute force over every
+    triangle (both octrees), same query counts."""
+    s = gpu.Scene.load_svati(os.path.join(scene_dir, scene + ".svati"))
+    s.set_size(W, H)
+    f = s.frame()
+    img_f, st_f = gpu.Context(s, "flat").render_image(f)
+    for accel in ("octree", "octree_gpu"):
+        ctx = gpu.Context(s, accel)
+        ctx.set_exact_reflections(True)
+        img, st = ctx.render_image(f)
+        assert_bitexact(img, img_f, f"{scene} {accel} exact reflections vs flat")
+        assert (st["closest"], st["shadow"]) == (st_f["closest"], st_f["shadow"])
+
+
+def test_exact_reflections_synthetic_frame(gpu):
+    """A 352k-triangle sphere field (1/8 of the spheres Nr 0.3, as C5) at
+    960x540 with the exact reflection walk == brute force, device octree."""
+    s = gpu.Scene.synthetic(6, 6, 9776, seed=0x5EED, width=960, height=540)
+    f = s.frame()
+    img_f, st_f = gpu.Context(s, "flat").render_image(f)
+    ctx = gpu.Context(s, "octree_gpu")
+    ctx.set_exact_reflections(True)
+    img, st = ctx.render_image(f)
+    assert_bitexact(img, img_f, "synthetic 960x540 exact reflections vs flat")
+    assert (st["closest"], st["shadow"]) == (st_f["closest"], st_f["shadow"])
+
+
+def test_exact_reflections_need_default_policy(gpu, scene_dir):
+    s = gpu.Scene.load_svati(os.path.join(scene_dir, "cube.svati"))
+    s.set_size(32, 32)
+    ctx = gpu.Context(s, "octree")
+    ctx.set_exact_reflections(True)
+    ctx.set_policy(1)
+    with pytest.raises(gpu.RtError) as e:
+        ctx.render_image(s.frame())
+    assert e.value.code == -1  # RT_EINVAL
+
+
 def test_endless_mirror_reports_depth(gpu, tmp_path):
     """Nr 1.0 mirrors facing each other: cpu/rt's recursion never ends (its
     stack overflows); the render stops each path at RT_MAX_BOUNCES and fails
@@ -899,17 +959,7 @@ def test_light_buffer_probe_grazing(gpu, li, exact):
                            f"(buffer lit, brute shadowed: {int((~got & ref).sum())}); first {bad[:5].tolist()}")
 
 
-@pytest.mark.parametrize("scene,accel", [("synthetic", "octree_gpu"), ("synthetic", "octree"),
-                                         ("car-on-road", "octree"), ("car-on-road", "octree_gpu")])
-def test_reflection_probe_grazing(gpu, scene_dir, scene, accel):
-    """VERDICT r04 item 4, route (b): reflection rays are walked per lane with
-    the culling slack (DESIGN.md §2 "Reflection rays: tested, not proven").
-    Rays built to cross triangles' planes at grazing angles (1e-7 .. 3e-2 rad,
-    tools/grazing.py grazing_rays: where the float Moller-Trumbore error
-    region is widest), half of them from origins on other triangles as a
-    reflection ray's are, queried through the walk exactly as a reflection
-    query (rt_hip_probe_closest) -- the winner's prim and new_dist bits equal
-    brute force over every triangle for every ray."""
+def _grazing_probe(gpu, scene_dir, scene):
     sys.path.insert(0, os.path.join(REPO, "tools"))
     from grazing import grazing_rays
     if scene == "synthetic":
@@ -919,30 +969,55 @@ def test_reflection_probe_grazing(gpu, scene_dir, scene, accel):
     tri = s.triangles_array()
     o, d = grazing_rays(tri, 3000, 40)
     assert len(o) > 60000
+    return s, tri, o, d
+
+
+@pytest.mark.parametrize("scene,accel", [("synthetic", "octree_gpu"), ("synthetic", "octree"),
+                                         ("car-on-road", "octree"), ("car-on-road", "octree_gpu")])
+def test_reflection_probe_grazing(gpu, scene_dir, scene, accel):
+    """Reflection rays exact by proof (rt_hip_set_exact_reflections, DESIGN.md
+    §2 "Reflection rays").  Rays built to cross triangles' planes at grazing
+    angles (1e-7 .. 3e-2 rad, tools/grazing.py grazing_rays: where the float
+    Moller-Trumbore error region is widest), half of them from origins on
+    other triangles as a reflection ray's are, queried through the proven
+    reflection walk (rt_hip_probe_closest): the winner's prim and new_dist
+    bits equal brute force over every triangle for EVERY ray -- including
+    the coplanar-grazing rays the culling slack misses (round 5)."""
+    s, tri, o, d = _grazing_probe(gpu, scene_dir, scene)
     ctx = gpu.Context(s, accel)
+    ctx.set_exact_reflections(True)
     pw, dw = ctx.probe_closest(o, d)
     pb, db = ctx.probe_closest(o, d, brute=True)
     hit = pb != 0xFFFFFFFF
     assert 0.05 < hit.mean() < 0.999, hit.mean()
     bad = np.flatnonzero((pw != pb) | (dw.view(np.uint32) != db.view(np.uint32)))
-    # A differing ray is allowed only in the residual-risk class the walk's
-    # slack cannot cover: the reference's winner is a float garbage hit on a
-    # triangle whose plane (nearly) CONTAINS the ray -- then a, s.h and d.q
-    # of cpu/hit.c:15-33 are all rounding noise and the float test accepts it
-    # from anywhere in the plane (round 5 found such rays with this probe:
-    # DESIGN.md §2 "Reflection rays").  Every other ray must be bit-exact.
+    assert len(bad) == 0, (f"{len(bad)} of {len(o)} grazing reflection rays differ from brute force: "
+                           f"first {bad[:5].tolist()}")
+
+
+@pytest.mark.parametrize("scene,accel", [("synthetic", "octree_gpu"), ("car-on-road", "octree")])
+def test_reflection_probe_grazing_slack_walk(gpu, scene_dir, scene, accel):
+    """The same probe through the default reflection walk (the culling slack,
+    not proven): a measurement of its residual class, not a guarantee.  Every
+    differing ray must be a float garbage hit on a triangle whose plane
+    (nearly) contains the ray (tools/grazing.py coplanar_grazing: a, s.h and
+    d.q of cpu/hit.c:15-33 are all rounding noise) -- the class round 5 found
+    and the exact mode closes."""
+    s, tri, o, d = _grazing_probe(gpu, scene_dir, scene)
+    ctx = gpu.Context(s, accel)
+    pw, dw = ctx.probe_closest(o, d)
+    pb, db = ctx.probe_closest(o, d, brute=True)
+    bad = np.flatnonzero((pw != pb) | (dw.view(np.uint32) != db.view(np.uint32)))
     from grazing import coplanar_grazing, float_mt
     unexplained = []
     for i in bad:
         idx, dist = float_mt(tri, o[i], d[i])
         assert len(idx) and dist.min().view(np.uint32) == db[i].view(np.uint32), i  # brute's winner found
-        k = idx[np.argmin(dist)]
-        if not coplanar_grazing(tri[k], o[i], d[i]):
+        if not coplanar_grazing(tri[idx[np.argmin(dist)]], o[i], d[i]):
             unexplained.append(int(i))
-    print(f"{scene}/{accel}: {len(o)} grazing rays, {len(bad)} differ, all coplanar-grazing: {not unexplained}")
-    assert not unexplained, (f"{len(unexplained)} of {len(o)} grazing reflection rays differ from brute force "
-                             f"outside the coplanar-grazing class: {unexplained[:5]}")
-    assert len(bad) <= 1e-3 * len(o), len(bad)
+    print(f"{scene}/{accel} slack walk: {len(o)} grazing rays, {len(bad)} differ, all coplanar-grazing: "
+          f"{not unexplained}")
+    assert not unexplained, unexplained[:5]
 
 
 def test_empty_rank_on_fresh_context(gpu, scene_dir, manifest):
