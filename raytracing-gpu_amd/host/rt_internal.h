@@ -6,6 +6,7 @@
 #include <stdint.h>
 
 #include "rt_hip.h"
+#include "rt_hip_test.h"
 #include "rt_scene.h"
 
 #ifdef __cplusplus

@@ -17,12 +17,30 @@ CASES = load_manifest_static()
 
 def _header_functions():
     names = set()
-    for h in ("rt_scene.h", "rt_hip.h"):
+    for h in ("rt_scene.h", "rt_hip.h", "rt_hip_test.h"):
         src = open(os.path.join(REPO, "include", h)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
         for m in re.finditer(r"^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b(rt_\w+)\s*\(", src, re.M):
             names.add(m.group(1))
     return sorted(names)
+
+
+def test_public_header_is_the_drop_in_boundary():
+    """include/rt_hip.h declares the drop-in ABI (context,
+    render, stats, assemble, multi-rank lists, rt_raytrace*, device memory
+    helpers, exactness modes); probes, surveys, verification and A/B knobs
+    live in include/rt_hip_test.h only."""
+    def decls(h):
+        src = re.sub(r"/\*.*?\*/", "", open(os.path.join(REPO, "include", h)).read(), flags=re.S)
+        return {m.group(1) for m in re.finditer(r"^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b(rt_\w+)\s*\(", src, re.M)}
+    pub, tst = decls("rt_hip.h"), decls("rt_hip_test.h")
+    assert not pub & tst
+    for hook in ("rt_hip_probe_closest", "rt_hip_set_policy", "rt_cand_survey", "rt_hip_cand_verify",
+                 "rt_hip_set_cull_slack", "rt_hip_frame_times", "rt_accel_probe"):
+        assert hook in tst and hook not in pub, hook
+    for entry in ("rt_hip_create", "rt_hip_render", "rt_hip_stats", "rt_hip_destroy", "rt_raytrace",
+                  "rt_raytrace_multi", "rt_hip_assemble", "rt_hip_cand_produce", "rt_hip_cand_consume"):
+        assert entry in pub, entry
 
 
 def test_library_exports_every_header_symbol(built):
