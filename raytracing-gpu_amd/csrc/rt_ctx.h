@@ -28,7 +28,6 @@
 #include "rt_lightbuf.h"
 #include "rt_shadow.h"
 #include "rt_reflect.h"
-#include "rt_entry.h"
 #include "rt_tiles.h"
 
 extern "C" {
@@ -68,10 +67,6 @@ extern "C" {
 #endif
 // asynchronous list builds for a new camera of the same size and rank split,
 // sized from the last build + headroom (cand_prepare; A/B knob)
-// entry depth of the camera packet walk's per-tile entry nodes (0: root)
-#ifndef RT_ENTRY_DEPTH_DEFAULT
-#define RT_ENTRY_DEPTH_DEFAULT 4
-#endif
 #ifndef RT_ASYNC_NEW_CAMERA
 #define RT_ASYNC_NEW_CAMERA 1
 #endif
@@ -179,12 +174,6 @@ struct rt_hip_ctx {
   // exact reflection rays (csrc/rt_reflect.hip, rt_hip_set_exact_reflections):
   // per-node error-region bounds, built once per tree when the mode is enabled
   int exact_refl = 0;
-  // per-tile entry nodes of the camera packet walk (csrc/rt_entry.hip); depth
-  // 0: every camera walk starts at the root (RT_ENTRY_DEPTH at creation)
-  int entry_depth = RT_ENTRY_DEPTH_DEFAULT;
-  uint32_t* d_entry_n = nullptr;
-  uint32_t* d_entry = nullptr;
-  size_t entry_cap = 0;  // tiles
   float4* d_node_rf = nullptr;
   unsigned long long rf_unbounded = 0;  // leaves holding a triangle no bound covers
   float sh_ulps = -1.0f;

@@ -59,8 +59,6 @@ extern "C" void rt_hip_destroy(rt_hip_ctx* c) {
   (void)hipFree(c->d_oob_count);
   (void)hipFree(c->d_frame_check);
   (void)hipFree(c->d_node_rf);
-  (void)hipFree(c->d_entry_n);
-  (void)hipFree(c->d_entry);
   (void)hipFree(c->d_sh_global);
   for (LBDevice* d : c->lb_dev) rt_lightbuf_free(d);
   (void)hipFree(c->d_lbuf);
@@ -336,7 +334,6 @@ extern "C" int rt_hip_create(int device, const rt_scene* scene, int accel, rt_hi
   rt_hip_ctx* c = new rt_hip_ctx();
   if (const char* e = std::getenv("RT_CAND_REFINE")) c->cand_refine = std::atoi(e) != 0;  // A/B knob
   if (const char* e = std::getenv("RT_ASYNC_LISTS")) c->async_lists = std::atoi(e) != 0;  // A/B knob
-  if (const char* e = std::getenv("RT_ENTRY_DEPTH")) c->entry_depth = std::atoi(e);       // A/B knob
   c->device = device;
   c->accel = dev_build ? (fs.ntri ? RT_ACCEL_OCTREE : RT_ACCEL_FLAT) : accel;
   c->nrec = (uint32_t)fs.nrec;
@@ -609,66 +606,6 @@ static int hit_buffers(rt_hip_ctx* c, size_t ntiles) {
   return RT_OK;
 }
 
-// The camera packet walk's per-tile entry nodes of this frame and rank
-// (csrc/rt_entry.hip): one launch, no host wait.
-static int entry_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream_t s) {
-  const size_t nt = (size_t)kp->ntiles_local;
-  if (nt > c->entry_cap) {
-    (void)hipFree(c->d_entry_n);
-    (void)hipFree(c->d_entry);
-    c->d_entry_n = c->d_entry = nullptr;
-    c->entry_cap = 0;
-    HIP_TRY(hipMalloc((void**)&c->d_entry_n, nt * sizeof(uint32_t)));
-    HIP_TRY(hipMalloc((void**)&c->d_entry, nt * RT_ENTRY_MAX * sizeof(uint32_t)));
-    c->entry_cap = nt;
-  }
-  EntryParams ep;
-  std::memset(&ep, 0, sizeof ep);
-  ep.node = c->d_node;
-  ep.depth = c->entry_depth;
-  const double u[3] = {f->u.x, f->u.y, f->u.z}, v[3] = {f->v.x, f->v.y, f->v.z};
-  const double pos[3] = {f->position.x, f->position.y, f->position.z}, C[3] = {f->C.x, f->C.y, f->C.z};
-  const double w[3] = {u[1] * v[2] - u[2] * v[1], u[2] * v[0] - u[0] * v[2], u[0] * v[1] - u[1] * v[0]};
-  const double ww = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
-  if (!(ww > 0.0)) return rt_set_error(RT_EINVAL, "degenerate camera frame");
-  const double L = ((C[0] - pos[0]) * w[0] + (C[1] - pos[1]) * w[1] + (C[2] - pos[2]) * w[2]) / ww;
-  const double ku[3] = {v[1] * w[2] - v[2] * w[1], v[2] * w[0] - v[0] * w[2], v[0] * w[1] - v[1] * w[0]};
-  const double kv[3] = {w[1] * u[2] - w[2] * u[1], w[2] * u[0] - w[0] * u[2], w[0] * u[1] - w[1] * u[0]};
-  for (int a = 0; a < 3; a++) {
-    ep.pos[a] = (float)pos[a];
-    ep.w[a] = (float)w[a];
-    ep.ku[a] = (float)ku[a];
-    ep.kv[a] = (float)kv[a];
-  }
-  ep.L = (float)L;
-  // the camera rays' largest culling slack (host/rt_cull.h, at the film's
-  // corners: |o - c|_max is convex), doubled
-  double em = 0.0;
-  const double cmag = std::fmax(std::fabs(c->scene_c[0]), std::fmax(std::fabs(c->scene_c[1]), std::fabs(c->scene_c[2])));
-  for (int cr = 0; cr < 4; cr++) {
-    const double k = (cr & 1) ? f->width * 0.5 + 1.0 : -f->width * 0.5 - 1.0;
-    const double l = (cr & 2) ? f->height * 0.5 + 1.0 : -f->height * 0.5 - 1.0;
-    double m = 0.0;
-    for (int a = 0; a < 3; a++) m = std::fmax(m, std::fabs(C[a] + u[a] * k + v[a] * l - c->scene_c[a]));
-    const double e = (double)(c->cam_eps_ulps * 5.9604645e-8f) * (m + c->scene_r) +
-                     (double)RT_CULL_PLANE * (cmag + c->scene_r) + 1e-6;
-    em = std::fmax(em, e);
-  }
-  ep.grow = (float)(2.0 * em * (1.0 + 1e-3));
-  ep.W = f->width;
-  ep.H = f->height;
-  ep.tiles_x = tiles_x_of(f->width);
-  ep.rank = kp->rank;
-  ep.nranks = kp->nranks;
-  ep.ntiles = (uint32_t)nt;
-  ep.entry_n = c->d_entry_n;
-  ep.entry = c->d_entry;
-  HIP_TRY(rt_entry_build(&ep, s));
-  kp->entry_n = c->d_entry_n;
-  kp->entry = c->d_entry;
-  return RT_OK;
-}
-
 extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nranks,
                              float* d_tiles, void* stream) {
   if (!c || !f || !d_tiles) return rt_set_error(RT_EINVAL, "null argument");
@@ -820,10 +757,6 @@ extern "C" int rt_hip_render(rt_hip_ctx* c, const rt_frame* f, int rank, int nra
     }
   }
   if (!(c->accel == RT_ACCEL_OCTREE && c->d_node && c->exact_camera && !use_ext)) c->last_async = 0;
-  if (c->accel == RT_ACCEL_OCTREE && c->d_node && c->entry_depth > 0) {
-    int rc = entry_prepare(c, f, &p, s);
-    if (rc) return rc;
-  }
   // an empty octree scene has nothing to traverse: the FLAT kernels with 0
   // records are exact (their grids are the FLAT instantiation's own)
   const bool empty = c->accel == RT_ACCEL_OCTREE && !c->d_node;

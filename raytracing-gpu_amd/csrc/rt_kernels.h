@@ -174,11 +174,6 @@ struct KParams {
   // the heavy tiles at the front of tile_order (rt_cand_order's count, on
   // the device; NULL: none): their items run at raised wave priority
   const uint32_t* n_heavy;
-  // per-tile entry nodes of the camera packet walk (csrc/rt_entry.hip):
-  // entry_n[t] of them (RT_ENTRY_ROOT: the root), RT_ENTRY_MAX per tile in
-  // entry, near to far; NULL: every camera walk starts at the root
-  const uint32_t* entry_n;
-  const uint32_t* entry;
   // per-frame completeness check (fold_kernel, the frame's last launch): the
   // conditions rt_hip_stats reports as errors, ORed into frame_check[0]
   // (RT_FRAME_*), frame_check[1] += 1 frame, [2] / [3] += its closest-hit /

@@ -719,7 +719,7 @@ int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream_t s, i
   // frame's earlier build; a fresh frame (a new camera: the build read its
   // total back anyway) reads its own back after the compaction's scan -- one
   // more short host wait instead of sorting the dropped entries
-  // (for a new camera the last frame's kept count + 1/8: the scatter writes
+  // (for a new camera the last frame's kept count + 1/16: the scatter writes
   // the unused tail as dropped, and a count past it sets ctr[7])
   const bool kept_same = c->kept_for.same(f, kp->rank, kp->nranks);
   const bool compact_known = RT_COMPACT_LISTS && async && c->cand_refine && c->kept_ready &&
@@ -748,7 +748,7 @@ int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream_t s, i
     // never expected -- leave a tail the scatter writes as dropped)
     uint32_t cap = total;
     if (compact_known) {
-      cap = kept_same ? c->kept : c->kept + c->kept / 8 + 4096;
+      cap = kept_same ? c->kept : c->kept + c->kept / 16 + 4096;
       if (cap > total) cap = total;
     }
     HIP_TRY(rt_cand_compact(c->d_cand_keys, c->d_cand_vals, total, c->d_cand_ctr + 6, (uint32_t)nt, cap, cnt, off,

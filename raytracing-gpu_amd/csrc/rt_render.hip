@@ -24,7 +24,6 @@
 
 #include "rt_cull.h"
 #include "rt_device.h"
-#include "rt_entry.h"
 #include "rt_kernels.h"
 #include "rt_reflect.h"
 #include "rt_tiles.h"
@@ -1134,41 +1133,9 @@ __device__ __forceinline__ void stage_push_children(const Ray& r, f3 inv, uint32
   }
 }
 
-// The camera packet walk's start from the tile's entry nodes (csrc/rt_entry.hip):
-// their records staged through LDS, each box tested by every lane, pushed
-// far to near with the mask of the lanes that want it -- as a node's
-// children are.  Returns false when the tile has none listed (RT_ENTRY_ROOT:
-// start at the root).
-__device__ __forceinline__ bool push_entries(const KParams& p, const Ray& r, f3 inv, bool act, uint32_t tile,
-                                             int& sp, WaveCtx& w, WorkCount& wc) {
-  const uint32_t n = __builtin_amdgcn_readfirstlane(p.entry_n[tile]);
-  if (n == RT_ENTRY_ROOT) return false;
-  const uint32_t* e = p.entry + (size_t)tile * RT_ENTRY_MAX;
-  wave_sync();  // after the previous readers of stage
-  if ((uint32_t)w.lane < 2 * n) {
-    const uint32_t ni = e[w.lane >> 1];
-    w.stage[w.lane] = p.node[2 * (size_t)ni + (w.lane & 1)];
-  }
-  wave_sync();
-  for (int j = (int)n - 1; j >= 0; --j) {  // stored near to far: the nearest ends on top
-    const float4 lo = w.stage[2 * j], hi = w.stage[2 * j + 1];
-    const bool want = act && box_enter(r, inv, lo, hi) != __builtin_inff();
-    const uint64_t lm = __ballot(want);
-    if (lm == 0) continue;
-    if (sp < kStack2) {
-      if (w.lane < 2) w.stk2[2 * sp + w.lane] = w.lane ? hi : lo;
-      if (w.lane == 0) w.stkm[sp] = lm;
-      sp++;
-    } else {
-      wc.overflow++;  // RT_EDEPTH, never silent
-    }
-  }
-  return true;
-}
-
 template <bool COUNT>
 __device__ void staged_closest(const KParams& p, const Ray& r, bool act, Best& b, WaveCtx& w,
-                               WorkCount& wc, uint32_t tile = 0xffffffffu) {
+                               WorkCount& wc) {
   const float4* __restrict__ node = p.node;
   const float4* __restrict__ tri = p.tri;
   uint64_t am = __ballot(act);
@@ -1176,12 +1143,10 @@ __device__ void staged_closest(const KParams& p, const Ray& r, bool act, Best& b
   f3 inv = inv_dir(r.d);
   uint32_t dm = wave_near_octant(act, r.d, am);
   int sp = 0;
-  if (!(p.entry_n && tile != 0xffffffffu && push_entries(p, r, inv, act, tile, sp, w, wc))) {
-    wave_sync();
-    if (w.lane < 2) w.stk2[w.lane] = node[w.lane];
-    if (w.lane == 0) w.stkm[0] = am;
-    sp = 1;
-  }
+  wave_sync();
+  if (w.lane < 2) w.stk2[w.lane] = node[w.lane];
+  if (w.lane == 0) w.stkm[0] = am;
+  sp = 1;
   float limit = rt_prune_limit(b.dist, r.eps);
   while (sp > 0) {
     --sp;
@@ -1319,7 +1284,7 @@ __device__ __forceinline__ bool use_tp(const KParams& p, bool act) {
 // Closest-hit query; converged call, act = lane has a query.
 template <int ACCEL, bool COUNT, int POL>
 __device__ __forceinline__ void closest_q(const KParams& p, const Ray& r, bool act, int depth, Best& b,
-                                          Stack& s, WaveCtx& w, WorkCount& wc, uint32_t tile = 0xffffffffu) {
+                                          Stack& s, WaveCtx& w, WorkCount& wc) {
   if (ACCEL == RT_ACCEL_FLAT_D) {
     if (use_tp(p, act))
       flat_closest_tp<COUNT>(p, r, act, b, wc);
@@ -1337,7 +1302,7 @@ __device__ __forceinline__ void closest_q(const KParams& p, const Ray& r, bool a
                 (POL != RT_POLICY_LANE && __popcll(__ballot(act)) >= kPacketMin &&
                  depth <= kPacketMaxDepth);
   if (staged) {
-    staged_closest<COUNT>(p, r, act, b, w, wc, depth == 0 ? tile : 0xffffffffu);
+    staged_closest<COUNT>(p, r, act, b, w, wc);
   } else {
     LaneCount lc = {0, 0, 0, 0, 0, 0, 0, 0};
     if (act) oct_closest<COUNT>(p, r, b, s, lc);
@@ -1854,7 +1819,7 @@ __device__ __forceinline__ uint32_t trace_path(const KParams& p, bool valid, f3 
     b.u = b.v = 0.0f;
     b.t = 0.0f;
     uint64_t c0 = COUNT ? __builtin_readcyclecounter() : 0ull;
-    closest_q<ACCEL, COUNT, POL>(p, r, alive, depth, b, s, w, wc, tile);
+    closest_q<ACCEL, COUNT, POL>(p, r, alive, depth, b, s, w, wc);
     if (COUNT) {
       const uint64_t c1 = __builtin_readcyclecounter();
       (depth == 0 ? wc.cy_cam : wc.cy_sec) += (uint32_t)(c1 - c0);

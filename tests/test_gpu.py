@@ -120,39 +120,6 @@ def test_exact_reflections_synthetic_frame(gpu):
     assert (st["closest"], st["shadow"]) == (st_f["closest"], st_f["shadow"])
 
 
-@pytest.mark.parametrize("scene", ["synthetic", "car-on-road"])
-def test_entry_nodes_same_image(gpu, scene_dir, scene, monkeypatch):
-    """The camera packet walk from per-tile entry nodes (csrc/rt_entry.hip,
-    RT_ENTRY_DEPTH) renders the same bits and query counts as the walk from
-    the root, at several entry depths and a 3-rank split."""
-    if scene == "synthetic":
-        s = gpu.Scene.synthetic(6, 6, 9776, seed=0x5EED, width=960, height=540)
-        accel = "octree_gpu"
-    else:
-        s = gpu.Scene.load_svati(os.path.join(scene_dir, scene + ".svati"))
-        s.set_size(960, 540)
-        accel = "octree"
-    f = s.frame()
-    imgs = {}
-    for depth in (0, 2, 4, 7):
-        monkeypatch.setenv("RT_ENTRY_DEPTH", str(depth))
-        ctx = gpu.Context(s, accel)
-        imgs[depth] = ctx.render_image(f)
-        if depth == 4:
-            n = 3
-            per = gpu.tile_buffer_floats(f.width, f.height, n)
-            tiles = [_tiles_of_rank(ctx, f, r, n)[0] for r in range(n)]
-    ref, st0 = imgs[0]
-    for depth, (img, st) in imgs.items():
-        assert_bitexact(img, ref, f"{scene} entry depth {depth} vs root")
-        assert (st["closest"], st["shadow"]) == (st0["closest"], st0["shadow"])
-    monkeypatch.setenv("RT_ENTRY_DEPTH", "0")
-    ctx0 = gpu.Context(s, accel)
-    for r in range(3):
-        t0, _ = _tiles_of_rank(ctx0, f, r, 3)
-        assert np.array_equal(t0.view(np.uint32), tiles[r].view(np.uint32)), r
-
-
 def test_exact_reflections_need_default_policy(gpu, scene_dir):
     s = gpu.Scene.load_svati(os.path.join(scene_dir, "cube.svati"))
     s.set_size(32, 32)
