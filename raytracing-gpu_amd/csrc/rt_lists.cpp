@@ -862,9 +862,12 @@ extern "C" int rt_hip_cand_produce(rt_hip_ctx* c, const rt_frame* f, int rank, i
   const int tb = rt_block_side(nranks);
   // key = rank << tbits | local tile (tpr: a global), rank nranks for an
   // entry the refinement dropped (or, in an asynchronous build, past the
-  // build's own total); then a stable partition by rank: each rank's entries
-  // keep their emission order, which the consumer's stable sort by tile
-  // turns into the per-tile order of the rank's own build
+  // build's own total); then a stable partition by rank.  The consumer's
+  // stable sort by tile gives each tile the same entries as the rank's own
+  // build -- in the producers' interleaved slice order, not necessarily the
+  // same order within a tile, which the render does not depend on (the
+  // winner is the lexicographic (new_dist, prim) minimum, rt_render.hip
+  // consider_exact)
   const int tbits = key_bits((size_t)tpr + 1);
   if (nranks > 256 || tbits + key_bits((size_t)nranks + 1) > 32)
     return rt_set_error(RT_EINVAL, "%d ranks x %u tiles per rank: routed keys exceed 32 bits", nranks, tpr);

@@ -1022,7 +1022,8 @@ def test_reflection_probe_grazing_slack_walk(gpu, scene_dir, scene, accel):
 
 def test_empty_rank_on_fresh_context(gpu, scene_dir, manifest):
     """A rank past the frame's last tile block renders nothing: 96x54 over 8
-    ranks has 6 blocks of 4x4 tiles, so ranks 6 and 7 own none.  On a fresh
+    ranks has 3 x 2 blocks of 4x4 tiles on the diagonal map (block (bx, by) ->
+    rank (bx + by) mod 8), so ranks 4 to 7 own none.  On a fresh
     context the render succeeds with zero counts, and the 8-rank assemble of
     all ranks (the empty ones' buffers as padding) is the golden image."""
     import ctypes as C
