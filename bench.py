@@ -438,6 +438,9 @@ def main():
     # --camera-pan pixels per step): a one-shot render or an animation
     # reuses nothing of an earlier identical frame (the lists' sizes, kept
     # count and work order are rebuilt with their read-backs)
+    # the timed frame's image, for the CPU baseline's pixel check (the
+    # fresh-camera frames below overwrite rgb with panned views)
+    img_timed = rgb.clone() if rank == 0 and world == 1 and not args.no_cpu else None
     fresh = None
     if args.camera_pan > 0:
         cam0 = rtgpu.Camera()
@@ -600,7 +603,7 @@ def main():
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu:
-            img = rgb.view(H, W, 3).cpu().numpy()
+            img = img_timed.view(H, W, 3).cpu().numpy()
             thr = args.cpu_threads or min(len(os.sched_getaffinity(0)) or 1,
                                           int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or 16)
             log(f"[rank 0] cpu baseline: {args.cpu_seconds:.0f}s of samples (Mode A 4 threads, "
