@@ -478,20 +478,24 @@ def main():
             dist.barrier()
         el_f = time.perf_counter() - t1
         ftf = ctx.frame_times(min(args.steps, 1024))
+        ktf = ctx.kernel_times(min(args.steps, 1024))
         # (an extra measurement: an incomplete frame here -- a new camera whose
         # lists outgrew the estimate from the last frame, rendered again by a
         # caller that checks rt_hip_stats -- voids only these numbers)
         fresh_q, why = frame_checked(ctx, rank, world, frames[-1], args.steps, "fresh-camera", fatal=False)
         ctx.set_timing(False)
-        tf = torch.tensor([el_f, sum(a for a, _ in ftf) / len(ftf)], dtype=torch.float64, device=dev)
+        tf = torch.tensor([el_f, sum(a for a, _ in ftf) / len(ftf)] +
+                          [sum(k[i] for k in ktf) / len(ktf) for i in range(3)], dtype=torch.float64, device=dev)
         if world > 1:
             dist.all_reduce(tf, op=dist.ReduceOp.MAX)
-        el_f, lists_f = tf.tolist()
+        el_f, lists_f, trace_f, shade_f, fold_f = tf.tolist()
         fresh = {"pan_px_per_step": args.camera_pan, "pan_world_units_per_step": round(step_units, 6),
                  "frames": args.steps,
                  "ms_per_step": round(el_f / args.steps * 1e3, 3) if fresh_q is not None else None,
                  "value": round(fresh_q / el_f / 1e6, 3) if fresh_q is not None else None,
-                 "candidate_lists_ms": round(lists_f, 3), "incomplete": why}
+                 "candidate_lists_ms": round(lists_f, 3),
+                 "kernel_ms": {"trace": round(trace_f, 3), "shade": round(shade_f, 3), "fold": round(fold_f, 3)},
+                 "incomplete": why}
     trace_ms = sum(a for a, _, _ in kt) / len(kt)
     shade_ms = sum(b for _, b, _ in kt) / len(kt)
     fold_ms = sum(c for _, _, c in kt) / len(kt)
