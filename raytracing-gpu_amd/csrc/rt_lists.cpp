@@ -190,7 +190,10 @@ static int grow_dev(T** p, size_t* cap, size_t need) {
   if (need <= *cap && *p) return RT_OK;
   (void)hipFree(*p);
   *p = nullptr;
-  size_t n = need + need / 4 + 64;
+  // headroom past a new camera's estimate (the last build's size + 1/4 +
+  // 4096, cand_prepare): growing a buffer frees the old one, and hipFree
+  // waits for the device -- a whole frame's host lead lost mid-build
+  size_t n = need + need / 2 + 8192;
   HIP_TRY(hipMalloc((void**)p, n * sizeof(T)));
   *cap = n;
   return RT_OK;
@@ -357,6 +360,7 @@ static int ensure_tmp(rt_hip_ctx* c, size_t bytes) {
   if (bytes <= c->scan_tmp_bytes && c->d_scan_tmp) return RT_OK;
   (void)hipFree(c->d_scan_tmp);
   c->d_scan_tmp = nullptr;
+  bytes += bytes / 2 + 65536;  // headroom (as grow_dev): a new camera's sort is a little longer
   HIP_TRY(hipMalloc(&c->d_scan_tmp, bytes));
   c->scan_tmp_bytes = bytes;
   return RT_OK;
@@ -737,7 +741,7 @@ int cand_prepare(rt_hip_ctx* c, const rt_frame* f, KParams* kp, hipStream_t s, i
       (void)hipFree(c->d_part);
       c->d_part = nullptr;
       c->part_cap = 0;
-      const size_t cap = 2 * ((size_t)nw + nw / 4) + 1024;
+      const size_t cap = 2 * ((size_t)nw + nw / 2) + 1024;  // headroom (as grow_dev)
       HIP_TRY(hipMalloc((void**)&c->d_part, cap * sizeof(uint32_t)));
       c->part_cap = cap;
     }
