@@ -759,6 +759,49 @@ def test_async_lists_repeated_frame(gpu):
         assert st1["cand_entries"] == st0["cand_entries"] > 0
 
 
+def _panned_frame(gpu, scene, du):
+    """The scene's frame with the eye moved du world units along the film's
+    u axis (bench.py --camera-pan's new cameras)."""
+    import ctypes as C
+    cam = gpu.Camera()
+    C.pointer(cam)[0] = scene.s.camera
+    f0 = scene.frame()
+    u = np.array([f0.u.x, f0.u.y, f0.u.z], np.float64)
+    u /= np.linalg.norm(u)
+    cam.position.x += float(u[0] * du)
+    cam.position.y += float(u[1] * du)
+    cam.position.z += float(u[2] * du)
+    f = gpu.Frame()
+    gpu._check(gpu.lib().rt_frame_from_camera(C.byref(cam), C.byref(f)), "frame")
+    return f
+
+
+def test_async_lists_new_cameras(gpu):
+    """New cameras of the same size build their lists without a read-back,
+    sized from the last build + headroom (rt_lists.cpp cand_prepare: the
+    estimated shape, the kept count of the last frame, buffers grown with
+    headroom so the build never frees mid-frame): a panned sequence on one
+    context equals, frame by frame, the read-back build of a fresh context
+    for the same camera -- image bit for bit and counts.  A jump far past the
+    estimate is reported (RT_EHITBUF: the frame's lists outgrew their
+    buffers) and the frame rendered again equals the reference, never an
+    incomplete image returned as complete."""
+    s = gpu.Scene.synthetic(6, 6, 9776, seed=0x5EED, width=960, height=540)
+    ctx = gpu.Context(s, "octree_gpu")
+    ctx.render_image(s.frame())  # the first frame of the size: read-back build
+    for k, du in enumerate((0.02, 0.05, 0.09, 0.14, 3.0)):
+        f = _panned_frame(gpu, s, du)
+        ref, st_ref = gpu.Context(s, "octree_gpu").render_image(f)
+        try:
+            img, st = ctx.render_image(f)
+        except gpu.RtError as e:
+            assert e.code == -10 and k == 4, (k, e.code)  # only the far jump may outgrow the estimate
+            img, st = ctx.render_image(f)
+        assert_bitexact(img, ref, f"camera {k} (pan {du}): asynchronous lists of a new camera")
+        assert (st["closest"], st["shadow"], st["cand_entries"]) == \
+            (st_ref["closest"], st_ref["shadow"], st_ref["cand_entries"])
+
+
 def test_triangle_parallel_lists_two_processes(gpu):
     """Two processes (ranks of torch.distributed.run, both on GPU 0, gloo
     for the exchange since RCCL needs a device per rank): each produces its
