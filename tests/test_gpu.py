@@ -1194,3 +1194,39 @@ def test_camera_refine_on_off(gpu, accel):
             v = ctx.cand_verify(f, rank, nranks)
             assert v["fp_mismatch"] == 0 and v["tile_mismatch"] == 0, (on, nranks, rank, v)
             assert v["filter_violation"] == 0, (on, nranks, rank, v)
+
+
+def test_bench_json_contract(gpu, tmp_path):
+    """bench.py as the driver runs it (one GPU, a small workload, a short CPU
+    baseline): one JSON line on stdout with the contract's fields -- the
+    metric and unit, whole-job value, per-step times (replay and fresh
+    camera), the roofline object of the dominant kernel and the CPU baseline
+    whose sampled pixels match the GPU image bit for bit."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--workload", "c1", "--steps", "3",
+                        "--warmup", "1", "--cpu-seconds", "2", "--cpu-threads", "2"],
+                       capture_output=True, text=True, timeout=240, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "ms_per_step_fresh",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["metric"] == "Mrays/sec (primary+shadow) at 3840x2160" and d["unit"] == "Mrays/s"
+    assert d["n_gpus"] == 1 and d["steps"] == 3 and d["warmup"] == 1 and d["higher_is_better"] is True
+    assert d["value"] > 0 and d["ms_per_step"] > 0 and d["ms_per_step_fresh"] > 0
+    assert "workload" in d["config"]
+    rf = d["roofline"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in rf, k
+    assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and 0 < rf["frac"] < 1
+    assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
+    cpu = d["cpu_baseline"]
+    for k in ("value", "unit", "cores", "kind", "sample"):
+        assert k in cpu, k
+    assert cpu["kind"] == "port" and cpu["cores"] == 2 and cpu["value"] > 0
+    assert cpu["sample_pixels_bitexact_vs_gpu"] is True
